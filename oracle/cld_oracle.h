@@ -1,0 +1,51 @@
+/* cld_oracle.h -- TEST INFRASTRUCTURE ONLY (see cld_oracle.c header). */
+#ifndef CLD_ORACLE_H_
+#define CLD_ORACLE_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Mirrors DetectLanguageSummaryV2's outputs (compact_lang_det_impl.cc:1707-1720) */
+typedef struct {
+  uint16_t lang3[3];
+  uint16_t summary_lang;
+  int32_t percent3[3];
+  int32_t reliable_percent3[3];
+  double normalized3[3];
+  int32_t text_bytes;
+  uint8_t is_reliable;
+  uint8_t passes;
+  uint8_t pad[2];
+} cldo_result;
+
+typedef struct {   /* ChunkSummary, scoreonescriptspan.h:240-252 */
+  uint16_t offset, chunk_start, lang1, lang2, score1, score2, bytes, grams, ulscript;
+  uint8_t rel_delta, rel_score;
+} cldo_chunk;
+
+typedef struct cldo_ctx cldo_ctx;
+typedef void (*cldo_trace_fn)(void* arg, const char* line);
+
+int cldo_load(const char* cldt_path);
+cldo_ctx* cldo_ctx_new(void);
+void cldo_ctx_free(cldo_ctx* c);
+void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg);
+int cldo_detect(cldo_ctx* c, const char* text, int len, cldo_result* r);
+const char* cldo_detect_language(cldo_ctx* c, const char* text);
+int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_result* out, int threads);
+const char* cldo_language_code(int lang);
+const char* cldo_language_name(int lang);
+int cldo_meta(int which);
+int cldo_score_linear(int ulscript, int score_cjk, int next_base, const uint16_t* offsets,
+                      const uint8_t* types, const uint32_t* langprobs, int n_linear,
+                      int dummy_offset, uint32_t* ring, cldo_chunk* out, int max_out);
+
+int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* types,
+                      const uint32_t* langprobs, int n_linear, const int* chunk_starts,
+                      int n_chunks, uint32_t* ring, cldo_chunk* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,124 @@
+"""ctypes binding of the C oracle -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker, never as the thing measured or shipped.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libcld_oracle.so")
+DEFAULT_TABLES = os.path.join(os.path.dirname(HERE), "language-detector_amd", "data", "cld2_mi355x.cldt")
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("lang3", ctypes.c_uint16 * 3), ("summary_lang", ctypes.c_uint16),
+                ("percent3", ctypes.c_int32 * 3), ("reliable_percent3", ctypes.c_int32 * 3),
+                ("normalized3", ctypes.c_double * 3), ("text_bytes", ctypes.c_int32),
+                ("is_reliable", ctypes.c_uint8), ("passes", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 2)]
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint16) for n in
+                ("offset", "chunk_start", "lang1", "lang2", "score1", "score2", "bytes", "grams", "ulscript")] + \
+               [("rel_delta", ctypes.c_uint8), ("rel_score", ctypes.c_uint8)]
+
+
+RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "<i4", 3),
+                         ("reliable_percent3", "<i4", 3), ("normalized3", "<f8", 3),
+                         ("text_bytes", "<i4"), ("is_reliable", "u1"), ("passes", "u1"), ("pad", "u1", 2)])
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(Result)
+
+TRACE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+class Oracle:
+    def __init__(self, tables=DEFAULT_TABLES):
+        if not os.path.exists(LIB):
+            build()
+        self.lib = lib = ctypes.CDLL(LIB)
+        lib.cldo_load.argtypes = [ctypes.c_char_p]
+        lib.cldo_ctx_new.restype = ctypes.c_void_p
+        lib.cldo_ctx_free.argtypes = [ctypes.c_void_p]
+        lib.cldo_set_trace.argtypes = [ctypes.c_void_p, TRACE_FN, ctypes.c_void_p]
+        lib.cldo_detect.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(Result)]
+        lib.cldo_detect_language.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        lib.cldo_detect_language.restype = ctypes.c_char_p
+        lib.cldo_detect_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        lib.cldo_language_code.restype = ctypes.c_char_p
+        lib.cldo_language_name.restype = ctypes.c_char_p
+        lib.cldo_score_linear.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        lib.cldo_score_chunks.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p]
+        rc = lib.cldo_load(tables.encode())
+        if rc != 0:
+            raise RuntimeError("cldo_load(%s) = %d" % (tables, rc))
+        self.ctx = lib.cldo_ctx_new()
+        self.unknown = lib.cldo_meta(1)
+        self.english = lib.cldo_meta(2)
+
+    def code(self, lang):
+        return self.lib.cldo_language_code(int(lang)).decode()
+
+    def name(self, lang):
+        return self.lib.cldo_language_name(int(lang)).decode()
+
+    def detect(self, text, trace=False):
+        """DetectLanguageSummaryV2 -> (summary_lang, Result[, trace lines])."""
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        lines = []
+        if trace:
+            cb = TRACE_FN(lambda _a, s: lines.append(s.decode("utf-8", "replace")))
+            self.lib.cldo_set_trace(self.ctx, cb, None)
+        r = Result()
+        lang = self.lib.cldo_detect(self.ctx, b, len(b), ctypes.byref(r))
+        if trace:
+            self.lib.cldo_set_trace(self.ctx, TRACE_FN(0), None)
+            return lang, r, lines
+        return lang, r
+
+    def detect_language(self, text):
+        """wrapper.cc:7-16 semantics: strlen, UNKNOWN -> 'en'."""
+        b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+        return self.lib.cldo_detect_language(self.ctx, b).decode()
+
+    def detect_batch(self, buf, offsets, threads=1):
+        buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        rc = self.lib.cldo_detect_batch(buf.ctypes.data, offsets.ctypes.data, n, out.ctypes.data, threads)
+        if rc != 0:
+            raise RuntimeError("cldo_detect_batch rc=%d" % rc)
+        return out
+
+    def score_linear(self, ulscript, score_cjk, next_base, offsets, types, langprobs, dummy_offset, ring=None):
+        n = len(offsets)
+        o = np.asarray(offsets, dtype=np.uint16); t = np.asarray(types, dtype=np.uint8)
+        lp = np.asarray(langprobs, dtype=np.uint32)
+        ring_arr = np.zeros(5, dtype=np.uint32) if ring is None else np.asarray(ring, dtype=np.uint32).copy()
+        out = (Chunk * 64)()
+        k = self.lib.cldo_score_linear(ulscript, int(score_cjk), next_base, o.ctypes.data, t.ctypes.data,
+                                       lp.ctypes.data, n, dummy_offset, ring_arr.ctypes.data, out, 64)
+        return [out[i] for i in range(k)], ring_arr
+
+    def score_chunks(self, ulscript, offsets, types, langprobs, chunk_starts, ring=None):
+        o = np.asarray(offsets, dtype=np.uint16); t = np.asarray(types, dtype=np.uint8)
+        lp = np.asarray(langprobs, dtype=np.uint32); cs = np.asarray(chunk_starts, dtype=np.int32)
+        ring_arr = np.zeros(5, dtype=np.uint32) if ring is None else np.asarray(ring, dtype=np.uint32).copy()
+        out = (Chunk * 64)()
+        k = self.lib.cldo_score_chunks(ulscript, o.ctypes.data, t.ctypes.data, lp.ctypes.data, len(o),
+                                       cs.ctypes.data, len(cs) - 1, ring_arr.ctypes.data, out)
+        if k < 0:
+            raise ValueError("cldo_score_chunks rc=%d" % k)
+        return [out[i] for i in range(k)], ring_arr

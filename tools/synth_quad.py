@@ -1,0 +1,196 @@
+"""Build the synthetic quadgram tables (Q1) and the per-language vocabularies.
+
+The reference's production quadgram table (cld2_generated_quadchrome_2.cc) is
+a missing blob (/root/reference/.MISSING_LARGE_BLOBS:5), so no real CLD2 quad
+data exists in this environment.  This tool derives a deterministic stand-in
+*table* (data, not code) from the reference's own octagram training tokens:
+
+  * every bucket of cld2_generated_deltaoctachrome.cc / _distinctoctachrome.cc
+    carries its source token in a comment ("_word_" = whole word); the token's
+    language is the top language of the bucket entry's indirect langprob;
+  * each whole word is broken into the quadgram chain GetQuadHits would walk
+    (cldutil.cc:338-392), hashed with QuadHashV2 (cldutil_shared.cc:196), and
+    every quad accumulates a per-language count;
+  * quads are packed into CLD2TableSummary 4-way buckets exactly as the real
+    table format requires (cld2tablesummary.h:29-49): 16-bit key in the high
+    half, 16-bit indirect in the low half; overflow goes to the dual table
+    (quadgram_obj2, the 0x80000000 indirect flag path, cldutil.cc:356-363);
+    quads seen in >3 languages use two langprobs (the kCLDTableSizeOne split,
+    scoreonescriptspan.cc:938-964).
+
+Outputs (all deterministic):
+  language-detector_amd/data/cld2_mi355x.cldt   base blob + QUAD/QUAD2 + provenance
+  language-detector_amd/data/vocab.json         {lang_code: [words...]} for synthetic text
+"""
+import json
+import os
+import re
+import struct
+import sys
+from collections import defaultdict
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import cldt  # noqa: E402
+
+REF = "/root/reference/cld2/internal"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+QUAD1_BUCKETS = 16384          # 256 KB of buckets; ~90% load -> real dual-table traffic
+QUAD2_BUCKETS = 8192
+KEYMASK = 0xFFFF0000
+
+
+def parse_token_table(path):
+    """Yield (keyvalue, token) for every non-empty slot of a generated octa table."""
+    txt = open(path, encoding="utf-8").read()
+    start = txt.index("hash_indirect[4], tokens[4]")
+    for line in txt[start:].splitlines():
+        m = re.match(r"\s*\{\{(0x[0-9a-f]+),(0x[0-9a-f]+),(0x[0-9a-f]+),(0x[0-9a-f]+)\}\},\s*//\s*(?:\[\d+\])?\s*(.*)$", line)
+        if not m:
+            if line.strip().startswith("};"):
+                break
+            continue
+        kvs = [int(m.group(i), 16) for i in range(1, 5)]
+        toks = [t.strip() for t in m.group(5).split(", ")]
+        for kv, tok in zip(kvs, toks):
+            if kv and tok and tok != "--":
+                yield kv, tok
+
+
+def main():
+    base = cldt.Blob.load(os.path.join(ROOT, "oracle/_ref/cld2_base.cldt"))
+    prop = base.script_prop()
+    lang_to_plang = base.u8(cldt.LANG_TO_PLANG)
+    p2l_latn = base.u16(cldt.PLANG_TO_LANG_LATN)
+    p2l_othr = base.u16(cldt.PLANG_TO_LANG_OTHR)
+    codes = base.strings(cldt.LANG_CODES)
+    rtype = base.u8(cldt.ULSCRIPT_RTYPE)
+    lgprob = base.u8(cldt.LGPROB).reshape(240, 8)
+    latin = base.meta["ulscript_latin"]
+
+    vocab = defaultdict(set)         # lang -> words
+    for fname, sid in (("cld2_generated_deltaoctachrome.cc", cldt.DELTA_OCTA),
+                       ("cld2_generated_distinctoctachrome.cc", cldt.DISTINCT_OCTA)):
+        tbl = base.table(sid)
+        for kv, tok in parse_token_table(os.path.join(REF, fname)):
+            if not (tok.startswith("_") and tok.endswith("_")) or "__" in tok or len(tok) < 4:
+                continue          # keep whole single words only
+            word = tok[1:-1].encode("utf-8")
+            ind = kv & ~tbl["key_mask"] & 0xFFFFFFFF
+            if ind >= len(tbl["ind"]):
+                continue
+            lp = int(tbl["ind"][ind])
+            ps = (lp >> 8) & 0xFF
+            if ps == 0:
+                continue
+            sc = cldt.script_num(prop, word, 0)
+            if sc == 0 or rtype[sc] != 2:       # RTypeMany scripts only
+                continue
+            lang = int(p2l_latn[ps] if sc == latin else p2l_othr[ps])
+            vocab[lang].add(word)
+
+    # Per-quad language counts, weighted 1/|vocab(lang)| so big vocabularies don't dominate.
+    counts = defaultdict(lambda: defaultdict(float))
+    for lang, words in vocab.items():
+        w = 1.0 / max(1, len(words))
+        for word in words:
+            for _, _, h in cldt.word_quads(word):
+                counts[h][lang] += w
+
+    def qprobs(langs):
+        tot = sum(c for _, c in langs)
+        return [max(1, min(12, int(round(3 + 9 * (c / tot))))) for _, c in langs]
+
+    def best_entry(q):
+        q = list(q) + [0] * (3 - len(q))
+        err = ((lgprob[:, 5:8].astype(int) - np.array(q)) ** 2)
+        # unused slots (q=0) must not constrain
+        err[:, [i for i in range(3) if q[i] == 0]] = 0
+        return int(np.argmin(err.sum(1)))
+
+    def make_langprob(langs):
+        q = qprobs(langs)
+        lp = best_entry(q)
+        for k, (lang, _) in enumerate(langs[:3]):
+            lp |= int(lang_to_plang[lang] if lang < len(lang_to_plang) else 0) << (8 * (k + 1))
+        return lp
+
+    singles, doubles = [], []          # (hash, langprob) / (hash, lp1, lp2)
+    for h in sorted(counts):
+        langs = sorted(counts[h].items(), key=lambda kv: (-kv[1], kv[0]))[:6]
+        if len(langs) <= 3:
+            singles.append((h, make_langprob(langs)))
+        else:
+            doubles.append((h, make_langprob(langs[:3]), make_langprob(langs[3:6])))
+
+    # Indirect layout: [0] reserved 0, singles [1..size_one), then pairs.
+    ind = [0]
+    entries = []                        # (hash, indirect)
+    for h, lp in singles:
+        entries.append((h, len(ind)))
+        ind.append(lp)
+    size_one = len(ind)
+    for h, lp1, lp2 in doubles:
+        entries.append((h, size_one + (len(ind) - size_one) // 2))
+        ind += [lp1, lp2]
+    assert len(ind) < 65536, len(ind)
+
+    # Deterministic insertion order (by hash) into table 1, overflow to table 2.
+    def place(entries, nbuckets):
+        b = np.zeros((nbuckets, 4), dtype=np.uint32)
+        fill = np.zeros(nbuckets, dtype=np.int32)
+        spill = []
+        for h, i in entries:
+            sub = (h + (h >> 12)) & (nbuckets - 1)
+            key = h & KEYMASK
+            # a key already present would shadow this entry; treat as spill
+            if any(((key ^ int(b[sub, k])) & KEYMASK) == 0 and b[sub, k] for k in range(fill[sub])):
+                spill.append((h, i)); continue
+            if fill[sub] < 4:
+                b[sub, fill[sub]] = key | i
+                fill[sub] += 1
+            else:
+                spill.append((h, i))
+        return b, spill
+
+    b1, spill = place(entries, QUAD1_BUCKETS)
+    b2, dropped = place(spill, QUAD2_BUCKETS)
+
+    prov = ("CLD2 chrome tables extracted from /root/reference/cld2/internal "
+            "(compile_libs.sh:30-40 set) by oracle/tablegen/extract_cld2_tables.cc; "
+            "QUAD/QUAD2 = SYNTHETIC Q1 built by tools/synth_quad.py from the octa-table "
+            "training tokens (%d langs, %d words, %d quads: %d single, %d double; "
+            "table1 %d buckets, table2 %d buckets, %d spilled, %d dropped). "
+            "Real quadchrome_2 is a missing blob." % (
+                len(vocab), sum(len(v) for v in vocab.values()), len(entries),
+                len(singles), len(doubles), QUAD1_BUCKETS, QUAD2_BUCKETS, len(spill), len(dropped)))
+
+    sections = []
+    for sid in sorted(base.sections):
+        sections.append((sid, base.raw(sid)))
+    sections.append((cldt.QUAD, cldt.table_section_bytes(size_one, QUAD1_BUCKETS, KEYMASK, 20261015, b1, ind)))
+    sections.append((cldt.QUAD2, cldt.table_section_bytes(size_one, QUAD2_BUCKETS, KEYMASK, 20261015, b2, ind)))
+    sections.append((cldt.PROVENANCE, prov.encode()))
+    sections.sort(key=lambda s: s[0])
+    out = os.path.join(ROOT, "language-detector_amd/data/cld2_mi355x.cldt")
+    cldt.write_blob(out, sections)
+
+    # Q0: the reference's own empty-table pattern (generated_distinct_bi_0.cc:22-48)
+    empty = cldt.table_section_bytes(1, 1, 0xFFFFFFFF, 20130101, np.zeros((1, 4)), [0])
+    empty2 = cldt.table_section_bytes(1, 0, 0xFFFFFFFF, 20130101, np.zeros((1, 4)), [0])
+    s0 = [(sid, p) for sid, p in sections if sid not in (cldt.QUAD, cldt.QUAD2, cldt.PROVENANCE)]
+    s0 += [(cldt.QUAD, empty), (cldt.QUAD2, empty2),
+           (cldt.PROVENANCE, b"Q0: empty quad table (reference placeholder pattern)")]
+    s0.sort(key=lambda s: s[0])
+    cldt.write_blob(os.path.join(ROOT, "language-detector_amd/data/cld2_q0.cldt"), s0)
+
+    vj = {codes[l]: sorted(w.decode("utf-8") for w in ws) for l, ws in sorted(vocab.items())}
+    with open(os.path.join(ROOT, "language-detector_amd/data/vocab.json"), "w", encoding="utf-8") as f:
+        json.dump(vj, f, ensure_ascii=False, indent=0, sort_keys=True)
+    print(prov)
+
+
+if __name__ == "__main__":
+    main()
