@@ -1,0 +1,133 @@
+"""Python host binding of libcld_mi355x.so (the C ABI in include/cld_mi355x.h).
+
+Mirrors the reference's caller-facing interface for this path:
+  detect_language(text) -> ISO code       main.go:77-81 Detect_language / wrapper.cc:7-16
+  detect_batch(docs)    -> cld_result[]   one DetectLanguageSummaryV2 per document
+  strip_extras(text)                      handlers.go:198-210 StripExtras (the caller-side
+                                          preprocessing the HTTP handler applies first)
+There is no CPU fallback: if the HIP library or a GPU is missing, calls raise.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libcld_mi355x.so")
+TABLES = os.path.join(HERE, "data", "cld2_mi355x.cldt")
+
+RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "i1", 3),
+                         ("is_reliable", "u1"), ("text_bytes", "<i4"), ("normalized3", "<f8", 3)])
+assert RESULT_DTYPE.itemsize == 40
+
+# Every symbol include/cld_mi355x.h declares (checked by tests/test_capi.py)
+EXPORTS = ("detect_language", "cld_init", "cld_shutdown", "cld_detect_batch", "cld_detect_batch_device",
+           "cld_language_code", "cld_language_name", "cld_last_batch_stats", "cld_version")
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("docs", ctypes.c_uint64), ("short_docs", ctypes.c_uint64), ("general_docs", ctypes.c_uint64),
+                ("passes", ctypes.c_uint64 * 4), ("short_ms", ctypes.c_double), ("general_ms", ctypes.c_double)]
+
+
+class CldError(RuntimeError):
+    pass
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree HIP library (never a fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CldError("libcld_mi355x.so is not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.detect_language.argtypes = [ctypes.c_char_p]
+        L.detect_language.restype = ctypes.c_char_p
+        L.cld_init.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.cld_detect_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32]
+        L.cld_detect_batch_device.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_void_p]
+        L.cld_language_code.restype = ctypes.c_char_p
+        L.cld_language_name.restype = ctypes.c_char_p
+        L.cld_version.restype = ctypes.c_char_p
+        L.cld_last_batch_stats.argtypes = [ctypes.c_int, ctypes.POINTER(BatchStats)]
+        _lib = L
+    return _lib
+
+
+def init(tables=None, n_devices=0):
+    rc = lib().cld_init(tables.encode() if tables else None, n_devices)
+    if rc != 0:
+        raise CldError("cld_init failed: %d" % rc)
+
+
+def pack(docs):
+    """list of str/bytes -> (uint8 buffer, uint64 offsets[n+1])."""
+    bs = [d.encode("utf-8") if isinstance(d, str) else bytes(d) for d in docs]
+    offs = np.zeros(len(bs) + 1, dtype=np.uint64)
+    np.cumsum([len(b) for b in bs], out=offs[1:])
+    buf = np.frombuffer(b"".join(bs), dtype=np.uint8) if bs else np.zeros(0, np.uint8)
+    return buf, offs
+
+
+def detect_batch(docs=None, buf=None, offsets=None):
+    if docs is not None:
+        buf, offsets = pack(docs)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    if n == 0:
+        return out
+    bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+    rc = lib().cld_detect_batch(bptr, offsets.ctypes.data, n, out.ctypes.data, 0)
+    if rc != 0:
+        raise CldError("cld_detect_batch failed: %d" % rc)
+    return out
+
+
+def detect_batch_device(device, d_buf_ptr, d_offsets_ptr, n, d_out_ptr, stream_ptr=None):
+    rc = lib().cld_detect_batch_device(device, d_buf_ptr, d_offsets_ptr, n, d_out_ptr, stream_ptr)
+    if rc != 0:
+        raise CldError("cld_detect_batch_device failed: %d" % rc)
+
+
+def last_stats(device=0):
+    st = BatchStats()
+    rc = lib().cld_last_batch_stats(device, ctypes.byref(st))
+    if rc != 0:
+        raise CldError("cld_last_batch_stats failed: %d" % rc)
+    return st
+
+
+def detect_language(text):
+    """main.go:77-81 / wrapper.cc:7-16: NUL-terminated text -> ISO code ('en' for unknown)."""
+    b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+    return lib().detect_language(b).decode()
+
+
+def language_code(lang):
+    return lib().cld_language_code(int(lang)).decode()
+
+
+def language_name(lang):
+    return lib().cld_language_name(int(lang)).decode()
+
+
+def strip_extras(text):
+    """handlers.go:198-210: drop words starting with '@' or 'http', rejoin with
+    a trailing space after every kept word (strings.Fields semantics)."""
+    out = []
+    for w in text.split():
+        if w.startswith("@") or w.startswith("http"):
+            continue
+        out.append(w + " ")
+    return "".join(out)

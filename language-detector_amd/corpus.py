@@ -1,0 +1,205 @@
+"""Deterministic synthetic corpora for the BASELINE.json configurations.
+
+Word vocabularies (data/vocab.json) are the whole-word training tokens of the
+reference's octagram tables (see tools/synth_quad.py); CJK character pools
+(data/cjk_charsets.json) are the characters of the reference unit-test CJK
+documents (unittest_data.h kTeststr_{zh_Hans,zh_Hant,ja_Hani,ko_Hani}).
+
+  c2  n x U[100,180] B tweets, >= 10 Latin-script languages, 10% capitalised
+      words, 5% digit/punctuation tokens                       
+  c3  n x 16384 B pages: four ~4 KB paragraphs in Latin / Cyrillic / Arabic /
+      Devanagari languages in random order                      
+  c4  n x ~150 B zh-Hans/zh-Hant/ja/ko documents                
+  c5  lognormal lengths (median 140 B, cap 64 KB) mixing c2..c4
+
+All generators are vectorised numpy and return (buf uint8[], offsets uint64[n+1]).
+"""
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEEDS = {"c2": 0xC1D20002, "c3": 0xC1D20003, "c4": 0xC1D20004, "c5": 0xC1D20005}
+
+C2_LANGS = ["en", "fr", "de", "es", "it", "pt", "nl", "sv", "da", "no", "fi", "pl", "cs", "ro", "hu", "tr"]
+C3_SCRIPTS = {
+    "Latn": ["en", "fr", "de", "es", "it", "pt", "nl", "pl", "cs", "sv"],
+    "Cyrl": ["ru", "uk", "bg", "sr", "mk", "kk"],
+    "Arab": ["ar", "fa", "ur"],
+    "Deva": ["hi", "mr", "ne"],
+}
+PUNCT_TOKENS = ["2013", "12", "3.5", "(c)", "--", "1998", "#1", "100%", "...", "!", "?", "&", ":)", "9:30", "2,000"]
+
+_vocab = None
+
+
+def vocab():
+    global _vocab
+    if _vocab is None:
+        with open(os.path.join(HERE, "data", "vocab.json"), encoding="utf-8") as f:
+            _vocab = {k: [w.encode("utf-8") for w in v] for k, v in json.load(f).items()}
+    return _vocab
+
+
+class WordTable:
+    """Concatenated 'word ' entries of several languages for vectorised assembly."""
+
+    def __init__(self, lang_words):
+        self.langs = list(lang_words)
+        entries, self.lo, self.cnt = [], [], []
+        for lang in self.langs:
+            ws = lang_words[lang]
+            self.lo.append(len(entries))
+            self.cnt.append(len(ws))
+            entries += [w + b" " for w in ws]
+        self.punct_lo = len(entries)
+        entries += [p.encode() + b" " for p in PUNCT_TOKENS]
+        self.punct_cnt = len(PUNCT_TOKENS)
+        self.lens = np.array([len(e) for e in entries], dtype=np.int64)
+        self.starts = np.zeros(len(entries), dtype=np.int64)
+        np.cumsum(self.lens[:-1], out=self.starts[1:])
+        self.bytes = np.frombuffer(b"".join(entries), dtype=np.uint8)
+        self.lo = np.array(self.lo, dtype=np.int64)
+        self.cnt = np.array(self.cnt, dtype=np.int64)
+        first = self.bytes[self.starts]
+        self.capitalisable = (first >= ord("a")) & (first <= ord("z"))
+
+
+def _assemble(rng, table, lang_idx, targets, kmax, cap_frac=0.10, punct_frac=0.05, pad_to=None):
+    """Per document: words of its language until the next word would pass
+    target bytes (at least one word).  Returns per-document byte arrays packed."""
+    n = len(lang_idx)
+    u = rng.random((n, kmax), dtype=np.float32)
+    widx = table.lo[lang_idx][:, None] + np.minimum((u * table.cnt[lang_idx][:, None]).astype(np.int64),
+                                                    table.cnt[lang_idx][:, None] - 1)
+    if punct_frac:
+        p = rng.random((n, kmax), dtype=np.float32) < punct_frac
+        pi = rng.integers(0, table.punct_cnt, size=(n, kmax))
+        widx = np.where(p, table.punct_lo + pi, widx)
+    wl = table.lens[widx]
+    cum = np.cumsum(wl, axis=1)
+    m = np.maximum(1, (cum <= targets[:, None]).sum(axis=1))
+    keep = np.arange(kmax)[None, :] < m[:, None]
+    sel = widx[keep]                                   # row-major: doc order, word order
+    seg = table.lens[sel]
+    doc_bytes = cum[np.arange(n), m - 1]
+    total = int(seg.sum())
+    seg_start = np.zeros(len(sel), dtype=np.int64)
+    np.cumsum(seg[:-1], out=seg_start[1:])
+    src = np.repeat(table.starts[sel] - seg_start, seg) + np.arange(total, dtype=np.int64)
+    out = table.bytes[src].copy()
+    if cap_frac:
+        c = (rng.random(len(sel), dtype=np.float32) < cap_frac) & table.capitalisable[sel]
+        out[seg_start[c]] -= 32
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(doc_bytes, out=offs[1:])
+    if pad_to is not None:                             # pad every document with spaces to pad_to bytes
+        padded = np.full(n * pad_to, ord(" "), dtype=np.uint8)
+        dst = np.repeat(np.arange(n, dtype=np.int64) * pad_to - offs[:-1].astype(np.int64), doc_bytes) + \
+            np.arange(total, dtype=np.int64)
+        padded[dst] = out
+        return padded, np.arange(n + 1, dtype=np.uint64) * pad_to
+    return out, offs
+
+
+def c2(n, seed=SEEDS["c2"]):
+    rng = np.random.default_rng(seed)
+    v = vocab()
+    table = WordTable({l: v[l] for l in C2_LANGS if l in v})
+    lang_idx = rng.integers(0, len(table.langs), size=n)
+    targets = rng.integers(100, 181, size=n)
+    return _assemble(rng, table, lang_idx, targets, kmax=48)
+
+
+def c3(n, seed=SEEDS["c3"], page=16384):
+    """Four paragraphs per page, one per script (random order, random language
+    of that script), each ~page/4 bytes; pages padded with spaces to `page`."""
+    rng = np.random.default_rng(seed)
+    v = vocab()
+    scripts = list(C3_SCRIPTS)
+    tables = {s: WordTable({l: v[l] for l in C3_SCRIPTS[s] if l in v}) for s in scripts}
+    para = page // 4 - 8
+    order = np.argsort(rng.random((n, 4)), axis=1)     # script order per page
+    parts = []
+    for k in range(4):
+        bufs = []
+        for si, s in enumerate(scripts):
+            rows = np.nonzero(order[:, k] == si)[0]
+            t = tables[s]
+            li = rng.integers(0, len(t.langs), size=len(rows))
+            tg = rng.integers(para - 256, para + 1, size=len(rows))
+            b, o = _assemble(rng, t, li, tg, kmax=para // 3, punct_frac=0.02)
+            bufs.append((rows, b, o))
+        parts.append(bufs)
+    # stitch: page = para0 + para1 + para2 + para3, then pad
+    lens = np.zeros((n, 4), dtype=np.int64)
+    pieces = [[None] * 4 for _ in range(n)]
+    for k in range(4):
+        for rows, b, o in parts[k]:
+            ol = o.astype(np.int64)
+            lens[rows, k] = ol[1:] - ol[:-1]
+            for j, r in enumerate(rows):
+                pieces[r][k] = b[ol[j]:ol[j + 1]]
+    out = np.full(n * page, ord(" "), dtype=np.uint8)
+    for r in range(n):
+        doc = np.concatenate(pieces[r])[:page]
+        out[r * page:r * page + len(doc)] = doc
+    return out, np.arange(n + 1, dtype=np.uint64) * page
+
+
+_cjk = None
+
+
+def cjk_pools():
+    global _cjk
+    if _cjk is None:
+        with open(os.path.join(HERE, "data", "cjk_charsets.json"), encoding="utf-8") as f:
+            _cjk = {k: [c.encode("utf-8") for c in v] for k, v in json.load(f).items()}
+    return _cjk
+
+
+def c4(n, seed=SEEDS["c4"], lo=120, hi=180):
+    """CJK 'words' are runs of 2-6 characters from the language's pool."""
+    rng = np.random.default_rng(seed)
+    pools = cjk_pools()
+    words = {}
+    for lang, chars in pools.items():
+        r = np.random.default_rng(seed ^ sum(lang.encode()))
+        ws = set()
+        while len(ws) < 400:
+            k = int(r.integers(2, 7))
+            ws.add(b"".join(chars[int(i)] for i in r.integers(0, len(chars), size=k)))
+        words[lang] = sorted(ws)
+    table = WordTable(words)
+    lang_idx = rng.integers(0, len(table.langs), size=n)
+    targets = rng.integers(lo, hi + 1, size=n)
+    return _assemble(rng, table, lang_idx, targets, kmax=40, cap_frac=0.0, punct_frac=0.03)
+
+
+def c5(n, seed=SEEDS["c5"], cap=65536):
+    """Lognormal lengths (median 140 B, p99 ~16 KB): tweets from c2/c4 pools,
+    long documents from c3-style pages truncated to length."""
+    rng = np.random.default_rng(seed)
+    sigma = np.log(16384 / 140) / 2.326
+    lens = np.minimum(cap, np.maximum(8, np.exp(np.log(140) + sigma * rng.standard_normal(n)))).astype(np.int64)
+    short = lens <= 1024
+    docs = [None] * n
+    si = np.nonzero(short)[0]
+    li = np.nonzero(~short)[0]
+    b2, o2 = c2(len(si), seed=seed + 1)
+    o2 = o2.astype(np.int64)
+    for j, r in enumerate(si):
+        docs[r] = b2[o2[j]:o2[j + 1]][:lens[r]]
+    if len(li):
+        pages = max(1, int(np.ceil(lens[li].max() / 16384)))
+        b3, o3 = c3(len(li), seed=seed + 2, page=16384 * pages)
+        o3 = o3.astype(np.int64)
+        for j, r in enumerate(li):
+            docs[r] = b3[o3[j]:o3[j] + lens[r]]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(d) for d in docs], out=offs[1:])
+    return np.concatenate(docs) if n else np.zeros(0, np.uint8), offs
+
+
+GENERATORS = {"c2": c2, "c3": c3, "c4": c4, "c5": c5}

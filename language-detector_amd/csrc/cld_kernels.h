@@ -1,0 +1,30 @@
+// cld_kernels.h -- launch interface between the host runtime and the kernels.
+#ifndef CLD_KERNELS_H_
+#define CLD_KERNELS_H_
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "cld_device.h"
+
+// Short-document bucket: documents up to kShortCap bytes run one per lane with
+// private buffers sized for that length (span text <= 2*CAP).
+constexpr int kShortCap = 256;
+constexpr int kShortSB = 2 * kShortCap + 64;
+constexpr int kShortLB = kShortSB * 3 / 2 + 64;
+constexpr int kShortHB = kShortCap + 32;
+
+// Device counter slots (one 64-byte line, zeroed per batch)
+enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
+       kCtrSlots = 16 };
+
+extern "C" {
+size_t cld_general_work_bytes();
+size_t cld_short_work_bytes();
+hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
+                            hipStream_t s);
+hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
+                              const uint32_t* list, cld_result* out, uint8_t* arena,
+                              uint64_t stride, int lanes, uint32_t* counters, hipStream_t s);
+}
+#endif

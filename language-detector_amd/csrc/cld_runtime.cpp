@@ -1,0 +1,485 @@
+// cld_runtime.cpp -- host runtime behind the C ABI (include/cld_mi355x.h).
+//
+//  * loads the CLDT table blob once per process, uploads it once per GPU;
+//  * one context per GPU: stream, table copy, general-kernel arena, staging;
+//  * cld_detect_batch shards documents across GPUs by byte count (documents
+//    are independent: no collective on the hot path), one host thread per GPU;
+//  * detect_language() (wrapper.h:8) coalesces concurrent callers into GPU
+//    micro-batches.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cld_device.h"
+#include "cld_kernels.h"
+#include "cldt_format.h"
+
+namespace {
+
+#define HIP_OK(x)                                                           \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                 \
+      fprintf(stderr, "cld_mi355x: %s failed: %s (%s:%d)\n", #x,            \
+              hipGetErrorString(e_), __FILE__, __LINE__);                   \
+      return CLD_EIO;                                                       \
+    }                                                                       \
+  } while (0)
+
+// ------------------------------------------------------------ host tables
+struct HostTables {
+  std::vector<uint8_t> blob;
+  cldt_meta meta{};
+  std::vector<std::string> codes, names;
+  std::string version;
+  DevTables offs{};   // pointer fields hold byte offsets into blob
+};
+
+const uint8_t* section(const std::vector<uint8_t>& b, uint32_t id, uint64_t* off, uint64_t* size) {
+  const cldt_file_header* fh = (const cldt_file_header*)b.data();
+  const cldt_section* s = (const cldt_section*)(b.data() + fh->section_table_offset);
+  for (uint32_t i = 0; i < fh->n_sections; ++i)
+    if (s[i].id == id) {
+      if (off) *off = s[i].offset;
+      if (size) *size = s[i].size;
+      return b.data() + s[i].offset;
+    }
+  return nullptr;
+}
+
+template <class P>
+P at(uint64_t off) { return reinterpret_cast<P>((uintptr_t)off); }
+
+bool parse_sm(const std::vector<uint8_t>& b, uint32_t id, DevSM* sm) {
+  uint64_t off, size;
+  const uint8_t* p = section(b, id, &off, &size);
+  if (!p) return false;
+  const cldt_sm_header* h = (const cldt_sm_header*)p;
+  sm->state0 = h->state0; sm->state0_size = h->state0_size; sm->total = h->total_size;
+  sm->shift = h->entry_shift; sm->n_remap = h->n_remap; sm->n_rstr = h->n_remap_string;
+  uint64_t tbl = off + sizeof(cldt_sm_header);
+  if (h->bytes_per_entry == 2) {
+    sm->t16 = at<const uint16_t*>(tbl); sm->t8 = nullptr;
+  } else {
+    sm->t8 = at<const uint8_t*>(tbl); sm->t16 = nullptr;
+  }
+  uint64_t r = (sizeof(cldt_sm_header) + (uint64_t)h->total_size * h->bytes_per_entry + 15) & ~15ull;
+  sm->remap = at<const uint8_t*>(off + r);
+  sm->rstr = at<const uint8_t*>(off + r + 4ull * h->n_remap);
+  return true;
+}
+
+bool parse_tbl(const std::vector<uint8_t>& b, uint32_t id, DevTbl* t) {
+  uint64_t off;
+  const uint8_t* p = section(b, id, &off, nullptr);
+  if (!p) return false;
+  const cldt_table_header* h = (const cldt_table_header*)p;
+  t->size_one = h->size_one; t->size = h->size; t->key_mask = h->key_mask;
+  t->n_ind = h->n_ind; t->n_buckets = h->n_buckets_stored;
+  uint64_t bo = off + sizeof(cldt_table_header);
+  t->b = at<const uint32_t*>(bo);
+  t->ind = at<const uint32_t*>(bo + 16ull * h->n_buckets_stored);
+  // buckets are read as one 16-byte vector: they must be 16-byte aligned
+  return (bo % 16) == 0 && (h->size == 0 || (h->size & (h->size - 1)) == 0);
+}
+
+std::vector<std::string> strings(const std::vector<uint8_t>& b, uint32_t id) {
+  std::vector<std::string> out;
+  const uint8_t* p = section(b, id, nullptr, nullptr);
+  if (!p) return out;
+  uint32_t n = *(const uint32_t*)p;
+  const uint32_t* o = (const uint32_t*)(p + 4);
+  const char* base = (const char*)(p + 4 + 4 * (n + 1));
+  for (uint32_t i = 0; i < n; ++i) out.emplace_back(base + o[i]);
+  return out;
+}
+
+int load_tables(const char* path, HostTables* t) {
+  FILE* f = fopen(path, "rb");
+  if (!f) { fprintf(stderr, "cld_mi355x: cannot open tables %s\n", path); return CLD_EINVAL; }
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  t->blob.resize((size_t)n);
+  size_t got = fread(t->blob.data(), 1, (size_t)n, f);
+  fclose(f);
+  if (got != (size_t)n || n < (long)sizeof(cldt_file_header)) return CLD_EINVAL;
+  const cldt_file_header* fh = (const cldt_file_header*)t->blob.data();
+  if (fh->magic != CLDT_MAGIC || fh->version != CLDT_VERSION) return CLD_EINVAL;
+  const uint8_t* m = section(t->blob, CLDT_META, nullptr, nullptr);
+  if (!m) return CLD_EINVAL;
+  memcpy(&t->meta, m, sizeof(t->meta));
+  DevTables& D = t->offs;
+  bool ok = parse_sm(t->blob, CLDT_SCRIPT_PROP, &D.script) && parse_sm(t->blob, CLDT_LOWER_REPL, &D.lower) &&
+            parse_sm(t->blob, CLDT_SCAN_NOT, &D.scan) && parse_sm(t->blob, CLDT_CJK_UNI_PROP, &D.uni) &&
+            parse_tbl(t->blob, CLDT_CJK_COMPAT, &D.compat) && parse_tbl(t->blob, CLDT_DELTA_BI, &D.deltabi) &&
+            parse_tbl(t->blob, CLDT_DISTINCT_BI, &D.distinctbi) && parse_tbl(t->blob, CLDT_QUAD, &D.quad) &&
+            parse_tbl(t->blob, CLDT_QUAD2, &D.quad2) && parse_tbl(t->blob, CLDT_DELTA_OCTA, &D.deltaocta) &&
+            parse_tbl(t->blob, CLDT_DISTINCT_OCTA, &D.distinctocta);
+  if (!ok) return CLD_EINVAL;
+  uint64_t off, size;
+  struct { uint32_t id; const void** dst; uint32_t* count; uint32_t elem; } secs[] = {
+      {CLDT_EXPECTED_SCORE, (const void**)&D.expected, &D.n_expected, 2},
+      {CLDT_LGPROB, (const void**)&D.lgprob, nullptr, 1},
+      {CLDT_LANG_TO_PLANG, (const void**)&D.l2p, &D.l2p_size, 1},
+      {CLDT_PLANG_TO_LANG_LATN, (const void**)&D.p2l_latn, nullptr, 2},
+      {CLDT_PLANG_TO_LANG_OTHR, (const void**)&D.p2l_othr, nullptr, 2},
+      {CLDT_ULSCRIPT_RTYPE, (const void**)&D.rtype, &D.n_scripts, 1},
+      {CLDT_ULSCRIPT_DEFAULT_LANG, (const void**)&D.deflang, nullptr, 2},
+      {CLDT_CLOSEST_ALT, (const void**)&D.closest, &D.n_closest, 2},
+      {CLDT_CLOSE_SET, (const void**)&D.close_set, &D.n_langs, 1},
+  };
+  for (auto& s : secs) {
+    if (!section(t->blob, s.id, &off, &size)) return CLD_EINVAL;
+    *s.dst = at<const void*>(off);
+    if (s.count) *s.count = (uint32_t)(size / s.elem);
+  }
+  const cldt_meta& M = t->meta;
+  D.latin = M.ulscript_latin; D.cyrillic = M.ulscript_cyrillic; D.arabic = M.ulscript_arabic;
+  D.common = M.ulscript_common; D.inherited = M.ulscript_inherited;
+  D.unknown_lang = M.unknown_language; D.english = M.english; D.tg_unknown = M.tg_unknown_language;
+  D.french = M.french; D.italian = M.italian; D.german = M.german; D.spanish = M.spanish;
+  D.hawaiian = M.hawaiian;
+  t->codes = strings(t->blob, CLDT_LANG_CODES);
+  t->names = strings(t->blob, CLDT_LANG_NAMES);
+  const cldt_table_header* q = (const cldt_table_header*)section(t->blob, CLDT_QUAD, nullptr, nullptr);
+  t->version = "cld-mi355x 1.0 tables=" + std::string(path) + " quad_build=" + std::to_string(q->build_date);
+  return CLD_OK;
+}
+
+template <class P>
+P rebase(P off, const uint8_t* base) {
+  return reinterpret_cast<P>(const_cast<uint8_t*>(base) + (uintptr_t)off);
+}
+
+DevTables device_tables(const DevTables& o, const uint8_t* d) {
+  DevTables T = o;
+  auto sm = [&](DevSM& s) {
+    if (s.t8) s.t8 = rebase(s.t8, d);
+    if (s.t16) s.t16 = rebase(s.t16, d);
+    s.remap = rebase(s.remap, d); s.rstr = rebase(s.rstr, d);
+  };
+  sm(T.script); sm(T.lower); sm(T.scan); sm(T.uni);
+  for (DevTbl* t : {&T.compat, &T.deltabi, &T.distinctbi, &T.quad, &T.quad2, &T.deltaocta, &T.distinctocta}) {
+    t->b = rebase(t->b, d); t->ind = rebase(t->ind, d);
+  }
+  T.expected = rebase(T.expected, d); T.lgprob = rebase(T.lgprob, d); T.l2p = rebase(T.l2p, d);
+  T.p2l_latn = rebase(T.p2l_latn, d); T.p2l_othr = rebase(T.p2l_othr, d); T.rtype = rebase(T.rtype, d);
+  T.deflang = rebase(T.deflang, d); T.closest = rebase(T.closest, d); T.close_set = rebase(T.close_set, d);
+  return T;
+}
+
+// ------------------------------------------------------------ per-GPU context
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  uint8_t* d_blob = nullptr;
+  DevTables T{};
+  uint8_t* d_arena = nullptr;
+  uint64_t stride = 0;
+  int lanes = 0;
+  uint32_t* d_counters = nullptr;
+  uint32_t* d_requeue = nullptr;
+  size_t requeue_cap = 0;
+  uint8_t* d_buf = nullptr; size_t buf_cap = 0;
+  uint64_t* d_offs = nullptr; size_t offs_cap = 0;
+  cld_result* d_out = nullptr; size_t out_cap = 0;
+  hipEvent_t ev[3]{};
+  cld_batch_stats last{};
+  uint64_t last_n = 0;
+  bool stats_pending = false;
+  std::mutex mu;
+};
+
+std::mutex g_init_mu;
+bool g_inited = false;
+int g_init_rc = CLD_ENODEV;
+HostTables g_tab;
+std::vector<Device*> g_devs;
+
+std::string default_tables_path() {
+  if (const char* e = getenv("CLD_MI355X_TABLES")) return e;
+  Dl_info info;
+  if (dladdr((void*)&default_tables_path, &info) && info.dli_fname) {
+    std::string so = info.dli_fname;
+    std::string dir = so.substr(0, so.find_last_of('/'));
+    return dir + "/../data/cld2_mi355x.cldt";
+  }
+  return "language-detector_amd/data/cld2_mi355x.cldt";
+}
+
+template <class T>
+int grow(T** p, size_t* cap, size_t need) {
+  if (*cap >= need) return CLD_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  size_t n = std::max(need, *cap * 3 / 2);
+  if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) { *cap = 0; return CLD_ENOMEM; }
+  *cap = n;
+  return CLD_OK;
+}
+
+int init_device(Device* d) {
+  HIP_OK(hipSetDevice(d->id));
+  HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  HIP_OK(hipMalloc(&d->d_blob, g_tab.blob.size()));
+  HIP_OK(hipMemcpy(d->d_blob, g_tab.blob.data(), g_tab.blob.size(), hipMemcpyHostToDevice));
+  d->T = device_tables(g_tab.offs, d->d_blob);
+  HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, d->id));
+  d->stride = (cld_general_work_bytes() + 255) & ~(uint64_t)255;
+  int lanes = prop.multiProcessorCount * 64 * 2;
+  if (const char* e = getenv("CLD_GENERAL_LANES")) lanes = atoi(e);
+  lanes = std::max(64, (lanes / 64) * 64);
+  while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
+  d->lanes = lanes;
+  HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
+  for (auto& e : d->ev) HIP_OK(hipEventCreate(&e));
+  return CLD_OK;
+}
+
+// Enqueue the whole pipeline for n documents already on device d.
+int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s) {
+  if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
+  HIP_OK(hipEventRecord(d->ev[0], s));
+  HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
+  HIP_OK(hipEventRecord(d->ev[1], s));
+  HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
+                            d->d_counters, s));
+  HIP_OK(hipEventRecord(d->ev[2], s));
+  d->last_n = n;
+  d->stats_pending = true;
+  return CLD_OK;
+}
+
+int collect_stats(Device* d) {
+  if (!d->stats_pending) return CLD_OK;
+  uint32_t c[kCtrSlots];
+  HIP_OK(hipMemcpyAsync(c, d->d_counters, sizeof(c), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  float ms1 = 0, ms2 = 0;
+  (void)hipEventElapsedTime(&ms1, d->ev[0], d->ev[1]);
+  (void)hipEventElapsedTime(&ms2, d->ev[1], d->ev[2]);
+  cld_batch_stats& st = d->last;
+  memset(&st, 0, sizeof(st));
+  st.docs = d->last_n;
+  st.general_docs = c[kCtrRequeue];
+  st.short_docs = d->last_n - c[kCtrRequeue];
+  st.passes[0] = st.short_docs + c[kCtrPass1];
+  st.passes[1] = c[kCtrPass2];
+  st.passes[2] = c[kCtrPass3];
+  st.passes[3] = c[kCtrError];
+  st.short_ms = ms1;
+  st.general_ms = ms2;
+  d->stats_pending = false;
+  return c[kCtrError] ? CLD_EIO : CLD_OK;
+}
+
+// Host batch on one device: H2D, kernels, D2H.
+int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out) {
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  const uint64_t base = offs[0], bytes = offs[n] - offs[0];
+  if (grow(&d->d_buf, &d->buf_cap, std::max<size_t>(bytes, 1))) return CLD_ENOMEM;
+  if (grow(&d->d_offs, &d->offs_cap, n + 1)) return CLD_ENOMEM;
+  if (grow(&d->d_out, &d->out_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  std::vector<uint64_t> rel(n + 1);
+  for (size_t i = 0; i <= n; ++i) rel[i] = offs[i] - base;
+  if (bytes) HIP_OK(hipMemcpyAsync(d->d_buf, buf + base, bytes, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(d->d_offs, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
+  int rc = enqueue(d, d->d_buf, d->d_offs, n, d->d_out, d->stream);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(out, d->d_out, n * sizeof(cld_result), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  return collect_stats(d);
+}
+
+// ------------------------------------------------ detect_language batching
+struct Pending {
+  const char* text;
+  size_t len;
+  cld_result res;
+  bool done = false;
+};
+std::mutex g_q_mu;
+std::condition_variable g_q_cv;
+std::vector<Pending*> g_queue;
+bool g_dispatching = false;
+
+}  // namespace
+
+extern "C" {
+
+int cld_init(const char* tables_path, int n_devices) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_inited) return g_init_rc;
+  g_inited = true;
+  std::string path = tables_path ? tables_path : default_tables_path();
+  int rc = load_tables(path.c_str(), &g_tab);
+  if (rc) return g_init_rc = rc;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    fprintf(stderr, "cld_mi355x: no HIP device available\n");
+    return g_init_rc = CLD_ENODEV;
+  }
+  if (n_devices <= 0 || n_devices > count) n_devices = count;
+  if (const char* e = getenv("CLD_MI355X_DEVICES")) n_devices = std::max(1, std::min(count, atoi(e)));
+  for (int i = 0; i < n_devices; ++i) {
+    Device* d = new Device();
+    d->id = i;
+    if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
+    g_devs.push_back(d);
+  }
+  return g_init_rc = CLD_OK;
+}
+
+void cld_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  for (Device* d : g_devs) {
+    (void)hipSetDevice(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    (void)hipFree(d->d_blob); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
+    (void)hipFree(d->d_requeue); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
+    for (auto& e : d->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+  }
+  g_devs.clear();
+  g_inited = false;
+  g_init_rc = CLD_ENODEV;
+}
+
+int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_result* out, uint32_t flags) {
+  if (flags != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
+  if (n == 0) return CLD_OK;
+  if (n > 0x7FFFFFFFu) return CLD_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return CLD_EINVAL;
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  const size_t ndev = g_devs.size();
+  // Shard by byte count (+ a per-document weight) at document boundaries.
+  const uint64_t total = (offsets[n] - offsets[0]) + 64ull * n;
+  std::vector<size_t> cut(ndev + 1, 0);
+  cut[ndev] = n;
+  for (size_t k = 1; k < ndev; ++k) {
+    uint64_t target = total * k / ndev;
+    size_t lo = cut[k - 1], hi = n;
+    while (lo < hi) {
+      size_t mid = (lo + hi) / 2;
+      if ((offsets[mid] - offsets[0]) + 64ull * mid < target) lo = mid + 1; else hi = mid;
+    }
+    cut[k] = lo;
+  }
+  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out);
+  std::vector<int> rcs(ndev, CLD_OK);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < ndev; ++k) {
+    if (cut[k + 1] == cut[k]) continue;
+    th.emplace_back([&, k] { rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k]); });
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs) if (r) return r;
+  return CLD_OK;
+}
+
+int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,
+                            cld_result* d_out, void* stream) {
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  if (device < 0 || device >= (int)g_devs.size()) return CLD_EINVAL;
+  if (n == 0) return CLD_OK;
+  Device* d = g_devs[device];
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  return enqueue(d, d_buf, d_offsets, n, d_out, s);
+}
+
+int cld_last_batch_stats(int device, cld_batch_stats* st) {
+  if (device < 0 || device >= (int)g_devs.size() || !st) return CLD_EINVAL;
+  Device* d = g_devs[device];
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  int rc = collect_stats(d);
+  *st = d->last;
+  return rc;
+}
+
+const char* cld_language_code(int lang) {
+  if (cld_init(nullptr, 0) != CLD_OK && g_tab.codes.empty()) return "un";
+  if (lang < 0 || (size_t)lang >= g_tab.codes.size()) lang = (int)g_tab.meta.unknown_language;
+  return g_tab.codes[lang].c_str();
+}
+
+const char* cld_language_name(int lang) {
+  if (cld_init(nullptr, 0) != CLD_OK && g_tab.names.empty()) return "Unknown";
+  if (lang < 0 || (size_t)lang >= g_tab.names.size()) lang = (int)g_tab.meta.unknown_language;
+  return g_tab.names[lang].c_str();
+}
+
+const char* cld_version(void) {
+  cld_init(nullptr, 0);
+  return g_tab.version.c_str();
+}
+
+// wrapper.cc:7-16.  Concurrent callers are coalesced: the first caller to
+// find no dispatch in flight becomes the dispatcher and runs every queued
+// document as one batch; the others wait for their slot to be filled.
+const char* detect_language(const char* text) {
+  if (cld_init(nullptr, 0) != CLD_OK) {
+    fprintf(stderr, "cld_mi355x: detect_language: GPU runtime unavailable\n");
+    abort();   // no CPU fallback: fail loudly
+  }
+  Pending p;
+  p.text = text ? text : "";
+  p.len = strlen(p.text);
+  std::unique_lock<std::mutex> lk(g_q_mu);
+  g_queue.push_back(&p);
+  for (;;) {
+    if (p.done) break;
+    if (!g_dispatching) {
+      g_dispatching = true;
+      std::vector<Pending*> batch;
+      batch.swap(g_queue);
+      lk.unlock();
+      std::vector<uint64_t> offs(batch.size() + 1, 0);
+      std::string bytes;
+      for (size_t i = 0; i < batch.size(); ++i) {
+        bytes.append(batch[i]->text, batch[i]->len);
+        offs[i + 1] = bytes.size();
+      }
+      std::vector<cld_result> res(batch.size());
+      int rc = cld_detect_batch((const uint8_t*)bytes.data(), offs.data(), batch.size(), res.data(), 0);
+      if (rc != CLD_OK) {
+        fprintf(stderr, "cld_mi355x: detect_language batch failed (%d)\n", rc);
+        abort();
+      }
+      lk.lock();
+      for (size_t i = 0; i < batch.size(); ++i) { batch[i]->res = res[i]; batch[i]->done = true; }
+      g_dispatching = false;
+      g_q_cv.notify_all();
+      continue;
+    }
+    g_q_cv.wait(lk);
+  }
+  lk.unlock();
+  int lang = p.res.summary_lang;
+  if (lang == (int)g_tab.meta.unknown_language) lang = (int)g_tab.meta.english;  // compact_lang_det.cc:91-93
+  return cld_language_code(lang);
+}
+
+}  // extern "C"

@@ -382,6 +382,8 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen)
       uint8_t c = 0;
     do_state_table:
       tb = tb0;
+      e = 0;       /* utf8statetable.cc:645-649 re-declares e = 0 here */
+      c = 0;
     do_state_table_newe:
       while (src < srclimit) {
         c = *src;
@@ -1706,3 +1708,9 @@ int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* type
   if (ring) { ring[0] = (uint32_t)db->n; for (int k = 0; k < 4; ++k) ring[1 + k] = db->lp[k]; }
   return n_chunks;
 }
+
+/* Table-property probes used by tests (not part of the restated path). */
+int cldo_lower(const char* in, int len, char* out, int olen) {
+  return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen);
+}
+int cldo_script_num(const char* s) { return script_num((const uint8_t*)s); }

@@ -45,6 +45,9 @@ int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* type
                       const uint32_t* langprobs, int n_linear, const int* chunk_starts,
                       int n_chunks, uint32_t* ring, cldo_chunk* out);
 
+int cldo_lower(const char* in, int len, char* out, int olen);
+int cldo_script_num(const char* s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 QUAD1_BUCKETS = 16384          # 256 KB of buckets; ~90% load -> real dual-table traffic
 QUAD2_BUCKETS = 8192
 KEYMASK = 0xFFFF0000
+# Quantised log-probs: calibrated so per-KB chunk scores sit near the reference's
+# expected scores (kAvgDeltaOctaScore), which keeps ReliabilityExpected meaningful.
+QA, QB = float(os.environ.get("SYNQ_A", 0.5)), float(os.environ.get("SYNQ_B", 3))
 
 
 def parse_token_table(path):
@@ -101,7 +104,7 @@ def main():
 
     def qprobs(langs):
         tot = sum(c for _, c in langs)
-        return [max(1, min(12, int(round(3 + 9 * (c / tot))))) for _, c in langs]
+        return [max(1, min(12, int(round(QA + QB * (c / tot))))) for _, c in langs]
 
     def best_entry(q):
         q = list(q) + [0] * (3 - len(q))
