@@ -51,6 +51,19 @@ const char* detect_language(const char* text);
 int cld_init(const char* tables_path, int n_devices);
 void cld_shutdown(void);
 
+/* Initialise on exactly one GPU (HIP ordinal `device`); context index 0.
+ * One process per GPU (torch.distributed / bench.py) uses this. */
+int cld_init_device(const char* tables_path, int device);
+
+/* Byte-balanced document shards: cuts[0..nshards] (cuts[0]=0, cuts[nshards]=n)
+ * such that shard k = documents [cuts[k], cuts[k+1]).  Host-only helper used
+ * by cld_detect_batch's multi-GPU split and by multi-process callers. */
+int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts);
+
+/* Sum of kernel durations (HIP events on the stream the kernels ran on) of
+ * every batch enqueued on context `ctx` since the previous call; resets. */
+int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
+
 /* Batch detection.  Documents are [buf + offsets[i], buf + offsets[i+1]),
  * i < n (offsets has n+1 entries, non-decreasing).  Each document is scored
  * as if followed by NUL bytes, i.e. exactly like detect_language() on a

@@ -22,8 +22,9 @@ RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent
 assert RESULT_DTYPE.itemsize == 40
 
 # Every symbol include/cld_mi355x.h declares (checked by tests/test_capi.py)
-EXPORTS = ("detect_language", "cld_init", "cld_shutdown", "cld_detect_batch", "cld_detect_batch_device",
-           "cld_language_code", "cld_language_name", "cld_last_batch_stats", "cld_version")
+EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cld_detect_batch",
+           "cld_detect_batch_device", "cld_plan_shards", "cld_kernel_time", "cld_language_code",
+           "cld_language_name", "cld_last_batch_stats", "cld_version")
 
 
 class BatchStats(ctypes.Structure):
@@ -59,6 +60,10 @@ def lib():
         L.cld_language_name.restype = ctypes.c_char_p
         L.cld_version.restype = ctypes.c_char_p
         L.cld_last_batch_stats.argtypes = [ctypes.c_int, ctypes.POINTER(BatchStats)]
+        L.cld_init_device.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.cld_plan_shards.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.cld_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -67,6 +72,32 @@ def init(tables=None, n_devices=0):
     rc = lib().cld_init(tables.encode() if tables else None, n_devices)
     if rc != 0:
         raise CldError("cld_init failed: %d" % rc)
+
+
+def init_device(device, tables=None):
+    """One process per GPU: bind the runtime to HIP device `device` (context 0)."""
+    rc = lib().cld_init_device(tables.encode() if tables else None, device)
+    if rc != 0:
+        raise CldError("cld_init_device(%d) failed: %d" % (device, rc))
+
+
+def plan_shards(offsets, nshards):
+    """Byte-balanced contiguous document shards (host-only, no GPU)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cuts = np.zeros(nshards + 1, dtype=np.uint64)
+    rc = lib().cld_plan_shards(offsets.ctypes.data, len(offsets) - 1, nshards, cuts.ctypes.data)
+    if rc != 0:
+        raise CldError("cld_plan_shards failed: %d" % rc)
+    return cuts.astype(np.int64)
+
+
+def kernel_time(ctx=0):
+    """(short_ms, general_ms, launches) summed over batches since the last call."""
+    a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    rc = lib().cld_kernel_time(ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n))
+    if rc != 0:
+        raise CldError("cld_kernel_time failed: %d" % rc)
+    return a.value, b.value, n.value
 
 
 def pack(docs):

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -196,6 +197,8 @@ struct Device {
   uint64_t* d_offs = nullptr; size_t offs_cap = 0;
   cld_result* d_out = nullptr; size_t out_cap = 0;
   hipEvent_t ev[3]{};
+  std::vector<std::array<hipEvent_t, 3>> ev_pool;   // one triple per enqueue since reset
+  size_t ev_used = 0;
   cld_batch_stats last{};
   uint64_t last_n = 0;
   bool stats_pending = false;
@@ -246,20 +249,26 @@ int init_device(Device* d) {
   while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
   d->lanes = lanes;
   HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
-  for (auto& e : d->ev) HIP_OK(hipEventCreate(&e));
   return CLD_OK;
 }
 
 // Enqueue the whole pipeline for n documents already on device d.
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s) {
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  if (d->ev_used == d->ev_pool.size()) {
+    std::array<hipEvent_t, 3> t{};
+    for (auto& e : t) HIP_OK(hipEventCreate(&e));
+    d->ev_pool.push_back(t);
+  }
+  auto& ev = d->ev_pool[d->ev_used++];
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
-  HIP_OK(hipEventRecord(d->ev[0], s));
+  HIP_OK(hipEventRecord(ev[0], s));
   HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
-  HIP_OK(hipEventRecord(d->ev[1], s));
+  HIP_OK(hipEventRecord(ev[1], s));
   HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
                             d->d_counters, s));
-  HIP_OK(hipEventRecord(d->ev[2], s));
+  HIP_OK(hipEventRecord(ev[2], s));
+  d->ev[0] = ev[0]; d->ev[1] = ev[1]; d->ev[2] = ev[2];
   d->last_n = n;
   d->stats_pending = true;
   return CLD_OK;
@@ -292,6 +301,7 @@ int collect_stats(Device* d) {
 int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
+  d->ev_used = 0;
   const uint64_t base = offs[0], bytes = offs[n] - offs[0];
   if (grow(&d->d_buf, &d->buf_cap, std::max<size_t>(bytes, 1))) return CLD_ENOMEM;
   if (grow(&d->d_offs, &d->offs_cap, n + 1)) return CLD_ENOMEM;
@@ -346,6 +356,59 @@ int cld_init(const char* tables_path, int n_devices) {
   return g_init_rc = CLD_OK;
 }
 
+int cld_init_device(const char* tables_path, int device) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_inited) return g_init_rc;
+  g_inited = true;
+  std::string path = tables_path ? tables_path : default_tables_path();
+  int rc = load_tables(path.c_str(), &g_tab);
+  if (rc) return g_init_rc = rc;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return g_init_rc = CLD_ENODEV;
+  Device* d = new Device();
+  d->id = device;
+  if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
+  g_devs.push_back(d);
+  return g_init_rc = CLD_OK;
+}
+
+int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches) {
+  if (ctx < 0 || ctx >= (int)g_devs.size()) return CLD_EINVAL;
+  Device* d = g_devs[ctx];
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  double a = 0, b = 0;
+  for (size_t i = 0; i < d->ev_used; ++i) {
+    HIP_OK(hipEventSynchronize(d->ev_pool[i][2]));
+    float x = 0, y = 0;
+    HIP_OK(hipEventElapsedTime(&x, d->ev_pool[i][0], d->ev_pool[i][1]));
+    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][2]));
+    a += x; b += y;
+  }
+  if (short_ms) *short_ms = a;
+  if (general_ms) *general_ms = b;
+  if (launches) *launches = (int)d->ev_used;
+  d->ev_used = 0;
+  return CLD_OK;
+}
+
+int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts) {
+  if (!offsets || !cuts || nshards < 1) return CLD_EINVAL;
+  const uint64_t total = (offsets[n] - offsets[0]) + 64ull * n;
+  cuts[0] = 0;
+  cuts[nshards] = n;
+  for (int k = 1; k < nshards; ++k) {
+    uint64_t target = total * (uint64_t)k / (uint64_t)nshards;
+    size_t lo = cuts[k - 1], hi = n;
+    while (lo < hi) {
+      size_t mid = (lo + hi) / 2;
+      if ((offsets[mid] - offsets[0]) + 64ull * mid < target) lo = mid + 1; else hi = mid;
+    }
+    cuts[k] = lo;
+  }
+  return CLD_OK;
+}
+
 void cld_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   for (Device* d : g_devs) {
@@ -353,7 +416,7 @@ void cld_shutdown(void) {
     (void)hipStreamSynchronize(d->stream);
     (void)hipFree(d->d_blob); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
-    for (auto& e : d->ev) (void)hipEventDestroy(e);
+    for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
     delete d;
   }
@@ -372,18 +435,8 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   if (rc) return rc;
   const size_t ndev = g_devs.size();
   // Shard by byte count (+ a per-document weight) at document boundaries.
-  const uint64_t total = (offsets[n] - offsets[0]) + 64ull * n;
   std::vector<size_t> cut(ndev + 1, 0);
-  cut[ndev] = n;
-  for (size_t k = 1; k < ndev; ++k) {
-    uint64_t target = total * k / ndev;
-    size_t lo = cut[k - 1], hi = n;
-    while (lo < hi) {
-      size_t mid = (lo + hi) / 2;
-      if ((offsets[mid] - offsets[0]) + 64ull * mid < target) lo = mid + 1; else hi = mid;
-    }
-    cut[k] = lo;
-  }
+  cld_plan_shards(offsets, n, (int)ndev, cut.data());
   if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
@@ -406,6 +459,7 @@ int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  if (d->ev_used >= 4096) d->ev_used = 0;     // bounded when callers never read timings
   return enqueue(d, d_buf, d_offsets, n, d_out, s);
 }
 

@@ -132,7 +132,9 @@ def parse_verbose_html(path):
           rec = {"doc": doc_i, "script": m.group(1), "text_bytes": int(m.group(2)),
                  "span_text": html.unescape(m.group(3)), "rounds": []}
           for hb in re.finditer(r"DumpHitBuffer\[(\w+), next_base/delta/distinct (\d+), (\d+), (\d+)\)<br>\n(.*?)<br>\nLinear\[\) <br>DumpLinearBuffer\[(\d+)\)<br>\n(.*?)<br>\nDumpChunkStart\[(\d+)\]<br>\n(.*?)<br>\n(.*?)<br>DumpSummaryBuffer\[(\d+)\]<br>\n[^\n]*\n(.*?)<br>\n<br>", seg, re.S):
-              base = [[int(a), int(b)] for a, b in re.findall(r"Q\[\d+\](-?\d+),(-?\d+),", hb.group(5))]
+              # Q[next_base] is the dummy end-of-scan entry the dump appends (:590-596)
+              base = [[int(a), int(b)] for i, a, b in re.findall(r"Q\[(\d+)\](-?\d+),(-?\d+),", hb.group(5))
+                      if int(i) < int(hb.group(2))]
               delta = [[int(a), int(b)] for a, b in re.findall(r"L\[\d+\](-?\d+),(-?\d+),", hb.group(5))]
               distinct = [[int(a), int(b)] for a, b in re.findall(r"(?<![A-Z])D\[\d+\](-?\d+),(-?\d+),", hb.group(5))]
               linear = [[int(i), int(o), t, int(lp, 16)] for i, o, t, lp in
@@ -169,6 +171,9 @@ def main():
         if d["var"]:
             used.add(d["var"])
             d["text_hex"] = lits[d["var"]].hex()
+            # The HTML shows every scored letter; equality of the letter streams
+            # says the dump was produced from exactly this input version.
+            d["exact_input"] = letters_key(d["shown_text"]) == keys[d["var"]]
     doc_vars = {d["var"] for d in docs}
     test_list = [{"expected": e, "var": v, "text_hex": lits[v].hex(), "in_html": v in doc_vars}
                  for e, v in pairs if v in lits]

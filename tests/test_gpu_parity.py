@@ -1,0 +1,124 @@
+"""HIP path vs the C oracle, bit-exact, through the C ABI (needs an MI355X)."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import corpus
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def assert_same(gpu_res, ref, what):
+    for f in FIELDS:
+        a, b = gpu_res[f], ref[f]
+        if not np.array_equal(a, b):
+            bad = np.nonzero((a != b).reshape(len(a), -1).any(axis=1))[0]
+            raise AssertionError("%s: %s differs on %d docs, first %s: gpu=%s oracle=%s"
+                                 % (what, f, len(bad), bad[:5], gpu_res[bad[0]], ref[bad[0]]))
+
+
+def check(gpu, oracle, buf, offs, what, threads=8):
+    got = gpu.detect_batch(buf=buf, offsets=offs)
+    ref = oracle.detect_batch(buf, offs, threads=threads)
+    assert_same(got, ref, what)
+    return got
+
+
+def test_golden_and_kat_documents(gpu, oracle, golden, kats):
+    docs = [bytes.fromhex(t["text_hex"]) for t in golden["test_pairs"]]
+    docs += [bytes.fromhex(d["text_hex"]) for d in golden["html_docs"]]
+    docs += [k["text"].encode() for k in kats]
+    buf, offs = gpu.pack(docs)
+    check(gpu, oracle, buf, offs, "fixtures")
+
+
+EDGE = [
+    b"", b" ", b"\t\n", b"a", b"A", b"1234567890", b"!!!???", b"\x00", b"a\x00b c", b"\xc3", b"\xff\xfe\xfd",
+    b"\xe0\xa0", b"\xf0\x9f\x98\x80 smile", b"\xc0\xa9bad", "Ünïcödé ÀÉÎ ÇŒ".encode(),
+    "İstanbul'da KIŞ".encode(), "Ⱥ Ⱦ ȺȺȺ".encode(), b"x" * 255, b"x" * 256, b"x" * 257, b"ab " * 5000,
+    ("العربية abc рус " * 50).encode(),
+    ("ꙮ" * 100).encode(), ("á" * 200).encode(), b"http://x.y/z @user #tag",
+]
+
+
+def test_edge_cases(gpu, oracle):
+    buf, offs = gpu.pack(EDGE)
+    check(gpu, oracle, buf, offs, "edge")
+
+
+def test_bucket_boundaries_and_requeue(gpu, oracle):
+    """Documents around the short-kernel capacity and ones needing passes 2/3
+    (Squeeze restart, Repeats) must agree whichever kernel finishes them."""
+    rng = np.random.default_rng(5)
+    b2, o2 = corpus.c2(4000, seed=11)
+    docs = []
+    for L in (200, 250, 255, 256, 257, 260, 300, 511, 512, 513, 1000, 4000):
+        i = int(rng.integers(0, 3000))
+        d = bytes(b2[o2[i]:o2[i + 40]])[:L]
+        docs.append(d)
+    docs.append(("aaaa bbbb cccc " * 400).encode())                 # squeeze trigger (repetitive)
+    docs.append((" ".join(["w%d" % i for i in range(2000)])).encode())
+    docs.append(bytes(b2[o2[0]:o2[300]]))                           # ~40 KB mixed-language: pass 3
+    buf, offs = gpu.pack(docs)
+    check(gpu, oracle, buf, offs, "boundaries")
+
+
+@pytest.mark.parametrize("cfg,n", [("c2", 50000), ("c4", 20000), ("c5", 3000), ("c3", 48)])
+def test_synthetic_corpora(gpu, oracle, cfg, n):
+    buf, offs = corpus.GENERATORS[cfg](n)
+    check(gpu, oracle, buf, offs, cfg, threads=16)
+
+
+def test_long_documents(gpu, oracle):
+    """Spans beyond the 40,928-byte script buffer, the len/2 soft split for
+    40-80 KB remainders, and 1000-hit rounds."""
+    b3, o3 = corpus.c3(8, page=65536 * 2)
+    docs = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(4)]
+    b2, o2 = corpus.c2(6000, seed=3)
+    docs.append(bytes(b2[o2[0]:o2[-1]]).replace(b" ", b" "))          # ~800 KB single document
+    buf, offs = gpu.pack(docs)
+    check(gpu, oracle, buf, offs, "long")
+
+
+def test_full_size_c2_properties(gpu, oracle):
+    """At BASELINE size (1M tweets): a random 20K sample is bit-exact vs the
+    oracle, and results are invariant under batch permutation / splitting."""
+    buf, offs = corpus.c2(1_000_000)
+    got = gpu.detect_batch(buf=buf, offsets=offs)
+    rng = np.random.default_rng(1)
+    idx = np.sort(rng.choice(1_000_000, size=20000, replace=False))
+    docs = [bytes(buf[offs[i]:offs[i + 1]]) for i in idx]
+    sb, so = gpu.pack(docs)
+    assert_same(got[idx], oracle.detect_batch(sb, so, threads=16), "c2 sample")
+    # permutation / re-batching invariance
+    perm = rng.permutation(len(docs))
+    pb, po = gpu.pack([docs[i] for i in perm])
+    again = gpu.detect_batch(buf=pb, offsets=po)
+    inv = np.empty_like(perm); inv[perm] = np.arange(len(perm))
+    assert_same(again[inv], got[idx], "permuted")
+    counts = np.bincount(got["summary_lang"], minlength=614)
+    assert counts.sum() == 1_000_000 and (counts > 0).sum() >= 12
+
+
+def test_detect_language_abi_concurrent(gpu, oracle, kats):
+    """wrapper.h detect_language: equal to the oracle's wrapper semantics, also
+    under concurrent callers (coalesced micro-batches)."""
+    texts = [k["text"] for k in kats] * 8
+    want = [oracle.detect_language(t) for t in texts]
+    got = [None] * len(texts)
+
+    def worker(lo):
+        for i in range(lo, len(texts), 8):
+            got[i] = gpu.detect_language(texts[i])
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert got == want
+    assert gpu.detect_language(" 私はガラスを食べられます。それは私を傷つけません。") == "ja"
+    assert gpu.detect_language("") == "en"
