@@ -64,6 +64,12 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
  * every batch enqueued on context `ctx` since the previous call; resets. */
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
+/* Diagnostics: per-stage shader-clock cycle sums of the wavefront kernel on
+ * context `ctx` since the previous call (0 load, 1 span, 2 lower, 3 quad/uni,
+ * 4 octa/bi, 5 score, 6 document level); all zero unless the runtime was
+ * started with CLD_PROFILE_STAGES=1.  Resets. */
+int cld_stage_cycles(int ctx, uint64_t* cycles8);
+
 /* Batch detection.  Documents are [buf + offsets[i], buf + offsets[i+1]),
  * i < n (offsets has n+1 entries, non-decreasing).  Each document is scored
  * as if followed by NUL bytes, i.e. exactly like detect_language() on a

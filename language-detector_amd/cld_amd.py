@@ -24,7 +24,7 @@ assert RESULT_DTYPE.itemsize == 40
 # Every symbol include/cld_mi355x.h declares (checked by tests/test_capi.py)
 EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cld_detect_batch",
            "cld_detect_batch_device", "cld_plan_shards", "cld_kernel_time", "cld_language_code",
-           "cld_language_name", "cld_last_batch_stats", "cld_version")
+           "cld_language_name", "cld_last_batch_stats", "cld_version", "cld_stage_cycles")
 
 
 class BatchStats(ctypes.Structure):
@@ -98,6 +98,15 @@ def kernel_time(ctx=0):
     if rc != 0:
         raise CldError("cld_kernel_time failed: %d" % rc)
     return a.value, b.value, n.value
+
+
+def stage_cycles(ctx=0):
+    """Per-stage cycle sums of the wavefront kernel (CLD_PROFILE_STAGES=1)."""
+    c = np.zeros(8, dtype=np.uint64)
+    rc = lib().cld_stage_cycles(ctx, ctypes.c_void_p(c.ctypes.data))
+    if rc != 0:
+        raise CldError("cld_stage_cycles failed: %d" % rc)
+    return c
 
 
 def pack(docs):

@@ -9,6 +9,9 @@
 // Short-document bucket: documents up to kShortCap bytes run one per lane with
 // private buffers sized for that length (span text <= 2*CAP).
 constexpr int kShortCap = 256;
+// Wavefront-per-document bucket (cld_wave.hip)
+constexpr int kWaveCap = 256;
+constexpr int kWaveWPB = 4;
 constexpr int kShortSB = 2 * kShortCap + 64;
 constexpr int kShortLB = kShortSB * 3 / 2 + 64;
 constexpr int kShortHB = kShortCap + 32;
@@ -20,6 +23,10 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
 extern "C" {
 size_t cld_general_work_bytes();
 size_t cld_short_work_bytes();
+hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+                           cld_result* out, uint32_t* requeue_list, uint32_t* counters,
+                           unsigned long long* prof, hipStream_t s);
+size_t cld_wave_smem_bytes();
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                             hipStream_t s);

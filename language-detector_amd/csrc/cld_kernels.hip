@@ -8,6 +8,7 @@
 //                persistent grid pulling documents from the re-queue list
 //                with one atomic dequeue per document.
 #include "cld_pipeline.hip"
+#include "cld_wave.hip"
 #include "cld_kernels.h"
 
 namespace cld {
@@ -60,11 +61,44 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
   }
 }
 
+// One wavefront per document of <= CAP bytes, WPB documents per workgroup.
+template <int CAP, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
+                                                   const uint64_t* __restrict__ offs, int n,
+                                                   cld_result* __restrict__ out,
+                                                   uint32_t* __restrict__ requeue_list,
+                                                   uint32_t* __restrict__ counters,
+                                                   unsigned long long* __restrict__ prof) {
+  __shared__ wave::Smem<CAP> smem[WPB];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * WPB + wv;
+  if (i >= n) return;
+  const uint64_t a = offs[i], b = offs[i + 1];
+  const int64_t len = (int64_t)(b - a);
+  bool rq = len > CAP;
+  if (!rq) rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], prof);
+  if (rq && lane == 0) {
+    uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
+    requeue_list[k] = (uint32_t)i;
+  }
+}
+
 }  // namespace cld
 
 extern "C" {
 size_t cld_general_work_bytes() { return sizeof(cld::GeneralWork); }
 size_t cld_short_work_bytes() { return sizeof(cld::ShortWork); }
+size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
+
+hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+                           cld_result* out, uint32_t* requeue_list, uint32_t* counters,
+                           unsigned long long* prof, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  dim3 grid((n + kWaveWPB - 1) / kWaveWPB), block(64 * kWaveWPB);
+  hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
+                     requeue_list, counters, prof);
+  return hipGetLastError();
+}
 
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,

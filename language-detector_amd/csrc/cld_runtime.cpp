@@ -190,6 +190,8 @@ struct Device {
   uint8_t* d_arena = nullptr;
   uint64_t stride = 0;
   int lanes = 0;
+  int front = 0;              // 0: wavefront-per-document kernel, 1: lane-per-document (CLD_FRONT=lane)
+  unsigned long long* d_prof = nullptr;   // per-stage cycle sums (CLD_PROFILE_STAGES=1)
   uint32_t* d_counters = nullptr;
   uint32_t* d_requeue = nullptr;
   size_t requeue_cap = 0;
@@ -248,6 +250,13 @@ int init_device(Device* d) {
   lanes = std::max(64, (lanes / 64) * 64);
   while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
   d->lanes = lanes;
+  if (const char* e = getenv("CLD_FRONT")) d->front = strcmp(e, "lane") == 0 ? 1 : 0;
+  if (const char* e = getenv("CLD_PROFILE_STAGES")) {
+    if (atoi(e) > 0) {
+      HIP_OK(hipMalloc(&d->d_prof, 8 * sizeof(unsigned long long)));
+      HIP_OK(hipMemset(d->d_prof, 0, 8 * sizeof(unsigned long long)));
+    }
+  }
   HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
   return CLD_OK;
 }
@@ -263,7 +272,10 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   auto& ev = d->ev_pool[d->ev_used++];
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
   HIP_OK(hipEventRecord(ev[0], s));
-  HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
+  if (d->front == 1)
+    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
+  else
+    HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, s));
   HIP_OK(hipEventRecord(ev[1], s));
   HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
                             d->d_counters, s));
@@ -370,6 +382,17 @@ int cld_init_device(const char* tables_path, int device) {
   if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
   g_devs.push_back(d);
   return g_init_rc = CLD_OK;
+}
+
+int cld_stage_cycles(int ctx, uint64_t* cycles8) {
+  if (!cycles8 || ctx < 0 || ctx >= (int)g_devs.size()) return CLD_EINVAL;
+  Device* d = g_devs[ctx];
+  if (!d->d_prof) { memset(cycles8, 0, 8 * sizeof(uint64_t)); return CLD_OK; }
+  (void)hipSetDevice(d->id);
+  HIP_OK(hipStreamSynchronize(d->stream));
+  HIP_OK(hipMemcpy(cycles8, d->d_prof, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemset(d->d_prof, 0, 8 * sizeof(unsigned long long)));
+  return CLD_OK;
 }
 
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches) {

@@ -1,0 +1,917 @@
+// cld_wave.hip -- one wavefront per document (documents of <= CAP bytes).
+//
+// The lane-per-document front end keeps ~8 KB of per-document state in
+// private memory; on gfx950 that is scratch, and a launch over 1M tweets moved
+// ~13 GB of scratch through HBM (profiles/round1a_c2_pmc_*.csv).  Here the 64
+// lanes of a wavefront share one document, its state sits in LDS (~7 KB per
+// wave), and every stage that is data-parallel in the reference runs across
+// lanes:
+//
+//   stage                         reference                      across lanes
+//   load + per-byte script/scan   getonescriptspan.cc:480-485,   bytes
+//                                 utf8statetable.cc:362-554
+//   span runs (GetOneScriptSpan)  getonescriptspan.cc:799-1027   64-bit ballot masks +
+//                                                                scalar bit scans
+//   LowerScriptSpan               utf8statetable.cc:608-867      characters + prefix sum
+//   GetQuadHits chain             cldutil.cc:315-405             next[] per byte, scalar walk,
+//                                                                hashes/probes per quad
+//   GetOctaHits                   cldutil.cc:416-533             words (scalar repeat filter)
+//   GetUniHits / GetBiHits        cldutil.cc:201-310             characters
+//   LinearizeAll + ChunkAll       scoreonescriptspan.cc:856-1031 emissions: chunk id by
+//                                                                rank arithmetic (no merge)
+//   ScoreOneChunk / boosts        scoreonescriptspan.cc:208-302  LDS atomics into a u32 tote,
+//                                                                3x wave argmax for top-3
+//   DocTote / summary             tote.cc, compact_lang_det_impl lane 0 (a few dozen ops)
+//
+// A document the wave cannot reproduce exactly in this form (longer than CAP,
+// a byte sequence whose scanner/lowercaser state crosses a character
+// boundary, a bucket overflow, or a second pass) is appended to the re-queue
+// list and redone from scratch by the general kernel, so results stay
+// bit-identical to the sequential restatement in every case.
+
+namespace cld {
+namespace wave {
+
+__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uflu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t ufl64(uint64_t v) {
+  return ((uint64_t)uflu((uint32_t)(v >> 32)) << 32) | uflu((uint32_t)v);
+}
+__device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint32_t rdlu(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
+  return ((uint64_t)rdlu((uint32_t)(v >> 32), l) << 32) | rdlu((uint32_t)v, l);
+}
+
+// Order LDS traffic between lanes of one wavefront (no workgroup barrier:
+// the waves of a workgroup work on different documents).
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// Register arrays indexed by a wave-uniform register number r (entry i of a
+// 64*N list lives in lane i&63 of register i>>6).
+template <int N, class V>
+__device__ __forceinline__ V pick(const V (&a)[N], int r) {
+  V v = a[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) if (r == i) v = a[i];
+  return v;
+}
+template <int N, class V>
+__device__ __forceinline__ void put_lane(V (&a)[N], int r, int l, V val) {
+  const bool me = (int)__lane_id() == l;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (r == i && me) a[i] = val;
+}
+template <int N>
+__device__ __forceinline__ void or_bit(uint64_t (&a)[N], int r, int l) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) if (r == i) a[i] |= 1ull << l;
+}
+
+__device__ __forceinline__ int excl_scan(int v, int lane) {
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x - v;
+}
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wmax(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64); v = o > v ? o : v; }
+  return v;
+}
+__device__ __forceinline__ uint32_t wmin(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64); v = o < v ? o : v; }
+  return v;
+}
+__device__ __forceinline__ uint64_t wor64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64);
+    uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
+    v |= ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// Per-wave capacities for documents of at most CAP bytes.  Anything that
+// would overflow them is re-queued, never truncated.
+template <int CAP>
+struct Cfg {
+  static constexpr int DOC = CAP + 32;              // document + NUL padding (DocView semantics)
+  static constexpr int NM = (CAP + 63) / 64;        // 64-bit mask words over document bytes
+  static constexpr int SB = CAP + 72;               // span text: ' ' + letters/single spaces + "   \0"
+  static constexpr int LB = (SB * 3) / 2 + 64;      // lowered span (max per-char growth 1.5x) + hash read pad
+  static constexpr int NR = 2;                      // registers of 64 entries: quad chain, words
+  static constexpr int NB = NR * 64;                // base hits / quad chain / words
+  static constexpr int NE = 2 * NB;                 // base emissions (<= 2 langprobs per hit)
+  static constexpr int ND = 96;
+  static constexpr int NX = 160;
+  static constexpr int MAXCH = NE / kChunksizeQuads + 3;
+  static_assert(NB < kMaxScoringHits - 1, "a round must never reach the reference's hit cap");
+  static_assert(CAP < 2048, "spans of a short document can never reach the squeeze test");
+};
+
+template <int CAP>
+struct Smem {
+  using C = Cfg<CAP>;
+  uint8_t doc[C::DOC];
+  uint8_t sn[C::DOC];                 // script number at each byte position (GetUTF8LetterScriptNum)
+  uint64_t lsm[C::NM];                // letter stops: char start, scanner stops there, script != 0
+  uint64_t brk[C::NM];                // letters that end a run for the current span script
+  union alignas(16) {
+    uint8_t sbuf[C::SB];              // span text (raw)
+    uint32_t tote[256];               // chunk tote, u32 per key (low 16 bits == reference uint16)
+  } u;
+  uint8_t lbuf[C::LB];                // lowered span text
+  union alignas(16) {                 // stage-local arrays
+    uint16_t nx[CAP];                 // load: p + ScanToLetterOrSpecial(p, L - p)
+    uint16_t nxq[C::LB];              // quad hits: next quad start for a quad starting at p
+    uint16_t wsp[C::NB + 1];          // octa hits: word-ending spaces
+    struct {                          // scoring: base emissions (offset, langprob, chunk), linear order
+      uint32_t be_lp[C::NE];
+      uint16_t be_off[C::NE + 1];
+      uint8_t be_ch[C::NE];
+    } e;
+  } a;
+  uint16_t b_off[C::NB]; uint32_t b_ind[C::NB];   // base hits before expansion
+  uint16_t d_off[C::ND]; uint32_t d_ind[C::ND];   // delta hits; compacted in place to emissions
+  uint16_t x_off[C::NX]; uint32_t x_ind[C::NX];   // distinct hits; likewise
+  uint8_t d_ch[C::ND], x_ch[C::NX];
+  uint16_t E[C::MAXCH];               // cumulative base-emission count closing each chunk
+  uint32_t lo[C::MAXCH];
+  uint32_t ring[2][4];                // distinct boosts, latn / othr, oldest first
+  DocTote dt;
+};
+
+// -------------------------------------------------------------- bit scans
+template <int NM>
+__device__ __forceinline__ int find_first(const uint64_t* m, int from, int L) {
+  if (from >= L) return L;
+  int w = from >> 6;
+  uint64_t x = ufl64(m[w]) & (~0ull << (from & 63));
+  for (;;) {
+    if (x) { int r = (w << 6) + __builtin_ctzll(x); return r < L ? r : L; }
+    ++w;
+    if (w >= NM || (w << 6) >= L) return L;
+    x = ufl64(m[w]);
+  }
+}
+
+// ------------------------------------------------------- stage 0: document
+// Loads the document, computes script numbers and scanner stops per byte
+// and checks that the per-character formulation below reproduces the
+// sequential scanner: the document tiles into lead+continuation characters
+// and a scan started at any character either stops on it or continues to the
+// scan result of the next character.
+template <int CAP>
+__device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane) {
+  using C = Cfg<CAP>;
+  for (int p = lane; p < C::DOC; p += 64) s.doc[p] = p < L ? g[p] : (uint8_t)0;
+  wsync();
+  DocView dv{s.doc, L};
+  for (int p = lane; p < L + 4; p += 64) s.sn[p] = (uint8_t)script_num(T, dv, p);
+  for (int p = lane; p < L; p += 64) s.a.nx[p] = (uint16_t)(p + scan_to_letter_or_special(T, dv, p, L - p));
+  wsync();
+  int bad = 0, conts = 0, need = 0;
+  for (int p = lane; p < L; p += 64) {
+    uint8_t c = s.doc[p];
+    if ((c & 0xC0) == 0x80) { ++conts; continue; }
+    int n = utf8_len(c);
+    if (p + n > L) { bad = 1; continue; }
+    for (int k = 1; k < n; ++k) bad |= ((s.doc[p + k] & 0xC0) != 0x80);
+    need += n - 1;
+    int np = s.a.nx[p];
+    if (np != p) {
+      int q = p + n;
+      int want = q >= L ? L : (int)s.a.nx[q];
+      bad |= (np != want);
+    }
+  }
+  bad |= (wsum(conts) != wsum(need)) ? 1 : 0;
+  if (__ballot(bad != 0)) return false;
+  for (int w = 0; w < C::NM; ++w) {
+    int p = w * 64 + lane;
+    bool ls = false;
+    if (p < L) ls = ((s.doc[p] & 0xC0) != 0x80) && s.a.nx[p] == p && s.sn[p] != 0;
+    uint64_t m = __ballot(ls);
+    if (lane == 0) s.lsm[w] = m;
+  }
+  wsync();
+  return true;
+}
+
+// ------------------------------------------------ stage 1: one script span
+// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) as runs:
+// ' ' + run1 + ' ' + run2 + ' ' ... + runK + ' ' + "   \0".  A run starts at
+// a letter stop of the span script (or Inherited) and ends at the first
+// character the letters loop would break on; the gap after it is skipped to
+// the next letter stop, which either continues the span or starts the next.
+// Returns text_bytes (0 = no further span); *next advances like next_byte_.
+template <int CAP>
+__device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int& ulscript, int lane) {
+  using C = Cfg<CAP>;
+  const int common = (int)T.common, inherited = (int)T.inherited;
+  const int q = find_first<C::NM>(s.lsm, next, L);
+  if (q >= L) { next = L; return 0; }
+  const int spanscript = ufl(s.sn[q]);
+  ulscript = spanscript;
+  for (int w = q >> 6; w < C::NM; ++w) {
+    int p = w * 64 + lane;
+    bool b = false;
+    if (p >= q && p < L && (s.doc[p] & 0xC0) != 0x80) {
+      int sc = s.sn[p];
+      if (sc != spanscript && sc != inherited) {
+        if (sc == common) {
+          b = true;
+        } else {
+          int sc2 = s.sn[p + utf8_len(s.doc[p])];
+          if (sc2 != common && sc2 != spanscript) b = true;
+        }
+      }
+    }
+    uint64_t m = __ballot(b);
+    if (lane == 0) s.brk[w] = m;
+  }
+  wsync();
+  if (lane == 0) s.u.sbuf[0] = ' ';
+  int put = 1, p = q, take;
+  for (;;) {
+    const int b = find_first<C::NM>(s.brk, p, L);
+    for (int i = lane; i < b - p; i += 64) s.u.sbuf[put + i] = s.doc[p + i];
+    put += b - p;
+    if (lane == 0) s.u.sbuf[put] = ' ';
+    ++put;
+    if (b >= L) { take = L; break; }
+    const int q2 = find_first<C::NM>(s.lsm, b, L);
+    if (q2 >= L) { take = L; break; }
+    const int sc = ufl(s.sn[q2]);
+    if (sc != spanscript && sc != inherited) { take = q2; break; }
+    p = q2;
+  }
+  if (lane < 4) s.u.sbuf[put + lane] = lane < 3 ? ' ' : 0;
+  next = take;
+  wsync();
+  return put;
+}
+
+// ------------------------------------------------ stage 2: lowercase
+// One character through the utf8repl_lettermarklower machine
+// (utf8statetable.cc:645-760), starting and -- checked -- ending in state 0,
+// so the characters of the span can be lowered independently.  Output bytes
+// are packed little-endian into *out.
+__device__ __forceinline__ void setb(uint64_t& o, int i, uint32_t v) {
+  o = (o & ~(0xFFull << (8 * i))) | ((uint64_t)(v & 0xFF) << (8 * i));
+}
+__device__ bool lower_char(const DevTables& T, const uint8_t* src, int n, uint64_t& out, int& olen) {
+  const DevSM& sm = T.lower;
+  const int sh = (int)sm.shift;
+  const int nE = 1 << sh;
+  const int64_t tb0 = sm.state0;
+  int64_t tb = tb0;
+  out = 0; olen = 0;
+  for (int i = 0; i < n; ++i) {
+    const uint8_t c = src[i];
+    const int e = sm8(sm, tb + c);
+    if (olen >= 8) return false;
+    out |= (uint64_t)c << (8 * olen);
+    ++olen;
+    if (e < kExitIllegalStructure) { tb = tb0 + ((int64_t)e << sh); continue; }
+    switch (e) {
+      case kExitReplace31:
+        if (olen < 3) return false;
+        olen -= 2; setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        out &= olen >= 8 ? ~0ull : ((1ull << (8 * olen)) - 1);
+        break;
+      case kExitReplace32:
+        if (olen < 3) return false;
+        olen -= 1; setb(out, olen - 2, sm8(sm, tb + c + nE * 2)); setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        out &= (1ull << (8 * olen)) - 1;
+        break;
+      case kExitReplace21:
+        if (olen < 2) return false;
+        olen -= 1; setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        out &= (1ull << (8 * olen)) - 1;
+        break;
+      case kExitReplace3:
+        if (olen < 3) return false;
+        setb(out, olen - 3, sm8(sm, tb + c + nE * 3)); setb(out, olen - 2, sm8(sm, tb + c + nE * 2));
+        setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        break;
+      case kExitReplace2:
+        if (olen < 2) return false;
+        setb(out, olen - 2, sm8(sm, tb + c + nE * 2)); setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        break;
+      case kExitReplace1:
+        setb(out, olen - 1, sm8(sm, tb + c + nE * 1));
+        break;
+      case kExitReplace1S0:
+        setb(out, olen - 1, sm8(sm, tb + c + 256 * 1));
+        break;
+      case kExitReplaceOffset2:
+      case kExitSpecial:
+      case kExitReplaceOffset1: {
+        bool z = (nE != 256) && in_state_zero(sm, tb);
+        int offset = 0;
+        if (e == kExitReplaceOffset2) offset += (uint8_t)sm8(sm, tb + c + (z ? 256 : nE) * 2) << 8;
+        offset += (uint8_t)sm8(sm, tb + c + (z ? 256 : nE) * 1);
+        if ((uint32_t)offset >= sm.n_remap) return false;
+        const uint8_t* re = sm.remap + 4 * offset;
+        const int del = re[0] & 0x7F, add = re[1] & 0x7F, soff = re[2] | (re[3] << 8);
+        if ((re[0] & 0x80) || del > olen || olen - del + add > 8) return false;
+        olen -= del;
+        out &= olen ? ((1ull << (8 * olen)) - 1) : 0ull;
+        for (int k = 0; k < add; ++k) {
+          uint32_t v = ((uint32_t)(soff + k) < sm.n_rstr) ? sm.rstr[soff + k] : 0u;
+          out |= (uint64_t)v << (8 * olen);
+          ++olen;
+        }
+        break;
+      }
+      default:
+        return false;
+    }
+    tb = tb0;
+  }
+  if (tb != tb0) return false;
+  // the output must itself tile into characters (hit scanners step by lead byte)
+  for (int i = 0; i < olen;) {
+    uint32_t b = (uint32_t)(out >> (8 * i)) & 0xFF;
+    if ((b & 0xC0) == 0x80) return false;
+    int m = utf8_len((uint8_t)b);
+    if (i + m > olen) return false;
+    for (int k = 1; k < m; ++k)
+      if ((((uint32_t)(out >> (8 * (i + k)))) & 0xC0) != 0x80) return false;
+    i += m;
+  }
+  return true;
+}
+
+// LowerScriptSpan (getonescriptspan.cc:1033-1054): returns text_bytes, or -1.
+template <int CAP>
+__device__ int lower_span(const DevTables& T, Smem<CAP>& s, int text_bytes, int lane) {
+  using C = Cfg<CAP>;
+  const int ilen = text_bytes + 3;
+  int obase = 0;
+  int bad = 0;
+  for (int w0 = 0; w0 < ilen; w0 += 64) {
+    const int p = w0 + lane;
+    uint64_t o = 0;
+    int olen = 0;
+    if (p < ilen && (s.u.sbuf[p] & 0xC0) != 0x80) {
+      if (!lower_char(T, &s.u.sbuf[p], utf8_len(s.u.sbuf[p]), o, olen)) { bad = 1; olen = 0; }
+    }
+    const int pre = excl_scan(olen, lane);
+    const int tot = rdl(pre + olen, 63);
+    if (obase + tot + 4 > C::LB - 16) bad = 1;
+    else
+      for (int k = 0; k < olen; ++k) s.lbuf[obase + pre + k] = (uint8_t)(o >> (8 * k));
+    obase += tot;
+  }
+  if (__ballot(bad != 0)) return -1;
+  for (int k = lane; k < 20; k += 64) s.lbuf[obase + k] = 0;
+  wsync();
+  return obase - 3;
+}
+
+// ------------------------------------------------ stage 3: hit streams
+// GetQuadHits (cldutil.cc:315-405).  The chain of quad starts is a pure
+// function of position, so next[] is computed for every byte in parallel and
+// walked by scalar code; hashes and bucket probes run per quad; the
+// "not one of the last two hits" filter is a scalar pass over the results.
+// Returns the end offset (reference `next`), or -1 on overflow.
+template <int CAP>
+__device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, int lane) {
+  using C = Cfg<CAP>;
+  const uint8_t* text = s.lbuf;
+  int start = 1;
+  if (text[start] == ' ') ++start;
+  for (int p = start + lane; p < limit; p += 64) {
+    int e = p;
+    e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+    int mid = e;
+    e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+    int nxt = (text[e] == ' ') ? e : mid;
+    if (nxt < limit) nxt += adv_space_vowel(text[nxt]);
+    else nxt = limit;
+    s.a.nxq[p] = (uint16_t)nxt;
+  }
+  wsync();
+  // scalar chain walk; chain entry i lives in lane i&63 of register i>>6
+  int cp[C::NR];
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) cp[r] = 0;
+  int n = 0, src = start;
+  while (src < limit) {
+    if (n >= C::NB) return -1;
+    put_lane(cp, n >> 6, n & 63, src);
+    ++n;
+    src = ufl(s.a.nxq[src]);
+  }
+  const int end = src;
+  // hashes and probes per chain entry
+  uint32_t h[C::NR], pr[C::NR];
+  bool hit[C::NR];
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) {
+    const int i = r * 64 + lane;
+    h[r] = 0; pr[r] = 0; hit[r] = false;
+    if (i < n) {
+      const int p = cp[r];
+      int e = p;
+      e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+      e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+      uint32_t hv = quad_hash_v2(text + p, e - p);
+      uint32_t probs = quad_lookup(T.quad, hv);
+      uint32_t ind = 0;
+      if (probs == 0 && T.quad2.size != 0) {
+        probs = quad_lookup(T.quad2, hv);
+        if (probs) ind = (probs & ~T.quad2.key_mask) | 0x80000000u;
+      } else if (probs) {
+        ind = probs & ~T.quad.key_mask;
+      }
+      h[r] = hv;
+      pr[r] = ind;
+      hit[r] = probs != 0;
+    }
+  }
+  // scalar repeat filter: drop a hit equal to either of the last two hits
+  uint64_t keep[C::NR];
+  uint64_t hitm[C::NR];
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) { keep[r] = 0; hitm[r] = __ballot(hit[r]); }
+  uint32_t pq0 = 0, pq1 = 0;
+  int npq = 0;
+  for (int i = 0; i < n; ++i) {
+    const int l = i & 63, r = i >> 6;
+    const uint32_t hv = rdlu(pick(h, r), l);
+    if (hv == pq0 || hv == pq1) continue;
+    const uint64_t hm = pick(hitm, r);
+    if (!((hm >> l) & 1)) continue;
+    if (npq == 0) pq0 = hv; else pq1 = hv;
+    npq ^= 1;
+    or_bit(keep, r, l);
+  }
+  int base = 0;
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) {
+    if ((keep[r] >> lane) & 1) {
+      const int k = base + __popcll(keep[r] & lanemask_lt(lane));
+      s.b_off[k] = (uint16_t)cp[r];
+      s.b_ind[k] = pr[r];
+    }
+    base += __popcll(keep[r]);
+  }
+  nb = base;
+  wsync();
+  return end;
+}
+
+// GetOctaHits (cldutil.cc:416-533): one lane per space-terminated word.
+template <int CAP>
+__device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int& nd, int& nx, int lane) {
+  using C = Cfg<CAP>;
+  const uint8_t* text = s.lbuf;
+  int start = 1;
+  if (text[start] == ' ') ++start;
+  const int lim = limit_next + 1;
+  // word-ending spaces, in order
+  int nw = 0;
+  for (int w0 = start; w0 < lim; w0 += 64) {
+    const int p = w0 + lane;
+    const bool sp = p < lim && text[p] == ' ';
+    const uint64_t m = __ballot(sp);
+    if (sp) {
+      int k = nw + __popcll(m & lanemask_lt(lane));
+      if (k < C::NB) s.a.wsp[k] = (uint16_t)p;
+    }
+    nw += __popcll(m);
+  }
+  if (nw > C::NB) return false;
+  wsync();
+  uint64_t wh[C::NR];
+  int ws[C::NR], pws[C::NR];
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) {
+    const int i = r * 64 + lane;
+    wh[r] = 0; ws[r] = 0; pws[r] = 0;
+    if (i < nw) {
+      const int a = i == 0 ? start : s.a.wsp[i - 1] + 1;
+      const int e = s.a.wsp[i];
+      int we = a, q = a, cc = 0;
+      while (q < e) {
+        ++cc;
+        q += utf8_len(text[q]);
+        if (cc <= 8) we = q;
+        else break;
+      }
+      ws[r] = a;
+      pws[r] = i <= 1 ? start : s.a.wsp[i - 2] + 1;
+      wh[r] = octa_hash40(text + a, we - a);
+    }
+  }
+  // scalar repeat filter (updates the pair partner even when probes miss)
+  uint64_t keep[C::NR];
+  uint32_t tlo[C::NR], thi[C::NR];
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) { keep[r] = 0; tlo[r] = 0; thi[r] = 0; }
+  uint64_t po0 = 0, po1 = 0;
+  int npo = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int l = i & 63, r = i >> 6;
+    const uint64_t v = rdl64(pick(wh, r), l);
+    if (v == po0 || v == po1) continue;
+    uint64_t tph;
+    if (npo == 0) { po0 = v; tph = po1; } else { po1 = v; tph = po0; }
+    npo ^= 1;
+    or_bit(keep, r, l);
+    put_lane(tlo, r, l, (uint32_t)tph);
+    put_lane(thi, r, l, (uint32_t)(tph >> 32));
+  }
+  // probes and ordered compaction: X gets (pair @ prior word, word @ word), D gets (word @ word)
+  int xb = 0, db = 0;
+  bool over = false;
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) {
+    uint32_t pp = 0, xp = 0, dp = 0;
+    const bool k = (keep[r] >> lane) & 1;
+    if (k) {
+      const uint64_t tph = ((uint64_t)thi[r] << 32) | tlo[r];
+      if (tph != 0 && tph != wh[r]) pp = octa_lookup(T.distinctocta, pair_hash(tph, wh[r]));
+      xp = octa_lookup(T.distinctocta, wh[r]);
+      dp = octa_lookup(T.deltaocta, wh[r]);
+    }
+    const int cx = (pp != 0) + (xp != 0), cd = (dp != 0);
+    const int ox = xb + excl_scan(cx, lane), od = db + excl_scan(cd, lane);
+    const int tx = rdl(ox + cx, 63) - xb, td = rdl(od + cd, 63) - db;
+    if (xb + tx > C::NX || db + td > C::ND) { over = true; break; }
+    int o = ox;
+    if (pp) { s.x_off[o] = (uint16_t)pws[r]; s.x_ind[o] = pp & ~T.distinctocta.key_mask; ++o; }
+    if (xp) { s.x_off[o] = (uint16_t)ws[r]; s.x_ind[o] = xp & ~T.distinctocta.key_mask; }
+    if (dp) { s.d_off[od] = (uint16_t)ws[r]; s.d_ind[od] = dp & ~T.deltaocta.key_mask; }
+    xb += tx; db += td;
+  }
+  if (over) return false;
+  nd = db; nx = xb;
+  wsync();
+  return true;
+}
+
+// GetUniHits + GetBiHits (cldutil.cc:201-310), one lane per character.
+template <int CAP>
+__device__ int cjk_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, int& nd, int& nx, int lane) {
+  using C = Cfg<CAP>;
+  const uint8_t* text = s.lbuf;
+  int start = 1;
+  if (text[start] == ' ') ++start;
+  int b = 0;
+  uint32_t endmax = (uint32_t)start;
+  for (int w0 = start; w0 < limit; w0 += 64) {
+    const int p = w0 + lane;
+    int prop = 0, len = 0;
+    if (p < limit && (text[p] & 0xC0) != 0x80) {
+      len = utf8_len(text[p]);
+      prop = uni_prop(T, text + p, len);
+      endmax = (uint32_t)(p + len) > endmax ? (uint32_t)(p + len) : endmax;
+    }
+    const uint64_t m = __ballot(prop > 0);
+    if (prop > 0) {
+      int k = b + __popcll(m & lanemask_lt(lane));
+      if (k < C::NB) { s.b_off[k] = (uint16_t)(p + len); s.b_ind[k] = (uint32_t)prop; }
+    }
+    b += __popcll(m);
+  }
+  if (b > C::NB) return -1;
+  const int next = (int)wmax(endmax);
+  // bigrams from offset 1 (no leading-space skip) to next
+  int dcount = 0, xcount = 0;
+  for (int w0 = 1; w0 < next; w0 += 64) {
+    const int p = w0 + lane;
+    uint32_t dp = 0, xp = 0;
+    if (p < next && (text[p] & 0xC0) != 0x80) {
+      const int len = utf8_len(text[p]);
+      const int len2 = utf8_len(text[p + len]) + len;
+      if (6 <= len2) {
+        const uint32_t bh = bi_hash_v2(text + p, len2);
+        dp = quad_lookup(T.deltabi, bh);
+        xp = quad_lookup(T.distinctbi, bh);
+      }
+    }
+    const uint64_t md = __ballot(dp != 0), mx = __ballot(xp != 0);
+    if (dp) {
+      int k = dcount + __popcll(md & lanemask_lt(lane));
+      if (k < C::ND) { s.d_off[k] = (uint16_t)p; s.d_ind[k] = dp & ~T.deltabi.key_mask; }
+    }
+    if (xp) {
+      int k = xcount + __popcll(mx & lanemask_lt(lane));
+      if (k < C::NX) { s.x_off[k] = (uint16_t)p; s.x_ind[k] = xp & ~T.distinctbi.key_mask; }
+    }
+    dcount += __popcll(md); xcount += __popcll(mx);
+  }
+  if (dcount > C::ND || xcount > C::NX) return -1;
+  nb = b; nd = dcount; nx = xcount;
+  wsync();
+  return next;
+}
+
+// ------------------------------------- stage 4: linearize + chunk + score
+// LinearizeAll/ChunkAll/ScoreAllHits (scoreonescriptspan.cc:856-1031, 208-302)
+// without materialising linear[]: every emitted langprob gets its chunk from
+// rank arithmetic.  Linear order is the seed, then (offset, delta < distinct <
+// base, index); chunk k closes after base-type emission E_k.
+template <int CAP>
+__device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool cjk, int nb, int nd, int nx,
+                            int dummy_off, int& ring_sel, int lane) {
+  using C = Cfg<CAP>;
+  const DevTbl& bo = cjk ? T.compat : T.quad;
+  const DevTbl& bo2 = cjk ? T.compat : T.quad2;
+  const DevTbl& dob = cjk ? T.deltabi : T.deltaocta;
+  const DevTbl& xob = cjk ? T.distinctbi : T.distinctocta;
+  const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
+
+  // base hits -> base emissions (1 or 2 langprobs each, zeros dropped), in order
+  int eb = 0;
+  for (int j0 = 0; j0 < nb; j0 += 64) {
+    const int j = j0 + lane;
+    uint32_t l1 = 0, l2 = 0;
+    int off = 0;
+    if (j < nb) {
+      off = s.b_off[j];
+      uint32_t ind = s.b_ind[j];
+      const DevTbl* lb = &bo;
+      if (ind & 0x80000000u) { lb = &bo2; ind &= ~0x80000000u; }
+      if (ind < lb->size_one) {
+        l1 = ind_at(*lb, ind);
+      } else {
+        ind += ind - lb->size_one;
+        l1 = ind_at(*lb, ind); l2 = ind_at(*lb, ind + 1);
+        if (l1 == 0) { l1 = l2; l2 = 0; }
+      }
+    }
+    const int c = (l1 != 0) + (l2 != 0);
+    const int o = eb + excl_scan(c, lane);
+    if (l1) { s.a.e.be_off[o] = (uint16_t)off; s.a.e.be_lp[o] = l1; }
+    if (l2) { s.a.e.be_off[o + 1] = (uint16_t)off; s.a.e.be_lp[o + 1] = l2; }
+    eb = rdl(o + c, 63);
+  }
+  // delta / distinct emissions
+  int ed = 0, ex = 0;
+  for (int j0 = 0; j0 < nd; j0 += 64) {
+    const int j = j0 + lane;
+    uint32_t lp = j < nd ? ind_at(dob, s.d_ind[j]) : 0u;
+    const int o = ed + excl_scan(lp != 0, lane);
+    uint16_t off = j < nd ? s.d_off[j] : 0;
+    if (lp) { s.d_off[o] = off; s.d_ind[o] = lp; }
+    ed = rdl(o + (lp != 0), 63);
+  }
+  for (int j0 = 0; j0 < nx; j0 += 64) {
+    const int j = j0 + lane;
+    uint32_t lp = j < nx ? ind_at(xob, s.x_ind[j]) : 0u;
+    const int o = ex + excl_scan(lp != 0, lane);
+    uint16_t off = j < nx ? s.x_off[j] : 0;
+    if (lp) { s.x_off[o] = off; s.x_ind[o] = lp; }
+    ex = rdl(o + (lp != 0), 63);
+  }
+  // chunk plan from the base-hit count (ChunkAll :978-1031)
+  int K = 0;
+  if (nb <= 0) {
+    K = 1;
+    if (lane == 0) s.E[0] = 0xFFFF;
+  } else {
+    int left = nb, e = 0;
+    while (left > 0) {
+      int blen = chunksize;
+      if (left < chunksize + (chunksize >> 1)) blen = left;
+      else if (left < 2 * chunksize) blen = (left + 1) >> 1;
+      e += blen;
+      if (lane == 0) s.E[K] = (uint16_t)e;
+      ++K;
+      left -= blen;
+    }
+    if (lane == 0) s.E[K - 1] = 0xFFFF;   // the last chunk takes everything that is left
+  }
+  // lo[k] = first (lowest) offset in chunk k; chunk 0 opens with the seed at `lowest` = 1
+  for (int k = lane; k < K; k += 64) s.lo[k] = k == 0 ? 1u : 0xFFFFFFFFu;
+  wsync();
+  // base emission t has base number t+2 (the seed is #1): chunk = min k with num <= E_k
+  for (int t = lane; t < eb; t += 64) {
+    const int num = t + 2;
+    int k = 0;
+    while (num > s.E[k]) ++k;
+    s.a.e.be_ch[t] = (uint8_t)k;
+    atomicMin(&s.lo[k], (uint32_t)s.a.e.be_off[t]);
+  }
+  // delta/distinct at offset o after m base emissions (m = 1 + #base emissions with offset < o):
+  // chunk = min k with m < E_k
+  for (int t = lane; t < ed + ex; t += 64) {
+    const bool isd = t < ed;
+    const int idx = isd ? t : t - ed;
+    const uint32_t o = isd ? s.d_off[idx] : s.x_off[idx];
+    int lo_i = 0, hi_i = eb;
+    while (lo_i < hi_i) {
+      int mid = (lo_i + hi_i) >> 1;
+      if ((uint32_t)s.a.e.be_off[mid] < o) lo_i = mid + 1; else hi_i = mid;
+    }
+    const int m = 1 + lo_i;
+    int k = 0;
+    while (m >= s.E[k]) ++k;
+    if (isd) s.d_ch[idx] = (uint8_t)k; else s.x_ch[idx] = (uint8_t)k;
+    atomicMin(&s.lo[k], o);
+  }
+  wsync();
+  // linear order starts with the seed at `lowest` (= 1 for the only round)
+  const uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
+  const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
+  ring_sel = rs;
+  // X emissions with chunk <= k, for the boosts (X is in linear order)
+  int xc = 0;
+  for (int k = 0; k < K; ++k) {
+    // zero the tote
+    reinterpret_cast<uint4*>(s.u.tote)[lane] = make_uint4(0, 0, 0, 0);
+    wsync();
+    uint64_t gm = 0;
+    int cnt = 0;
+    auto add = [&](uint32_t lp) {
+      const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
+      const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
+      if (k1) { atomicAdd(&s.u.tote[k1], (uint32_t)e[5]); gm |= 1ull << (k1 >> 2); }
+      if (k2) { atomicAdd(&s.u.tote[k2], (uint32_t)e[6]); gm |= 1ull << (k2 >> 2); }
+      if (k3) { atomicAdd(&s.u.tote[k3], (uint32_t)e[7]); gm |= 1ull << (k3 >> 2); }
+    };
+    if (k == 0 && lane == 0) { add(seed); ++cnt; }
+    for (int t = lane; t < eb; t += 64)
+      if (s.a.e.be_ch[t] == k) { add(s.a.e.be_lp[t]); ++cnt; }
+    for (int t = lane; t < ed; t += 64)
+      if (s.d_ch[t] == k) add(s.d_ind[t]);
+    int xin = 0;
+    for (int t = lane; t < ex; t += 64)
+      if (s.x_ch[t] <= k) { ++xin; if (s.x_ch[t] == k) add(s.x_ind[t]); }
+    xc = wsum(xin);
+    // boosts: the last four distinct langprobs up to the end of this chunk
+    if (lane < 4) {
+      const int u = xc + lane;
+      const uint32_t lp = u < 4 ? s.ring[rs][u] : s.x_ind[u - 4];
+      if (lp > 0) add(lp);
+    }
+    gm = wor64(gm);
+    const int score_count = wsum(cnt);
+    wsync();
+    // top three keys of the in-use groups: (score desc, key asc)
+    const uint4 v4 = reinterpret_cast<const uint4*>(s.u.tote)[lane];
+    const bool inuse = (gm >> lane) & 1;
+    uint32_t cand[4] = {v4.x & 0xFFFF, v4.y & 0xFFFF, v4.z & 0xFFFF, v4.w & 0xFFFF};
+    int key3[3] = {-1, -1, -1};
+    uint32_t sc3[3] = {0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      uint32_t best = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = lane * 4 + i;
+        const bool taken = key == key3[0] || key == key3[1];
+        const uint32_t comp = (inuse && !taken) ? ((cand[i] + 1) << 8) | (uint32_t)(255 - key) : 0u;
+        best = comp > best ? comp : best;
+      }
+      best = wmax(best);
+      if (best) { key3[r] = 255 - (int)(best & 0xFF); sc3[r] = (best >> 8) - 1; }
+    }
+    if (lane == 0) {
+      const uint32_t lo_k = s.lo[k];
+      const int lo = lo_k == 0xFFFFFFFFu ? dummy_off : (int)lo_k;
+      int hi = dummy_off;
+      if (k + 1 < K && s.lo[k + 1] != 0xFFFFFFFFu) hi = (int)s.lo[k + 1];
+      const int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
+      const int lang2 = from_per_script_number(T, ulscript, (uint8_t)key3[1]);
+      const int len = hi - lo;
+      const int sc1 = key3[0] >= 0 ? (int)sc3[0] : 0;
+      const int sc2 = key3[1] >= 0 ? (int)sc3[1] : 0;
+      int actual = 0;
+      if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
+      const int esub = lang1 * 4 + lscript4(T, ulscript);
+      const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+      const uint16_t bytes = (uint16_t)len, grams = (uint16_t)score_count;
+      const uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
+      int rd = (uint8_t)reliability_delta(s1, s2, grams);
+      const int cs1 = close_set(T, lang1);
+      if (cs1 != 0 && cs1 == close_set(T, lang2)) rd = 100;
+      const int rsc = (uint8_t)reliability_expected(actual, expected);
+      if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
+    }
+    wsync();
+  }
+  // the ring keeps the last four distinct langprobs
+  if (lane == 0) {
+    uint32_t r4[4];
+    for (int i = 0; i < 4; ++i) {
+      const int u = ex + i;
+      r4[i] = u < 4 ? s.ring[rs][u] : s.x_ind[u - 4];
+    }
+    for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
+  }
+  wsync();
+}
+
+// ------------------------------------------------------ the document
+template <int CAP>
+__device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
+                       cld_result* __restrict__ out, unsigned long long* __restrict__ prof) {
+  // optional per-stage cycle accounting (CLD_PROFILE_STAGES=1): 0 load, 1 span,
+  // 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level
+  long long t_stage = prof ? (long long)clock64() : 0;
+  auto mark = [&](int st) {
+    if (prof) {
+      long long t = (long long)clock64();
+      if (lane == 0) atomicAdd(&prof[st], (unsigned long long)(t - t_stage));
+      t_stage = t;
+    }
+  };
+  const int unk = (int)T.unknown_lang;
+  if (L == 0) {
+    if (lane == 0) {
+      Extract x;
+      for (int i = 0; i < 3; ++i) { x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; x.rp3[i] = 0; }
+      x.text_bytes = 0;
+      write_result(out, x, unk, false);
+    }
+    return true;
+  }
+  if (!load_document<CAP>(T, g, L, s, lane)) return false;
+  mark(0);
+  if (lane == 0) s.dt.init();
+  if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
+  wsync();
+  int next = 0, total = 0;
+  for (;;) {
+    int ulscript = 0;
+    int tb = next_span<CAP>(T, s, L, next, ulscript, lane);
+    mark(1);
+    if (tb == 0) break;
+    tb = lower_span<CAP>(T, s, tb, lane);
+    mark(2);
+    if (tb < 0) return false;
+    const int rt = rtype_of(T, ulscript);
+    if (rt == RTypeNone || rt == RTypeOne) {
+      if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
+      wsync();
+    } else {
+      const bool cjk = rt == RTypeCJK;
+      int nb = 0, nd = 0, nx = 0, endo;
+      if (cjk) {
+        endo = cjk_hits<CAP>(T, s, tb, nb, nd, nx, lane);
+        mark(3);
+        if (endo < 0) return false;
+      } else {
+        endo = quad_hits<CAP>(T, s, tb, nb, lane);
+        mark(3);
+        if (endo < 0) return false;
+        if (!octa_hits<CAP>(T, s, endo, nd, nx, lane)) return false;
+        mark(4);
+      }
+      if (endo < tb) return false;     // a second round would be needed (never for short documents)
+      int rsel;
+      if (1 < tb) score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane);
+      mark(5);
+    }
+    total += tb;
+  }
+  // document level (compact_lang_det_impl.cc:1997-2065), lane 0
+  int ok = 1;
+  if (lane == 0) {
+    DocTote& dt = s.dt;
+    refine_scored_close_pairs(T, dt);
+    dt.sort3();
+    Extract x;
+    extract_lang_etc(T, dt, total, x);
+    const bool good = total <= 256 || (x.reliable && x.pct3[0] >= 70) || (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
+    if (!good) {
+      ok = 0;
+    } else {
+      remove_unreliable_languages(T, dt);
+      dt.sort3();
+      extract_lang_etc(T, dt, total, x);
+      bool rel;
+      const int summary = calc_summary_lang(T, total, x, rel);
+      write_result(out, x, summary, rel);
+    }
+  }
+  mark(6);
+  return rdl(ok, 0) != 0;
+}
+
+}  // namespace wave
+}  // namespace cld
