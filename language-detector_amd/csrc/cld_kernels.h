@@ -12,6 +12,8 @@ constexpr int kShortCap = 256;
 // Wavefront-per-document bucket (cld_wave.hip)
 constexpr int kWaveCap = 256;
 constexpr int kWaveWPB = 4;
+// Largest kLgProbV2Tbl score byte the packed wave tote accepts (runtime checks the blob)
+constexpr int kMaxLgProbScore = 16;
 constexpr int kShortSB = 2 * kShortCap + 64;
 constexpr int kShortLB = kShortSB * 3 / 2 + 64;
 constexpr int kShortHB = kShortCap + 32;

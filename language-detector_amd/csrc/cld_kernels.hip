@@ -7,9 +7,9 @@
 //  k_general     any document, all passes, per-lane state in a global arena;
 //                persistent grid pulling documents from the re-queue list
 //                with one atomic dequeue per document.
+#include "cld_kernels.h"
 #include "cld_pipeline.hip"
 #include "cld_wave.hip"
-#include "cld_kernels.h"
 
 namespace cld {
 
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
 
 // One wavefront per document of <= CAP bytes, WPB documents per workgroup.
 template <int CAP, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64 * WPB, 6) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
                                                    const uint64_t* __restrict__ offs, int n,
                                                    cld_result* __restrict__ out,
                                                    uint32_t* __restrict__ requeue_list,

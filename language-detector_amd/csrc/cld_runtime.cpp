@@ -146,6 +146,15 @@ int load_tables(const char* path, HostTables* t) {
     *s.dst = at<const void*>(off);
     if (s.count) *s.count = (uint32_t)(size / s.elem);
   }
+  {  // the wavefront kernel's packed tote relies on small score bytes (kMaxLgProbScore)
+    if (!section(t->blob, CLDT_LGPROB, &off, &size) || size % 8 || off % 4) return CLD_EINVAL;
+    for (uint64_t r = 0; r < size; r += 8)
+      for (int k = 5; k < 8; ++k)
+        if (t->blob[off + r + k] > kMaxLgProbScore) {
+          fprintf(stderr, "cld_mi355x: kLgProbV2Tbl score %d exceeds %d\n", t->blob[off + r + k], kMaxLgProbScore);
+          return CLD_EINVAL;
+        }
+  }
   const cldt_meta& M = t->meta;
   D.latin = M.ulscript_latin; D.cyrillic = M.ulscript_cyrillic; D.arabic = M.ulscript_arabic;
   D.common = M.ulscript_common; D.inherited = M.ulscript_inherited;

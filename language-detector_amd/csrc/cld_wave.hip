@@ -119,12 +119,17 @@ struct Cfg {
   static constexpr int LB = (SB * 3) / 2 + 64;      // lowered span (max per-char growth 1.5x) + hash read pad
   static constexpr int NR = 2;                      // registers of 64 entries: quad chain, words
   static constexpr int NB = NR * 64;                // base hits / quad chain / words
-  static constexpr int NE = 2 * NB;                 // base emissions (<= 2 langprobs per hit)
+  static constexpr int NE = 160;                    // base emissions (<= 2 langprobs per hit; overflow requeues)
   static constexpr int ND = 96;
   static constexpr int NX = 160;
   static constexpr int MAXCH = NE / kChunksizeQuads + 3;
   static_assert(NB < kMaxScoringHits - 1, "a round must never reach the reference's hit cap");
   static_assert(CAP < 2048, "spans of a short document can never reach the squeeze test");
+  // Packed tote (kToteNoCarry): a key's 16-bit half can neither wrap nor
+  // carry into its neighbour when every add is <= kMaxLgProbScore (the host
+  // checks the table at load) and a chunk holds at most NE + ND + NX + 1
+  // emissions plus 4 boosts.
+  static_assert((NE + ND + NX + 5) * kMaxLgProbScore < 65536, "tote headroom");
 };
 
 template <int CAP>
@@ -136,7 +141,7 @@ struct Smem {
   uint64_t brk[C::NM];                // letters that end a run for the current span script
   union alignas(16) {
     uint8_t sbuf[C::SB];              // span text (raw)
-    uint32_t tote[256];               // chunk tote, u32 per key (low 16 bits == reference uint16)
+    uint32_t tote[128];               // chunk tote: two 16-bit keys per word (see kToteNoCarry)
   } u;
   uint8_t lbuf[C::LB];                // lowered span text
   union alignas(16) {                 // stage-local arrays
@@ -635,7 +640,7 @@ __device__ int cjk_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, in
 // rank arithmetic.  Linear order is the seed, then (offset, delta < distinct <
 // base, index); chunk k closes after base-type emission E_k.
 template <int CAP>
-__device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool cjk, int nb, int nd, int nx,
+__device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int dummy_off, int& ring_sel, int lane) {
   using C = Cfg<CAP>;
   const DevTbl& bo = cjk ? T.compat : T.quad;
@@ -665,9 +670,10 @@ __device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     }
     const int c = (l1 != 0) + (l2 != 0);
     const int o = eb + excl_scan(c, lane);
+    eb = rdl(o + c, 63);
+    if (eb > C::NE) return false;
     if (l1) { s.a.e.be_off[o] = (uint16_t)off; s.a.e.be_lp[o] = l1; }
     if (l2) { s.a.e.be_off[o + 1] = (uint16_t)off; s.a.e.be_lp[o + 1] = l2; }
-    eb = rdl(o + c, 63);
   }
   // delta / distinct emissions
   int ed = 0, ex = 0;
@@ -742,16 +748,17 @@ __device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   int xc = 0;
   for (int k = 0; k < K; ++k) {
     // zero the tote
-    reinterpret_cast<uint4*>(s.u.tote)[lane] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint2*>(s.u.tote)[lane] = make_uint2(0, 0);
     wsync();
     uint64_t gm = 0;
     int cnt = 0;
+    // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row
     auto add = [&](uint32_t lp) {
-      const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
+      const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
       const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
-      if (k1) { atomicAdd(&s.u.tote[k1], (uint32_t)e[5]); gm |= 1ull << (k1 >> 2); }
-      if (k2) { atomicAdd(&s.u.tote[k2], (uint32_t)e[6]); gm |= 1ull << (k2 >> 2); }
-      if (k3) { atomicAdd(&s.u.tote[k3], (uint32_t)e[7]); gm |= 1ull << (k3 >> 2); }
+      if (k1) { atomicAdd(&s.u.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
+      if (k2) { atomicAdd(&s.u.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
+      if (k3) { atomicAdd(&s.u.tote[k3 >> 1], (e >> 24) << ((k3 & 1) * 16)); gm |= 1ull << (k3 >> 2); }
     };
     if (k == 0 && lane == 0) { add(seed); ++cnt; }
     for (int t = lane; t < eb; t += 64)
@@ -772,9 +779,9 @@ __device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     const int score_count = wsum(cnt);
     wsync();
     // top three keys of the in-use groups: (score desc, key asc)
-    const uint4 v4 = reinterpret_cast<const uint4*>(s.u.tote)[lane];
+    const uint2 v2 = reinterpret_cast<const uint2*>(s.u.tote)[lane];
     const bool inuse = (gm >> lane) & 1;
-    uint32_t cand[4] = {v4.x & 0xFFFF, v4.y & 0xFFFF, v4.z & 0xFFFF, v4.w & 0xFFFF};
+    uint32_t cand[4] = {v2.x & 0xFFFF, v2.x >> 16, v2.y & 0xFFFF, v2.y >> 16};
     int key3[3] = {-1, -1, -1};
     uint32_t sc3[3] = {0, 0, 0};
 #pragma unroll
@@ -824,6 +831,7 @@ __device__ void score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
   wsync();
+  return true;
 }
 
 // ------------------------------------------------------ the document
@@ -884,7 +892,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       }
       if (endo < tb) return false;     // a second round would be needed (never for short documents)
       int rsel;
-      if (1 < tb) score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane);
+      if (1 < tb && !score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane)) return false;
       mark(5);
     }
     total += tb;
