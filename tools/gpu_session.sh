@@ -21,7 +21,7 @@ run() {  # run <seconds> <log> cmd...
 }
 for s in $STEPS; do
   case $s in
-    test)  run 900 pytest_gpu.log python -m pytest tests -m gpu -x -q -rA --durations=15 ;;
+    test)  run 900 pytest_gpu.log python -u -m pytest tests -m gpu -x -v -rA --durations=15 --timeout 300 --timeout-method thread ;;
     smoke) run 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 400 bench_c2.log python bench.py ;;
     benchall)
