@@ -61,7 +61,8 @@ int cld_init_device(const char* tables_path, int device);
 int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts);
 
 /* Sum of kernel durations (HIP events on the stream the kernels ran on) of
- * every batch enqueued on context `ctx` since the previous call; resets. */
+ * every batch enqueued on context `ctx` since the previous call; resets.
+ * short_ms = wavefront kernel; general_ms = long-document + sequential kernels. */
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
 /* Diagnostics: per-stage shader-clock cycle sums of the wavefront kernel on
@@ -95,10 +96,14 @@ const char* cld_language_name(int lang);
 /* Counters of the most recent batch on this thread's last device call. */
 typedef struct cld_batch_stats {
   uint64_t docs;
-  uint64_t short_docs;       /* finished by the short-document kernel          */
-  uint64_t general_docs;     /* handled by the general (any length) kernel     */
-  uint64_t passes[4];        /* documents needing 1, 2, 3 passes               */
-  double short_ms, general_ms; /* kernel time from HIP events                  */
+  uint64_t short_docs;       /* finished by the short-document (wavefront) kernel */
+  uint64_t general_docs;     /* finished by the sequential any-length kernel      */
+  uint64_t passes[4];        /* documents needing 1, 2, 3 passes; [3] = errors     */
+  double short_ms, general_ms; /* kernel time from HIP events                     */
+  uint64_t long_docs;        /* finished by the long-document wavefront kernel    */
+  double long_ms;
+  uint64_t long_requeue[8];  /* why k_long handed documents on: 1 length, 2 scanner
+                                state, 3 span/lowercase, 4 Squeeze restart, 5 capacity */
 } cld_batch_stats;
 int cld_last_batch_stats(int device, cld_batch_stats* st);
 

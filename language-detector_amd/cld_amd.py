@@ -29,7 +29,9 @@ EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cl
 
 class BatchStats(ctypes.Structure):
     _fields_ = [("docs", ctypes.c_uint64), ("short_docs", ctypes.c_uint64), ("general_docs", ctypes.c_uint64),
-                ("passes", ctypes.c_uint64 * 4), ("short_ms", ctypes.c_double), ("general_ms", ctypes.c_double)]
+                ("passes", ctypes.c_uint64 * 4), ("short_ms", ctypes.c_double), ("general_ms", ctypes.c_double),
+                ("long_docs", ctypes.c_uint64), ("long_ms", ctypes.c_double),
+                ("long_requeue", ctypes.c_uint64 * 8)]
 
 
 class CldError(RuntimeError):

@@ -19,8 +19,12 @@ constexpr int kShortLB = kShortSB * 3 / 2 + 64;
 constexpr int kShortHB = kShortCap + 32;
 
 // Device counter slots (one 64-byte line, zeroed per batch)
+// kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general.
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
+       kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
        kCtrSlots = 16 };
+// k_long: waves per workgroup
+constexpr int kLongWPB = 4;
 
 extern "C" {
 size_t cld_general_work_bytes();
@@ -34,6 +38,12 @@ hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64
                             hipStream_t s);
 hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
-                              uint64_t stride, int lanes, uint32_t* counters, hipStream_t s);
+                              uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
+                              hipStream_t s);
+size_t cld_long_slot_bytes();
+hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
+                           uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
+                           hipStream_t s);
 }
 #endif

@@ -4,12 +4,17 @@
 //                memory, pass 1 only.  Anything it cannot finish (longer
 //                document, Squeeze restart, Repeats pass, capacity) is
 //                appended to the re-queue list.
+//  k_wave<CAP>   one wavefront per document of <= CAP bytes, state in LDS.
+//  k_long        one wavefront per document of any length up to lng::kDocCap,
+//                per-wave slot in HBM; persistent grid over the wave kernel's
+//                re-queue list.
 //  k_general     any document, all passes, per-lane state in a global arena;
 //                persistent grid pulling documents from the re-queue list
 //                with one atomic dequeue per document.
 #include "cld_kernels.h"
 #include "cld_pipeline.hip"
 #include "cld_wave.hip"
+#include "cld_long.hip"
 
 namespace cld {
 
@@ -44,12 +49,12 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
                                                const uint32_t* __restrict__ list,
                                                cld_result* __restrict__ out,
                                                uint8_t* __restrict__ arena, uint64_t stride,
-                                               uint32_t* __restrict__ counters) {
+                                               uint32_t* __restrict__ counters, int ctr_count, int ctr_deq) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
-  const uint32_t total = __hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (;;) {
-    uint32_t k = atomicAdd(&counters[kCtrDequeue], 1u);
+    uint32_t k = atomicAdd(&counters[ctr_deq], 1u);
     if (k >= total) break;                       // every lane reaches this exit
     const uint32_t i = list[k];
     const uint64_t a = offs[i], b = offs[i + 1];
@@ -83,9 +88,75 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_wave(DevTables T, const uint8_t
   }
 }
 
+// One wavefront per long document, persistent: each wave owns slot
+// blockIdx.x * WPB + wave and pulls documents from the wave kernel's re-queue
+// list (one atomic per document) until the list is drained -- every wave
+// reaches that exit.  Documents it cannot reproduce go to the k_general list.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_long(DevTables T, const uint8_t* __restrict__ buf,
+                                                  const uint64_t* __restrict__ offs,
+                                                  const uint32_t* __restrict__ list,
+                                                  cld_result* __restrict__ out, uint8_t* __restrict__ slots,
+                                                  uint32_t* __restrict__ requeue2,
+                                                  uint32_t* __restrict__ counters, uint32_t* trace,
+                                                  uint32_t* dbg, uint32_t dbg_doc) {
+  __shared__ lng::Smem smem[WPB];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t* tr = trace ? trace + 4 * (blockIdx.x * WPB + wv) : nullptr;
+  lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::Slot));
+  const uint32_t total =
+      wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
+  const bool exact = lng::space_lowers_to_space(T);
+  lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
+  for (;;) {
+    // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
+    // A lane-0-only atomic feeding readfirstlane at the loop head let the
+    // compiler split the loop so the other lanes re-read k = 0 forever.
+    const uint32_t k = wave::uflu(atomicAdd(&counters[kCtrDequeue], lane == 0 ? 1u : 0u));
+    if (k >= total) break;
+    const uint32_t i = list[k];
+    const uint64_t a = offs[i], b = offs[i + 1];
+    const uint64_t len = b - a;
+    int passes = 0;
+    if (lane == 0) {
+      smem[wv].dbg = (dbg && i == dbg_doc) ? dbg : nullptr;
+      smem[wv].dbg_pos = 0;
+    }
+    wave::wsync();
+    if (exact && len <= (uint64_t)lng::kDocCap)
+      passes = lng::detect(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i);
+    lng::trace(tr, lane, i, 99, passes);
+    passes = wave::ufl(passes);
+    if (lane == 0) {
+      if (passes >= 1 && passes <= 2) {
+        atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
+      } else {
+        const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);
+        requeue2[q] = i;
+        atomicAdd(&counters[kCtrWhy + min(max(-passes, 0), 7)], 1u);
+      }
+    }
+  }
+  lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
+}
+
 }  // namespace cld
 
 extern "C" {
+size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }
+
+hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
+                           uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
+                           hipStream_t s) {
+  if (n_slots < kLongWPB) return hipErrorInvalidValue;
+  dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
+  hipLaunchKernelGGL((cld::k_long<kLongWPB>), grid, block, 0, s, *T, buf, offs, list, out, slots, requeue2,
+                     counters, trace, dbg, dbg_doc);
+  return hipGetLastError();
+}
+
 size_t cld_general_work_bytes() { return sizeof(cld::GeneralWork); }
 size_t cld_short_work_bytes() { return sizeof(cld::ShortWork); }
 size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
@@ -111,10 +182,11 @@ hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64
 
 hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
-                              uint64_t stride, int lanes, uint32_t* counters, hipStream_t s) {
+                              uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
+                              hipStream_t s) {
   dim3 grid(lanes / 64), block(64);
   hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, *T, buf, offs, list, out, arena, stride,
-                     counters);
+                     counters, ctr_count, ctr_deq);
   return hipGetLastError();
 }
 }

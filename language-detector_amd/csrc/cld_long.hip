@@ -1,0 +1,1264 @@
+// cld_long.hip -- one wavefront per document of any length up to kDocCap (k_long).
+//
+// The wavefront kernel (cld_wave.hip) keeps a <=256-byte document in LDS.
+// Longer documents -- multi-span pages, 1000-hit rounds, the Repeats pass --
+// run here: the 64 lanes still share one document, but the per-span buffers
+// (lowered text up to the reference's 61,440 bytes, word lists, quad chain,
+// hit and emission streams, the 4096-entry predictor) sit in a per-wave slot
+// in HBM that stays L2/MALL resident while the wave works on it; LDS holds the
+// chunk tote, chunk plan and DocTote.
+//
+//   stage                              reference                         across lanes
+//   per-byte script/scanner classes    getonescriptspan.cc:480-485,      bytes; checked to be a per-
+//                                      utf8statetable.cc:362-554         character (local) formulation
+//   GetOneScriptSpan + LowerScriptSpan getonescriptspan.cc:799-1054      bytes: run/gap state from the
+//     (fused)                                                            last break / letter-stop event
+//                                                                        (ballot masks), per-char lowering,
+//                                                                        prefix-sum compaction; soft/hard
+//                                                                        span limits from prefix sums
+//   CheapSqueezeTriggerTest            compact_lang_det_impl.cc:952-971  chars (predictor below)
+//   CheapRepWordsInplace (pass 2)      compact_lang_det_impl.cc:610-692  chars: 12-bit hash from the last
+//                                                                        three chars, equal hashes inside a
+//                                                                        window matched by 12 ballots;
+//                                                                        segment sums; compaction
+//   GetQuadHits                        cldutil.cc:315-405                the chain enters every word at its
+//                                                                        first byte: one lane walks one
+//                                                                        word; hashes/probes per entry; the
+//                                                                        last-two-hits filter by ballot with a
+//                                                                        scalar resolve on conflict; 1000 cut
+//   GetOctaHits                        cldutil.cc:416-533                words; same filter scheme; caps
+//   GetUniHits / GetBiHits             cldutil.cc:201-310                chars
+//   LinearizeAll/ChunkAll/ScoreAllHits scoreonescriptspan.cc:856-1031,   chunk k = contiguous range of each
+//                                      208-302                           stream (rank arithmetic); LDS tote
+//   DocTote / summary                  tote.cc, compact_lang_det_impl    lane 0
+//
+// Anything this formulation cannot reproduce exactly (a document longer than
+// kDocCap, a non-local scanner/lowercaser state, the Squeeze restart, a
+// capacity overflow) is appended to the next re-queue list and redone by
+// k_general from scratch.
+
+namespace cld {
+namespace lng {
+
+using wave::excl_scan;
+using wave::lower_char;
+using wave::lanemask_lt;
+using wave::rdl;
+using wave::rdl64;
+using wave::rdlu;
+using wave::ufl;
+using wave::ufl64;
+using wave::uflu;
+using wave::wor64;
+using wave::wsum;
+using wave::wsync;
+
+constexpr int kDocCap = 69632;                       // longest document taken (C5 caps at 64 KB)
+constexpr int kLB = kMaxScriptLowerBuffer + 256;     // lowered span + pads + hash read slack
+constexpr int kDocWords = kDocCap / 64 + 2;
+constexpr int kSpanWords = kLB / 64 + 1;
+constexpr int kListCap = kLB / 2;                    // words / spaces / chain entries per span
+constexpr int kHB = 1024;                            // hits per round (reference: <= 1000)
+constexpr int kEB = 2048;                            // base emissions per round (<= 2 per hit)
+constexpr int kMaxCh = 64;                           // chunks per round (<= 50 + 1)
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+
+// Per-wave working set in HBM (one per resident wavefront of the persistent grid).
+struct Slot {
+  uint32_t epoch;
+  uint32_t pad_[31];
+  uint64_t pred[kPredictionTableSize];   // predictor: (epoch << 32) | last char after hash h
+  uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
+  uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats)
+  uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces
+  uint8_t sn[kDocCap + 128];             // GetUTF8LetterScriptNum per document byte
+  uint8_t lb[2][kLB];                    // lowered span text; [1] = after CheapRepWords
+  uint16_t wst[kListCap];                // quad chain entry points (word starts)
+  uint16_t wsp[kListCap];                // word-ending spaces (octa words)
+  uint16_t chain[kListCap];              // quad chain of the span
+  uint16_t b_off[kHB];
+  uint32_t b_ind[kHB];
+  uint16_t d_off[kHB];
+  uint32_t d_ind[kHB];
+  uint16_t x_off[kHB];
+  uint32_t x_ind[kHB];
+  uint16_t be_off[kEB];
+  uint32_t be_lp[kEB];
+};
+
+// Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4)
+struct alignas(16) Smem {
+  uint32_t tote[256];                    // chunk tote, one key per word (uint16 wrap applied at read)
+  int32_t theta[kMaxCh];                 // chunk k takes delta/distinct emissions with offset <= theta_k
+  uint32_t lo[kMaxCh];                   // first offset of chunk k
+  uint16_t E[kMaxCh];                    // base emission number closing chunk k
+  uint16_t bst[kMaxCh + 1];
+  uint16_t st[2][kMaxCh + 1];            // first delta [0] / distinct [1] emission of chunk k
+  uint32_t ring[2][4];                   // distinct boosts, latn / othr, oldest first
+  DocTote dt;
+  uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
+  uint32_t dbg_pos;
+};
+
+// Debug dump records (u32 words): 'S' span {ul, tb, pass}; 'R' round {off, next,
+// nb, nd, nx, then nb+nd+nx (offset, indirect) pairs}; 'C' chunk {lo, hi, lang1,
+// lang2, score1, score2, grams, rel_delta, rel_score}.
+__device__ void dbg_words(Smem& s, int lane, const uint32_t* v, int n) {
+  if (!s.dbg) return;
+  if (lane == 0) {
+    for (int i = 0; i < n; ++i) s.dbg[1 + s.dbg_pos + i] = v[i];
+    s.dbg_pos += n;
+    s.dbg[0] = s.dbg_pos;
+  }
+  wave::wsync();
+}
+
+// Debug trace (CLD_TRACE=1): lane 0 of each wave stores (document, stage,
+// value) into pinned host memory so a stuck batch names its document.
+__device__ __forceinline__ void trace(uint32_t* tr, int lane, uint32_t doc, uint32_t stage, uint32_t v) {
+  const uint64_t act = __ballot(1);
+  if (tr && lane == __builtin_ctzll(act)) {
+    __hip_atomic_store(&tr[0], doc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&tr[1], stage | ((uint32_t)__popcll(act) << 16) | ((uint32_t)lane << 24), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&tr[2], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&tr[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__device__ __forceinline__ int topbit(uint64_t m) { return 63 - __builtin_clzll(m); }
+__device__ __forceinline__ uint64_t mask_le(int lane) { return lane >= 63 ? ~0ull : ((2ull << lane) - 1); }
+__device__ __forceinline__ int nth_bit(uint64_t m, int n) {
+  for (int i = 0; i < n; ++i) m &= m - 1;
+  return __builtin_ctzll(m);
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int l) { return (uint32_t)__shfl((int)v, l, 64); }
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
+  return ((uint64_t)shfl32((uint32_t)(v >> 32), l) << 32) | shfl32((uint32_t)v, l);
+}
+// Orders global-memory traffic between the lanes of one wavefront (the slot
+// is private to the wave; workgroup scope = same CU, same L1).
+__device__ __forceinline__ void gsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// First set bit at or after `from` in a bitmask over positions [0, L); L if none.
+__device__ int find_first_g(const uint64_t* m, int from, int L) {
+  from = ufl(from);
+  if (from >= L) return L;
+  int w = from >> 6;
+  uint64_t x = ufl64(m[w]) & (~0ull << (from & 63));
+  for (;;) {
+    if (x) {
+      const int r = (w << 6) + __builtin_ctzll(x);
+      return r < L ? r : L;
+    }
+    ++w;
+    if ((w << 6) >= L) return L;
+    x = ufl64(m[w]);
+  }
+}
+
+// ----------------------------------------------------- stage 0: classify
+// ScanToLetterOrSpecial (getonescriptspan.cc:480-485, utf8statetable.cc:460-554)
+// as a per-character property: from state 0 the character either exits on its
+// first byte (the scan stops here: 1), or on a later byte from a non-zero state
+// (the reference backs up to the lead byte: 1), or returns to state 0 after its
+// last byte (the scan continues with the next character: 0).  Anything else
+// (-1) makes the sequential scan depend on earlier characters.
+// A character cut by the end of the document (`cut`) runs out of input
+// instead: the scan ends there, and unless it is back in state 0 it backs up
+// to the lead byte (a stop), exactly as at :538-546.
+__device__ int scan_char(const DevTables& T, const DocView& d, int p, int n, bool cut) {
+  const DevSM& sm = T.scan;
+  const int64_t tb0 = sm.state0;
+  int64_t tb = tb0;
+  for (int k = 0; k < n; ++k) {
+    const int e = sm8(sm, tb + d.at(p + k));
+    if (e >= kExitIllegalStructure) {
+      if (e == kExitDoAgain) return -1;
+      if (k == 0) return 1;
+      return in_state_zero(sm, tb) ? -1 : 1;
+    }
+    tb = tb0 + ((int64_t)e << sm.shift);
+  }
+  if (cut) return in_state_zero(sm, tb) ? (tb == tb0 ? 0 : -1) : 1;
+  return tb == tb0 ? 0 : -1;
+}
+
+// Script number per byte (also the 4 NUL bytes after the end, as DocView
+// reads them) and the letter-stop mask; false if the document does not tile
+// into well-formed characters with local scanner behaviour.
+__device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lane) {
+  const int L = dv.len;
+  int bad = 0, conts = 0, need = 0;
+  const int nw = (L + 4 + 63) >> 6;
+  for (int w = 0; w < nw; ++w) {
+    const int p = (w << 6) + lane;
+    bool ls = false;
+    int sn = 0;
+    if (p < L + 4) sn = script_num(T, dv, p);
+    if (p < L) {
+      const uint8_t c = dv.at(p);
+      if ((c & 0xC0) == 0x80) {
+        ++conts;
+      } else {
+        const int n = utf8_len(c);
+        const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
+        for (int k = 1; k < avail; ++k) bad |= ((dv.at(p + k) & 0xC0) != 0x80);
+        need += avail - 1;
+        const int st = scan_char(T, dv, p, avail, avail < n);
+        if (st < 0) bad = 1;
+        ls = st > 0 && sn != 0;
+      }
+    }
+    if (p < L + 4) S.sn[p] = (uint8_t)sn;
+    const uint64_t m = __ballot(ls);
+    if (lane == 0) S.lsm[w] = m;
+  }
+  bad |= (wsum(conts) != wsum(need)) ? 1 : 0;
+  gsync();
+  return __ballot(bad != 0) == 0;
+}
+
+// --------------------------------------- stage 1: span text, lowered (fused)
+// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) followed by
+// LowerScriptSpan (:1033-1054).  Span text = ' ' + run + ' ' + run + ' ' ...
+// A run starts at a letter stop of the span script (or Inherited) and ends at
+// the first break character; the gap after it runs to the next letter stop,
+// which continues the span (span script / Inherited) or ends it.  Within a
+// 64-byte window every byte's state is the type of the last event at or
+// before it (break -> gap, continuing letter stop -> run), so all lanes decide
+// at once.  The soft limit (put >= put_soft_limit after a run's space) and the
+// hard limit (put >= kMaxScriptBytes after a character) come from prefix sums
+// of the raw byte count.  The characters go straight through the lowercaser
+// (each one starts and ends in state 0, checked) into lb.
+// A final character cut by the document end that lands in a run is copied
+// with NUL bytes (DocView), and the lowercaser stops at its lead byte; that
+// tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
+// status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
+__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
+                         int& status, int lane) {
+  const int L = dv.len;
+  const int common = (int)T.common, inherited = (int)T.inherited;
+  const int remaining = L - next;
+  int soft = kMaxScriptBytes - kWithinScriptTail;
+  if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) soft = remaining / 2;
+  const int q = find_first_g(S.lsm, next, L);
+  status = 1;
+  if (q >= L) {
+    next = L;
+    status = 0;
+    return 0;
+  }
+  const int ss = ufl(S.sn[q]);
+  ulscript = ss;
+  if (lane == 0) lb[0] = ' ';
+  int lpos = 1, put = 1, grow = 0, bad = 0, nxt = L;
+  bool run = false, cut = false;
+  for (int w = q >> 6;; ++w) {
+    const int x = (w << 6) + lane;
+    const bool valid = x >= q && x < L;
+    const uint8_t c = valid ? dv.p[x] : (uint8_t)0;
+    const bool lead = valid && (c & 0xC0) != 0x80;
+    const int n = utf8_len(c);
+    bool brk = false, ok = false, foreign = false;
+    if (lead) {
+      const int sc = S.sn[x];
+      if (sc != ss && sc != inherited) {
+        if (sc == common) {
+          brk = true;
+        } else {
+          const int sc2 = S.sn[x + n];
+          brk = sc2 != common && sc2 != ss;
+        }
+      }
+      if ((S.lsm[w] >> lane) & 1) {
+        if (sc == ss || sc == inherited) ok = true;
+        else foreign = true;
+      }
+    }
+    const uint64_t Bm = __ballot(brk), Om = __ballot(ok);
+    const uint64_t ev_le = (Bm | Om) & mask_le(lane), ev_lt = (Bm | Om) & lanemask_lt(lane);
+    const bool inrun = ev_le ? ((Om >> topbit(ev_le)) & 1) : run;
+    const bool prev_run = ev_lt ? ((Om >> topbit(ev_lt)) & 1) : run;
+    const bool endc = foreign && (brk || !prev_run);     // a letter stop of another script after a gap
+    const bool sep = brk && prev_run;                    // a run ends here: its ' '
+    const bool cutc = lead && x + n > L;                 // only the last character
+    const bool chr = lead && inrun && !cutc;
+    const int raw = chr ? n : (sep ? 1 : 0);
+    const int pre = excl_scan(raw, lane);
+    const uint64_t Em = __ballot(endc);
+    const uint64_t Hm = __ballot(chr && put + pre + n >= kMaxScriptBytes);
+    const uint64_t Cm = __ballot(cutc && lead && inrun);
+    const uint64_t Sm = __ballot(sep && put + pre + 1 >= soft);
+    const uint64_t stopm = Em | Hm | Sm;
+    const int stop = stopm ? __builtin_ctzll(stopm) : 64;
+    const bool act = lane <= stop;
+    const bool hard_here = lane == stop && ((Hm >> lane) & 1);
+    const bool out_chr = act && chr;
+    const bool out_sep = act && (sep || hard_here);
+    uint64_t o = 0;
+    int olen = 0;
+    if (out_chr) {
+      if (!lower_char(T, dv.p + x, n, o, olen)) {
+        bad = 1;
+        olen = 0;
+      }
+      grow += olen > n ? olen - n : 0;
+    }
+    const int tl = olen + (out_sep ? 1 : 0);
+    const int opre = excl_scan(tl, lane);
+    const int otot = rdl(opre + tl, 63);
+    put += wsum(act ? raw + (hard_here ? 1 : 0) : 0);
+    if (lpos + otot + 64 > kLB) {
+      bad = 1;
+      break;
+    }
+    for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(o >> (8 * k));
+    if (out_sep) lb[lpos + opre + olen] = ' ';
+    lpos += otot;
+    if (stop < 64) {
+      const int xs = (w << 6) + stop;
+      if ((Hm >> stop) & 1) nxt = find_first_g(S.lsm, xs + rdl(n, stop), L);
+      else if ((Sm >> stop) & 1) nxt = find_first_g(S.lsm, xs, L);   // the gap scan starts at the break char
+      else nxt = xs;                                                  // another script's letter stop
+      break;
+    }
+    const uint64_t ev = Bm | Om;
+    if (ev) run = (Om >> topbit(ev)) & 1;
+    if (Cm) {                                                         // the cut last character
+      cut = true;
+      nxt = L;
+      const int xc = (w << 6) + __builtin_ctzll(Cm);
+      int filled = 0;
+      if (lane == 0) {
+        uint8_t tail[12];
+        const int nc = utf8_len(dv.p[xc]);
+        for (int k = 0; k < nc; ++k) tail[k] = (uint8_t)dv.at(xc + k);
+        for (int k = 0; k < 4; ++k) tail[nc + k] = ' ';               // separator + "   " (ilen stops before \0)
+        filled = lower_replace(T, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
+      }
+      lpos += rdl(filled, 0);
+      put += 1;
+      break;
+    }
+    if ((w << 6) + 64 >= L) {                                         // end of document
+      if (run) {
+        if (lane == 0) lb[lpos] = ' ';
+        ++lpos;
+        ++put;
+      }
+      nxt = L;
+      break;
+    }
+  }
+  if (!__ballot(bad != 0))
+    for (int k = lane; k < 40; k += 64) lb[lpos + k] = (!cut && k < 3) ? ' ' : 0;   // "   " pad, NULs
+  if (cut) lpos -= 3;                                                 // text_bytes = filled - 3
+  // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
+  // spans near the 40 KB limit that also grow; re-queue those.
+  if (put + 3 + wsum(grow) > kMaxScriptLowerBuffer - 8) bad = 1;
+  next = nxt;
+  gsync();
+  if (__ballot(bad != 0)) status = -1;
+  return lpos;
+}
+
+// ------------------------------------------------------ predictor (squeeze/repeats)
+__device__ uint32_t new_epoch(Slot& S, int lane) {
+  uint32_t e = uflu(S.epoch) + 1u;
+  if (e == 0) {                                     // wrapped: clear for real
+    for (int i = lane; i < kPredictionTableSize; i += 64) S.pred[i] = 0;
+    e = 1;
+  }
+  gsync();
+  if (lane == 0) S.epoch = e;
+  return e;
+}
+
+// One window of CountPredictedBytes / CheapRepWordsInplace's predictor
+// (compact_lang_det_impl.cc:541-580, 610-692) over the characters whose lead
+// bytes are the lanes of lm, in lane order: p = tbl[h]; tbl[h] = c;
+// predicted = (c == p); h = ((h << 4) ^ c) & 0xFFF.  h after a character
+// depends only on it and the two before it, so every lane computes its own;
+// lanes with equal table keys are matched with 12 ballots and the latest
+// earlier one supplies p.  hcarry is the hash after the last character.
+__device__ bool predict_window(uint64_t* tbl, uint32_t epoch, uint64_t lm, uint32_t c, uint32_t& hcarry, int lane) {
+  if (!lm) return false;
+  const bool me = (lm >> lane) & 1;
+  const uint64_t below = lm & lanemask_lt(lane);
+  const int p1 = below ? topbit(below) : -1;
+  const uint64_t below2 = p1 > 0 ? (below & lanemask_lt(p1)) : 0ull;
+  const int p2 = below2 ? topbit(below2) : -1;
+  const uint32_t c1 = shfl32(c, p1 < 0 ? lane : p1);
+  const uint32_t c2 = shfl32(c, p2 < 0 ? lane : p2);
+  uint32_t h;
+  if (p1 < 0) h = (c ^ (hcarry << 4)) & 0xFFFu;
+  else if (p2 < 0) h = (c ^ (c1 << 4) ^ (hcarry << 8)) & 0xFFFu;
+  else h = (c ^ (c1 << 4) ^ (c2 << 8)) & 0xFFFu;
+  const uint32_t hp = shfl32(h, p1 < 0 ? lane : p1);
+  const uint32_t key = p1 < 0 ? hcarry : hp;
+  uint64_t eq = lm;
+#pragma unroll
+  for (int b = 0; b < 12; ++b) {
+    const bool bit = (key >> b) & 1;
+    const uint64_t m = __ballot(bit);
+    eq &= bit ? m : ~m;
+  }
+  const uint64_t earlier = eq & lanemask_lt(lane);
+  uint32_t pc = shfl32(c, earlier ? topbit(earlier) : lane);
+  if (me && !earlier) {
+    const uint64_t e = tbl[key];
+    pc = (uint32_t)(e >> 32) == epoch ? (uint32_t)e : 0u;
+  }
+  const bool last = (eq & ~mask_le(lane)) == 0;
+  if (me && last) tbl[key] = ((uint64_t)epoch << 32) | c;
+  hcarry = rdlu(h, topbit(lm));
+  gsync();
+  return me && c == pc;
+}
+
+// CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) on a lowered span
+// of more than 2048 bytes: >= 25% spaces or >= 67% predicted bytes in the first
+// 256 bytes (fresh table, hash 0).
+__device__ bool squeeze_trigger(Slot& S, const uint8_t* text, int lane) {
+  int sp = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sp += text[lane * 4 + k] == ' ';
+  if (wsum(sp) >= (256 * 25) / 100) return true;
+  const uint32_t ep = new_epoch(S, lane);
+  uint32_t h = 0;
+  int pc = 0;
+  for (int w = 0; w < 4; ++w) {
+    const int x = (w << 6) + lane;
+    const uint8_t b = text[x];
+    const bool lead = (b & 0xC0) != 0x80;
+    int incr = 1;
+    const uint32_t c = lead ? (uint32_t)next_char_code(text + x, &incr) : 0u;
+    const uint64_t lm = __ballot(lead);
+    const bool pr = predict_window(S.pred, ep, lm, c, h, lane);
+    pc += (lead && pr) ? incr : 0;
+  }
+  return wsum(pc) >= (256 * 67) / 100;
+}
+
+// CheapRepWordsInplace (compact_lang_det_impl.cc:610-692), src -> dst.  The
+// predictor table and hash carry over from span to span within the pass.  A
+// segment runs from a space (inclusive: its byte counts for the next word) to
+// the next space; at that space the bytes after the previous space, this space
+// included, are dropped if more than half of the segment was predicted.
+__device__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
+                         int lane) {
+  const int nw = (len + 63) >> 6;
+  int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
+  for (int w = 0; w < nw; ++w) {
+    const int x = (w << 6) + lane;
+    const bool valid = x < len;
+    const uint8_t b = valid ? src[x] : (uint8_t)0;
+    const bool lead = valid && (b & 0xC0) != 0x80;
+    int incr = 1;
+    const uint32_t c = lead ? (uint32_t)next_char_code(src + x, &incr) : 0u;
+    const uint64_t lm = __ballot(lead);
+    const bool pr = predict_window(S.pred, ep, lm, c, hcarry, lane);
+    const int wl = lead ? incr : 0, gd = (lead && pr) ? incr : 0;
+    const bool sp = lead && b == ' ';
+    const uint64_t spm = __ballot(sp);
+    const int ewl = excl_scan(wl, lane), egd = excl_scan(gd, lane);
+    const uint64_t psp = spm & lanemask_lt(lane);
+    const int ps = psp ? topbit(psp) : lane;
+    const int ewl_ps = __shfl(ewl, ps, 64), egd_ps = __shfl(egd, ps, 64);
+    const int swl = psp ? ewl - ewl_ps : cwl + ewl;
+    const int sgd = psp ? egd - egd_ps : cgd + egd;
+    const uint64_t dm = __ballot(sp && sgd * 2 > swl);
+    if (lane == 0) {
+      S.spm[w] = spm;
+      S.delm[w] = dm;
+    }
+    const int twl = rdl(ewl + wl, 63), tgd = rdl(egd + gd, 63);
+    if (spm) {
+      const int ls = topbit(spm);
+      cwl = twl - rdl(ewl, ls);
+      cgd = tgd - rdl(egd, ls);
+    } else {
+      cwl += twl;
+      cgd += tgd;
+    }
+  }
+  gsync();
+  int dpos = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int x = (w << 6) + lane;
+    bool keep = false;
+    if (x < len) {
+      int ww = w;
+      uint64_t m = S.spm[w] & (~0ull << lane);
+      while (!m && ((ww + 1) << 6) < len) m = S.spm[++ww];
+      keep = true;
+      if (m) {
+        const int s = __builtin_ctzll(m);
+        keep = !((S.delm[ww] >> s) & 1);
+      }
+    }
+    const uint64_t km = __ballot(keep);
+    if (keep) dst[dpos + __popcll(km & lanemask_lt(lane))] = src[x];
+    dpos += __popcll(km);
+  }
+  // in place, the bytes from dpos on keep their old values; then "   \0" if
+  // at least 4 bytes went, else a single ' ' if any went (:684-689)
+  for (int k = lane; k < 48; k += 64) {
+    uint8_t v = src[dpos + k];
+    if (dpos < len - 3 && k < 4) v = k < 3 ? ' ' : 0;
+    else if (dpos < len && k == 0) v = ' ';
+    dst[dpos + k] = v;
+  }
+  gsync();
+  return dpos;
+}
+
+// ---------------------------------------------------- quad chain of a span
+// GetQuadHits' chain (cldutil.cc:349-401): from src, e = 4 chars on (stopping
+// at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
+// else mid (+1 on a vowel).  It never jumps over a space, so it enters every
+// word at its first byte and a word's entries depend on that word alone.
+__device__ bool word_lists(const uint8_t* text, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+  nws = 0;
+  nsp = 0;
+  for (int w0 = start; w0 <= tb; w0 += 64) {
+    const int x = w0 + lane;
+    const bool isws = x < tb && (x == start || text[x - 1] == ' ');
+    const bool issp = x <= tb && text[x] == ' ';
+    const uint64_t m1 = __ballot(isws), m2 = __ballot(issp);
+    if (isws) {
+      const int k = nws + __popcll(m1 & lanemask_lt(lane));
+      if (k < kListCap) S.wst[k] = (uint16_t)x;
+    }
+    if (issp) {
+      const int k = nsp + __popcll(m2 & lanemask_lt(lane));
+      if (k < kListCap) S.wsp[k] = (uint16_t)x;
+    }
+    nws += __popcll(m1);
+    nsp += __popcll(m2);
+  }
+  gsync();
+  return nws <= kListCap && nsp <= kListCap;
+}
+
+__device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uint16_t* out) {
+  int cnt = 0, src = s;
+  for (;;) {
+    if (out) out[cnt] = (uint16_t)src;
+    ++cnt;
+    int e = src;
+    e += adv_but_space(text[e]);
+    e += adv_but_space(text[e]);
+    const int mid = e;
+    e += adv_but_space(text[e]);
+    e += adv_but_space(text[e]);
+    if (text[e] == ' ') break;                    // next = e + 1: the next word start, or the end
+    if (mid >= tb) break;                         // next = limit
+    src = mid + adv_space_vowel(text[mid]);
+    if (src >= tb) break;
+  }
+  return cnt;
+}
+
+__device__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int lane) {
+  int nch = 0;
+  for (int i0 = 0; i0 < nws; i0 += 64) {
+    const int i = i0 + lane;
+    int cnt = 0, s = 0;
+    if (i < nws) {
+      s = S.wst[i];
+      cnt = walk_word(text, s, tb, nullptr);
+    }
+    const int pre = excl_scan(cnt, lane);
+    const int tot = rdl(pre + cnt, 63);
+    if (nch + tot > kListCap) return -1;
+    if (i < nws) walk_word(text, s, tb, S.chain + nch + pre);
+    nch += tot;
+  }
+  gsync();
+  return nch;
+}
+
+// GetQuadHits for one round from chain entry c0 (cldutil.cc:315-405): probes
+// per entry, the "not one of the last two hits" filter, the 1000-hit cut.
+// Returns the round end (the reference's `next`); c0 advances.
+__device__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int nch, int& c0, int& nb,
+                          int lane) {
+  nb = 0;
+  uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
+  for (int i0 = c0; i0 < nch; i0 += 64) {
+    const int i = i0 + lane;
+    bool hit = false;
+    uint32_t hv = 0, ind = 0;
+    int p = 0;
+    if (i < nch) {
+      p = S.chain[i];
+      int e = p;
+      e += adv_but_space(text[e]);
+      e += adv_but_space(text[e]);
+      e += adv_but_space(text[e]);
+      e += adv_but_space(text[e]);
+      hv = quad_hash_v2(text + p, e - p);
+      uint32_t probs = quad_lookup(T.quad, hv);
+      if (probs == 0 && T.quad2.size != 0) {
+        probs = quad_lookup(T.quad2, hv);
+        if (probs) ind = (probs & ~T.quad2.key_mask) | 0x80000000u;
+      } else if (probs) {
+        ind = probs & ~T.quad.key_mask;
+      }
+      hit = probs != 0;
+    }
+    const uint64_t hm = __ballot(hit);
+    // every hit kept so far => its two predecessors are the previous hit lanes
+    const uint64_t hb = hm & lanemask_lt(lane);
+    const int q1 = hb ? topbit(hb) : -1;
+    const uint64_t hb2 = q1 > 0 ? (hb & lanemask_lt(q1)) : 0ull;
+    const int q2 = hb2 ? topbit(hb2) : -1;
+    const uint32_t h1 = shfl32(hv, q1 < 0 ? lane : q1), h2 = shfl32(hv, q2 < 0 ? lane : q2);
+    const uint32_t a = q1 < 0 ? A : h1;
+    const uint32_t bb = q1 < 0 ? B : (q2 < 0 ? A : h2);
+    const uint64_t cm = __ballot(hit && (hv == a || hv == bb));
+    uint64_t keep = hm;
+    uint32_t nA, nB;
+    if (cm) {
+      const int f = __builtin_ctzll(cm);
+      keep = hm & lanemask_lt(f);
+      uint32_t xA = rdlu(a, f), xB = rdlu(bb, f);
+      for (uint64_t r = hm & ~lanemask_lt(f); r; r &= r - 1) {
+        const int l = __builtin_ctzll(r);
+        const uint32_t v = rdlu(hv, l);
+        if (v == xA || v == xB) continue;
+        xB = xA;
+        xA = v;
+        keep |= 1ull << l;
+      }
+      nA = xA;
+      nB = xB;
+    } else if (hm) {
+      const int t1 = topbit(hm);
+      nA = rdlu(hv, t1);
+      const uint64_t r2 = hm & ~(1ull << t1);
+      nB = r2 ? rdlu(hv, topbit(r2)) : A;
+    } else {
+      nA = A;
+      nB = B;
+    }
+    const int kc = __popcll(keep);
+    int lastl = 64;
+    if (nb + kc >= kMaxScoringHits) {
+      lastl = nth_bit(keep, kMaxScoringHits - nb - 1);
+      keep &= mask_le(lastl);
+    }
+    if ((keep >> lane) & 1) {
+      const int k = nb + __popcll(keep & lanemask_lt(lane));
+      S.b_off[k] = (uint16_t)p;
+      S.b_ind[k] = ind;
+    }
+    nb += __popcll(keep);
+    if (lastl < 64) {
+      c0 = i0 + lastl + 1;
+      gsync();
+      return c0 < nch ? ufl(S.chain[c0]) : tb;
+    }
+    A = nA;
+    B = nB;
+  }
+  c0 = nch;
+  gsync();
+  return tb;
+}
+
+// GetOctaHits (cldutil.cc:416-533) over [off, next]: one lane per word (words
+// end at the spaces in [start, next]); the two-word repeat filter updates the
+// pair partner even when the probes miss; caps: 1000 delta / 999 distinct.
+__device__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int nsp, int& j0, int off, int next,
+                           int& nd, int& nx, int lane) {
+  const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
+  const int lim = next + 1;
+  nd = 0;
+  nx = 0;
+  uint64_t A = 0, B = 0;                 // last two kept word hashes
+  const int jfirst = j0;
+  for (int jb = j0;; jb += 64) {
+    const int j = jb + lane;
+    const bool v = j < nsp && (int)S.wsp[j] < lim;
+    const uint64_t vm = __ballot(v);
+    if (!vm) break;
+    const int nv = __popcll(vm);
+    int a = start, pws = start, e = 0;
+    uint64_t wh = 0;
+    if (v) {
+      e = S.wsp[j];
+      a = j == jfirst ? start : S.wsp[j - 1] + 1;
+      pws = j <= jfirst + 1 ? start : S.wsp[j - 2] + 1;
+      int we = a, q = a, cc = 0;
+      while (q < e) {
+        ++cc;
+        q += utf8_len(text[q]);
+        if (cc <= 8) we = q;
+        else break;
+      }
+      wh = octa_hash40(text + a, we - a);
+    }
+    // filter (every word takes part): fast path assumes no drop in this block
+    const uint64_t h1 = shfl64(wh, lane >= 1 ? lane - 1 : lane), h2 = shfl64(wh, lane >= 2 ? lane - 2 : lane);
+    const uint64_t pa = lane >= 1 ? h1 : A;
+    const uint64_t pb = lane >= 2 ? h2 : (lane == 1 ? A : B);
+    const uint64_t cm = __ballot(v && (wh == pa || wh == pb));
+    uint64_t keep = vm;
+    uint32_t tlo = (uint32_t)pa, thi = (uint32_t)(pa >> 32);    // pair partner = previous kept word
+    uint64_t nA, nB;
+    if (cm) {
+      const int f = __builtin_ctzll(cm);
+      keep = vm & lanemask_lt(f);
+      uint64_t xA = rdl64(pa, f), xB = rdl64(pb, f);
+      for (int l = f; l < nv; ++l) {
+        const uint64_t hv = rdl64(wh, l);
+        if (hv == xA || hv == xB) continue;
+        if (lane == l) {
+          tlo = (uint32_t)xA;
+          thi = (uint32_t)(xA >> 32);
+        }
+        xB = xA;
+        xA = hv;
+        keep |= 1ull << l;
+      }
+      nA = xA;
+      nB = xB;
+    } else {
+      nA = rdl64(wh, nv - 1);
+      nB = nv >= 2 ? rdl64(wh, nv - 2) : A;
+    }
+    uint32_t pp = 0, xp = 0, dp = 0;
+    if ((keep >> lane) & 1) {
+      const uint64_t tph = ((uint64_t)thi << 32) | tlo;
+      if (tph != 0 && tph != wh) pp = octa_lookup(T.distinctocta, pair_hash(tph, wh));
+      xp = octa_lookup(T.distinctocta, wh);
+      dp = octa_lookup(T.deltaocta, wh);
+    }
+    const int cx = (pp != 0) + (xp != 0), cd = (dp != 0);
+    const int ex = excl_scan(cx, lane), ed = excl_scan(cd, lane);
+    const uint64_t capm = __ballot(v && (nx + ex + cx >= kMaxScoringHits - 1 || nd + ed + cd >= kMaxScoringHits));
+    const int cut = capm ? __builtin_ctzll(capm) : 64;
+    if (lane <= cut) {
+      int o = nx + ex;
+      if (pp) {
+        S.x_off[o] = (uint16_t)pws;
+        S.x_ind[o] = pp & ~T.distinctocta.key_mask;
+        ++o;
+      }
+      if (xp) {
+        S.x_off[o] = (uint16_t)a;
+        S.x_ind[o] = xp & ~T.distinctocta.key_mask;
+      }
+      if (dp) {
+        S.d_off[nd + ed] = (uint16_t)a;
+        S.d_ind[nd + ed] = dp & ~T.deltaocta.key_mask;
+      }
+    }
+    const int lastl = cut < 64 ? cut : 63;
+    nx += rdl(ex + cx, lastl);
+    nd += rdl(ed + cd, lastl);
+    if (cut < 64 || nv < 64) break;
+    A = nA;
+    B = nB;
+  }
+  // next round's words start after `next` (a chain position, never a space)
+  int lo = j0, hi = nsp;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int)ufl(S.wsp[mid]) < lim) lo = mid + 1;
+    else hi = mid;
+  }
+  j0 = lo;
+  gsync();
+}
+
+// GetUniHits + GetBiHits (cldutil.cc:201-310) for one round from off.
+__device__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int off, int& nb, int& nd,
+                         int& nx, int lane) {
+  const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
+  nb = 0;
+  int next = -1;
+  uint32_t endmax = (uint32_t)start;
+  for (int w0 = start; w0 < tb; w0 += 64) {
+    const int x = w0 + lane;
+    int prop = 0, len = 0;
+    if (x < tb && (text[x] & 0xC0) != 0x80) {
+      len = utf8_len(text[x]);
+      prop = uni_prop(T, text + x, len);
+      endmax = (uint32_t)(x + len) > endmax ? (uint32_t)(x + len) : endmax;
+    }
+    uint64_t hm = __ballot(prop > 0);
+    int lastl = 64;
+    if (nb + __popcll(hm) >= kMaxScoringHits) {
+      lastl = nth_bit(hm, kMaxScoringHits - nb - 1);
+      hm &= mask_le(lastl);
+    }
+    if ((hm >> lane) & 1) {
+      const int k = nb + __popcll(hm & lanemask_lt(lane));
+      S.b_off[k] = (uint16_t)(x + len);
+      S.b_ind[k] = (uint32_t)prop;
+    }
+    nb += __popcll(hm);
+    if (lastl < 64) {
+      next = rdl(x + len, lastl);
+      break;
+    }
+  }
+  if (next < 0) next = (int)wave::wmax(endmax);
+  nd = 0;
+  nx = 0;
+  for (int w0 = off; w0 < next; w0 += 64) {
+    const int x = w0 + lane;
+    uint32_t dp = 0, xp = 0;
+    const bool v = x < next && (text[x] & 0xC0) != 0x80;
+    if (v) {
+      const int len = utf8_len(text[x]);
+      const int len2 = utf8_len(text[x + len]) + len;
+      if (6 <= len2) {
+        const uint32_t bh = bi_hash_v2(text + x, len2);
+        dp = quad_lookup(T.deltabi, bh);
+        xp = quad_lookup(T.distinctbi, bh);
+      }
+    }
+    const int cd = dp != 0, cx = xp != 0;
+    const int ed = excl_scan(cd, lane), ex = excl_scan(cx, lane);
+    const uint64_t capm = __ballot(v && (nd + ed + cd >= kMaxScoringHits || nx + ex + cx >= kMaxScoringHits - 1));
+    const int cut = capm ? __builtin_ctzll(capm) : 64;
+    if (lane <= cut) {
+      if (dp) {
+        S.d_off[nd + ed] = (uint16_t)x;
+        S.d_ind[nd + ed] = dp & ~T.deltabi.key_mask;
+      }
+      if (xp) {
+        S.x_off[nx + ex] = (uint16_t)x;
+        S.x_ind[nx + ex] = xp & ~T.distinctbi.key_mask;
+      }
+    }
+    const int lastl = cut < 64 ? cut : 63;
+    nd += rdl(ed + cd, lastl);
+    nx += rdl(ex + cx, lastl);
+    if (cut < 64) break;
+  }
+  gsync();
+  return next;
+}
+
+// ------------------------------------- linearize + chunk + score (one round)
+// LinearizeAll / ChunkAll / ScoreAllHits (scoreonescriptspan.cc:856-1031,
+// 208-302) without materialising linear[].  Linear order = the seed (offset
+// `lowest`), then (offset, delta < distinct < base, index).  Base emission t
+// is base entry t+2 (the seed is #1) and chunk k closes after base entry E_k,
+// so chunk k holds base emissions [E_{k-1}-1, E_k-1).  A delta/distinct
+// emission at offset o follows 1 + #(base emissions with offset < o) base
+// entries and lands in the first chunk k with that count < E_k, i.e. with
+// o <= theta_k = be_off[E_k - 2].  Every chunk is therefore one contiguous
+// range of each stream.
+__device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
+                            int lowest, int dummy_off, int lane) {
+  const DevTbl& bo = cjk ? T.compat : T.quad;
+  const DevTbl& bo2 = cjk ? T.compat : T.quad2;
+  const DevTbl& dob = cjk ? T.deltabi : T.deltaocta;
+  const DevTbl& xob = cjk ? T.distinctbi : T.distinctocta;
+  const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
+
+  // base hits -> base emissions (1 or 2 langprobs, zeros dropped)
+  int eb = 0;
+  for (int j0 = 0; j0 < nb; j0 += 64) {
+    const int j = j0 + lane;
+    uint32_t l1 = 0, l2 = 0;
+    int off = 0;
+    if (j < nb) {
+      off = S.b_off[j];
+      uint32_t ind = S.b_ind[j];
+      const DevTbl* lb = &bo;
+      if (ind & 0x80000000u) {
+        lb = &bo2;
+        ind &= ~0x80000000u;
+      }
+      if (ind < lb->size_one) {
+        l1 = ind_at(*lb, ind);
+      } else {
+        ind += ind - lb->size_one;
+        l1 = ind_at(*lb, ind);
+        l2 = ind_at(*lb, ind + 1);
+        if (l1 == 0) {
+          l1 = l2;
+          l2 = 0;
+        }
+      }
+    }
+    const int c = (l1 != 0) + (l2 != 0);
+    const int o = eb + excl_scan(c, lane);
+    eb = rdl(o + c, 63);
+    if (l1) {
+      S.be_off[o] = (uint16_t)off;
+      S.be_lp[o] = l1;
+    }
+    if (l2) {
+      S.be_off[o + 1] = (uint16_t)off;
+      S.be_lp[o + 1] = l2;
+    }
+  }
+  // delta / distinct emissions, compacted in place (ind -> langprob)
+  int ed = 0, ex = 0;
+  for (int j0 = 0; j0 < nd; j0 += 64) {
+    const int j = j0 + lane;
+    const uint32_t lp = j < nd ? ind_at(dob, S.d_ind[j]) : 0u;
+    const uint16_t off = j < nd ? S.d_off[j] : (uint16_t)0;
+    const int o = ed + excl_scan(lp != 0, lane);
+    ed = rdl(o + (lp != 0), 63);
+    if (lp) {
+      S.d_off[o] = off;
+      S.d_ind[o] = lp;
+    }
+  }
+  for (int j0 = 0; j0 < nx; j0 += 64) {
+    const int j = j0 + lane;
+    const uint32_t lp = j < nx ? ind_at(xob, S.x_ind[j]) : 0u;
+    const uint16_t off = j < nx ? S.x_off[j] : (uint16_t)0;
+    const int o = ex + excl_scan(lp != 0, lane);
+    ex = rdl(o + (lp != 0), 63);
+    if (lp) {
+      S.x_off[o] = off;
+      S.x_ind[o] = lp;
+    }
+  }
+  // chunk plan from the base-hit count (ChunkAll :978-1031)
+  int K = 0;
+  if (nb <= 0) {
+    K = 1;
+    if (lane == 0) s.E[0] = 0xFFFF;
+  } else {
+    int left = nb, e = 0;
+    while (left > 0) {
+      int blen = chunksize;
+      if (left < chunksize + (chunksize >> 1)) blen = left;
+      else if (left < 2 * chunksize) blen = (left + 1) >> 1;
+      e += blen;
+      if (lane == 0) s.E[K] = (uint16_t)e;
+      ++K;
+      left -= blen;
+    }
+    if (lane == 0) s.E[K - 1] = 0xFFFF;   // the last chunk takes everything that is left
+  }
+  gsync();                                  // emissions visible; E in LDS
+  for (int k = lane; k <= K; k += 64) {
+    if (k < K) {
+      int th = 0x7FFFFFFF;
+      if (k < K - 1) {
+        const int idx = (int)s.E[k] - 2;
+        th = idx < 0 ? -1 : (idx < eb ? (int)S.be_off[idx] : 0x7FFFFFFF);
+      }
+      s.theta[k] = th;
+      const int bs = k == 0 ? 0 : min(max((int)s.E[k - 1] - 1, 0), eb);
+      s.bst[k] = (uint16_t)bs;
+    } else {
+      s.bst[K] = (uint16_t)eb;
+    }
+    s.st[0][k] = (uint16_t)ed;
+    s.st[1][k] = (uint16_t)ex;
+  }
+  wsync();
+  // chunk of every delta / distinct emission; chunk k's range starts at the
+  // first emission whose chunk is >= k (LDS indexed directly: a selected
+  // generic pointer would turn these into flat stores, unordered against
+  // the ds_write initialisation above)
+  for (int pass = 0; pass < 2; ++pass) {
+    const int n = pass == 0 ? ed : ex;
+    const uint16_t* offs = pass == 0 ? S.d_off : S.x_off;
+    int pch = -1;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      int ch = K - 1;
+      if (i < n) {
+        const int o = offs[i];
+        int lo = 0, hi = K - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (o <= s.theta[mid]) hi = mid;
+          else lo = mid + 1;
+        }
+        ch = lo;
+      }
+      const int up = __shfl(ch, lane - 1, 64);          // all lanes: ?: would run it with lane 0 off
+      const int prev = lane == 0 ? pch : up;
+      if (i < n)
+        for (int k = prev + 1; k <= ch; ++k) s.st[pass][k] = (uint16_t)i;
+      pch = rdl(ch, 63);
+    }
+  }
+  wsync();
+  // lo[k] = first offset of chunk k (chunk 0 opens with the seed at `lowest`)
+  for (int k = lane; k < K; k += 64) {
+    uint32_t m = k == 0 ? (uint32_t)lowest : kInf;
+    const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
+    const int ds = s.st[0][k], de = s.st[0][k + 1], xs = s.st[1][k], xe = s.st[1][k + 1];
+    if (bs < be) m = min(m, (uint32_t)S.be_off[bs]);
+    if (ds < de) m = min(m, (uint32_t)S.d_off[ds]);
+    if (xs < xe) m = min(m, (uint32_t)S.x_off[xs]);
+    s.lo[k] = m;
+  }
+  wsync();
+  const uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
+  const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
+  for (int k = 0; k < K; ++k) {
+    reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
+    const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
+    const int ds = s.st[0][k], de = s.st[0][k + 1], xs = s.st[1][k], xe = s.st[1][k + 1];
+    wsync();
+    const int seedn = k == 0 ? 1 : 0;
+    const int nB = be - bs, nD = de - ds, nX = xe - xs;
+    const int tot = seedn + nB + nD + nX + kMaxBoosts;
+    uint64_t gm = 0;
+    for (int t = lane; t < tot; t += 64) {
+      uint32_t lp;
+      int u = t;
+      if (u < seedn) {
+        lp = seed;
+      } else if ((u -= seedn) < nB) {
+        lp = S.be_lp[bs + u];
+      } else if ((u -= nB) < nD) {
+        lp = S.d_ind[ds + u];
+      } else if ((u -= nD) < nX) {
+        lp = S.x_ind[xs + u];
+      } else {                               // boosts: the last four distinct langprobs so far
+        const int v = xe - kMaxBoosts + (u - nX);
+        lp = v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_ind[v];
+        if (lp == 0) continue;
+      }
+      // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row
+      const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
+      const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
+      if (k1) { atomicAdd(&s.tote[k1], (e >> 8) & 0xFF); gm |= 1ull << (k1 >> 2); }
+      if (k2) { atomicAdd(&s.tote[k2], (e >> 16) & 0xFF); gm |= 1ull << (k2 >> 2); }
+      if (k3) { atomicAdd(&s.tote[k3], e >> 24); gm |= 1ull << (k3 >> 2); }
+    }
+    gm = wor64(gm);
+    const int score_count = nB + seedn;
+    wsync();
+    // top three keys of the in-use groups: (uint16 score desc, key asc)
+    const uint4 v4 = reinterpret_cast<const uint4*>(s.tote)[lane];
+    const bool inuse = (gm >> lane) & 1;
+    const uint32_t cand[4] = {v4.x & 0xFFFF, v4.y & 0xFFFF, v4.z & 0xFFFF, v4.w & 0xFFFF};
+    int key3[3] = {-1, -1, -1};
+    uint32_t sc3[3] = {0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      uint32_t best = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = lane * 4 + i;
+        const bool taken = key == key3[0] || key == key3[1];
+        const uint32_t comp = (inuse && !taken) ? ((cand[i] + 1) << 8) | (uint32_t)(255 - key) : 0u;
+        best = comp > best ? comp : best;
+      }
+      best = wave::wmax(best);
+      if (best) {
+        key3[r] = 255 - (int)(best & 0xFF);
+        sc3[r] = (best >> 8) - 1;
+      }
+    }
+    if (lane == 0) {
+      const uint32_t lo_k = s.lo[k];
+      const int lo = lo_k == kInf ? dummy_off : (int)lo_k;
+      int hi = dummy_off;
+      if (k + 1 < K && s.lo[k + 1] != kInf) hi = (int)s.lo[k + 1];
+      const int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
+      const int lang2 = from_per_script_number(T, ulscript, (uint8_t)key3[1]);
+      const int len = hi - lo;
+      const int sc1 = key3[0] >= 0 ? (int)sc3[0] : 0;
+      const int sc2 = key3[1] >= 0 ? (int)sc3[1] : 0;
+      int actual = 0;
+      if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
+      const int esub = lang1 * 4 + lscript4(T, ulscript);
+      const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+      const uint16_t bytes = (uint16_t)len, grams = (uint16_t)score_count;
+      const uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
+      int rd = (uint8_t)reliability_delta(s1, s2, grams);
+      const int cs1 = close_set(T, lang1);
+      if (cs1 != 0 && cs1 == close_set(T, lang2)) rd = 100;
+      const int rsc = (uint8_t)reliability_expected(actual, expected);
+      if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
+      if (s.dbg) {
+        uint32_t* o = s.dbg + 1 + s.dbg_pos;
+        const uint32_t v[18] = {'C', (uint32_t)lo, (uint32_t)hi, (uint32_t)lang1, (uint32_t)lang2, s1, s2,
+                                grams, (uint32_t)rd, (uint32_t)rsc, (uint32_t)bs, (uint32_t)be, (uint32_t)ds,
+                                (uint32_t)de, (uint32_t)xs, (uint32_t)xe, (uint32_t)s.theta[k], (uint32_t)(eb << 16 | K)};
+        for (int i = 0; i < 18; ++i) o[i] = v[i];
+        s.dbg_pos += 18;
+        s.dbg[0] = s.dbg_pos;
+      }
+    }
+    wsync();
+  }
+  // the ring keeps the last four distinct langprobs
+  if (lane == 0) {
+    uint32_t r4[4];
+    for (int i = 0; i < 4; ++i) {
+      const int u = ex - kMaxBoosts + i;
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : S.x_ind[u];
+    }
+    for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
+  }
+  wsync();
+}
+
+__device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, int lane) {
+  if (!s.dbg) return;
+  const uint32_t h[6] = {'R', (uint32_t)off, (uint32_t)next, (uint32_t)nb, (uint32_t)nd, (uint32_t)nx};
+  dbg_words(s, lane, h, 6);
+  uint32_t* o = s.dbg + 1 + s.dbg_pos;
+  for (int i = lane; i < nb; i += 64) { o[2 * i] = S.b_off[i]; o[2 * i + 1] = S.b_ind[i]; }
+  o += 2 * nb;
+  for (int i = lane; i < nd; i += 64) { o[2 * i] = S.d_off[i]; o[2 * i + 1] = S.d_ind[i]; }
+  o += 2 * nd;
+  for (int i = lane; i < nx; i += 64) { o[2 * i] = S.x_off[i]; o[2 * i + 1] = S.x_ind[i]; }
+  wave::wsync();
+  if (lane == 0) {
+    s.dbg_pos += 2 * (nb + nd + nx);
+    s.dbg[0] = s.dbg_pos;
+  }
+  gsync();
+}
+
+// ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
+// of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
+__device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb, int ulscript,
+                           int lane, uint32_t* tr, uint32_t doc) {
+  const int rt = rtype_of(T, ulscript);
+  if (rt == RTypeNone || rt == RTypeOne) {
+    if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
+    wsync();
+    return true;
+  }
+  if (tb <= 1) return true;
+  int off = 1;
+  if (rt == RTypeCJK) {
+    while (off < tb) {
+      int nb, nd, nx;
+      trace(tr, lane, doc, 20, off);
+      const int next = cjk_round(T, text, tb, S, off, nb, nd, nx, lane);
+      trace(tr, lane, doc, 21, next);
+      dbg_round(S, s, off, next, nb, nd, nx, lane);
+      score_round(T, S, s, ulscript, true, nb, nd, nx, off, next, lane);
+      off = next;
+    }
+    return true;
+  }
+  const int start = 1 + (ufl(text[1]) == ' ' ? 1 : 0);
+  int nws, nsp;
+  if (!word_lists(text, tb, start, S, nws, nsp, lane)) return false;
+  trace(tr, lane, doc, 10, nws);
+  const int nch = build_chain(text, tb, S, nws, lane);
+  if (nch < 0) return false;
+  trace(tr, lane, doc, 11, nch);
+  int c0 = 0, j0 = 0;
+  while (off < tb) {
+    int nb, nd, nx;
+    trace(tr, lane, doc, 12, off);
+    const int next = quad_round(T, text, tb, S, nch, c0, nb, lane);
+    trace(tr, lane, doc, 13, next);
+    octa_round(T, text, S, nsp, j0, off, next, nd, nx, lane);
+    trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
+    dbg_round(S, s, off, next, nb, nd, nx, lane);
+    score_round(T, S, s, ulscript, false, nb, nd, nx, off, next, lane);
+    off = next;
+  }
+  return true;
+}
+
+// DetectLanguageSummaryV2 (compact_lang_det_impl.cc:1707-2106) for one
+// document: pass 1, and pass 2 with Repeats when pass 1 is not good enough.
+// Returns the number of passes, or -reason (kWhy*) to re-queue.
+enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
+__device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
+                      cld_result* __restrict__ out, uint32_t* tr, uint32_t doc) {
+  const int unk = (int)T.unknown_lang;
+  if (L == 0) {
+    if (lane == 0) {
+      Extract x;
+      for (int i = 0; i < 3; ++i) { x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; x.rp3[i] = 0; }
+      x.text_bytes = 0;
+      write_result(out, x, unk, false);
+    }
+    return 1;
+  }
+  if (L > kDocCap - 64) return -kWhyLength;
+  const DocView dv{g, L};
+  trace(tr, lane, doc, 1, L);
+  if (!classify(T, dv, S, lane)) return -kWhyClassify;
+  trace(tr, lane, doc, 2, 0);
+  for (int pass = 1; pass <= 2; ++pass) {
+    if (lane == 0) s.dt.init();
+    if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
+    uint32_t hcarry = 0, ep = 0;
+    if (pass == 2) ep = new_epoch(S, lane);
+    wsync();
+    int next = 0, total = 0;
+    for (;;) {
+      int ul = 0, st = 0;
+      trace(tr, lane, doc, 3, next);
+      int tb = next_span(T, dv, S, S.lb[0], next, ul, st, lane);
+      trace(tr, lane, doc, 4, tb);
+      if (st == 0) break;
+      if (st < 0) return -kWhySpan;
+      const uint8_t* text = S.lb[0];
+      if (pass == 1) {
+        if (tb > 2048 && squeeze_trigger(S, text, lane)) return -kWhySqueeze;   // Squeeze restart: k_general
+      } else {
+        tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, lane);
+        text = S.lb[1];
+      }
+      trace(tr, lane, doc, 5, tb);
+      {
+        const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
+        dbg_words(s, lane, v, 4);
+      }
+      if (!score_span(T, S, s, text, tb, ul, lane, tr, doc)) return -kWhyCapacity;
+      total += tb;
+    }
+    int res = 1;
+    if (lane == 0) {
+      DocTote& dt = s.dt;
+      refine_scored_close_pairs(T, dt);
+      dt.sort3();
+      Extract x;
+      extract_lang_etc(T, dt, total, x);
+      const bool good = pass == 2 || total <= 256 || (x.reliable && x.pct3[0] >= 70) ||
+                        (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
+      if (!good) {
+        res = 2;
+      } else {
+        remove_unreliable_languages(T, dt);
+        dt.sort3();
+        extract_lang_etc(T, dt, total, x);
+        bool rel;
+        const int summary = calc_summary_lang(T, total, x, rel);
+        write_result(out, x, summary, rel);
+      }
+    }
+    res = rdl(res, 0);
+    wsync();
+    if (res == 1) return pass;
+  }
+  return 0;
+}
+
+// The fused span builder emits separators and pads as ' ' without lowering
+// them; that is exact only if the lowercaser maps ' ' to itself.
+__device__ bool space_lowers_to_space(const DevTables& T) {
+  const uint8_t sp = ' ';
+  uint64_t o = 0;
+  int olen = 0;
+  return lower_char(T, &sp, 1, o, olen) && olen == 1 && o == (uint64_t)' ';
+}
+
+}  // namespace lng
+}  // namespace cld

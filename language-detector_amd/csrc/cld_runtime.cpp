@@ -200,6 +200,14 @@ struct Device {
   uint64_t stride = 0;
   int lanes = 0;
   int front = 0;              // 0: wavefront-per-document kernel, 1: lane-per-document (CLD_FRONT=lane)
+  uint8_t* d_slots = nullptr; // k_long per-wave slots (0 slots: CLD_LONG=0, long documents go to k_general)
+  int n_slots = 0;
+  uint32_t* d_requeue2 = nullptr;
+  size_t requeue2_cap = 0;
+  uint32_t* h_trace = nullptr;  // CLD_TRACE=1: pinned host progress words, 4 per k_long wave
+  uint32_t* d_dbg = nullptr;    // CLD_DEBUG_DOC=i: k_long dumps document i's rounds/chunks
+  uint32_t dbg_doc = 0xFFFFFFFFu;
+  double trace_timeout = 0;
   unsigned long long* d_prof = nullptr;   // per-stage cycle sums (CLD_PROFILE_STAGES=1)
   uint32_t* d_counters = nullptr;
   uint32_t* d_requeue = nullptr;
@@ -207,8 +215,8 @@ struct Device {
   uint8_t* d_buf = nullptr; size_t buf_cap = 0;
   uint64_t* d_offs = nullptr; size_t offs_cap = 0;
   cld_result* d_out = nullptr; size_t out_cap = 0;
-  hipEvent_t ev[3]{};
-  std::vector<std::array<hipEvent_t, 3>> ev_pool;   // one triple per enqueue since reset
+  hipEvent_t ev[4]{};
+  std::vector<std::array<hipEvent_t, 4>> ev_pool;   // one set per enqueue since reset
   size_t ev_used = 0;
   cld_batch_stats last{};
   uint64_t last_n = 0;
@@ -267,29 +275,64 @@ int init_device(Device* d) {
     }
   }
   HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
+  // k_long: one slot per resident wavefront of its persistent grid
+  int waves = 8;
+  if (const char* e = getenv("CLD_LONG_WAVES")) waves = atoi(e);
+  if (const char* e = getenv("CLD_LONG")) if (atoi(e) == 0) waves = 0;
+  int n_slots = (prop.multiProcessorCount * waves / kLongWPB) * kLongWPB;
+  const uint64_t slot = cld_long_slot_bytes();
+  while (n_slots > 0 && (uint64_t)n_slots * slot > (8ull << 30)) n_slots -= kLongWPB;
+  if (n_slots > 0) {
+    HIP_OK(hipMalloc(&d->d_slots, (uint64_t)n_slots * slot));
+    HIP_OK(hipMemset(d->d_slots, 0, (uint64_t)n_slots * slot));   // predictor epochs start at 0
+    d->n_slots = n_slots;
+  }
+  if (const char* e = getenv("CLD_DEBUG_DOC")) {
+    d->dbg_doc = (uint32_t)atoll(e);
+    HIP_OK(hipMalloc(&d->d_dbg, 64u << 20));
+  }
+  if (const char* e = getenv("CLD_TRACE")) {
+    if (atoi(e) > 0 && n_slots > 0) {
+      HIP_OK(hipHostMalloc((void**)&d->h_trace, (size_t)n_slots * 16, hipHostMallocCoherent | hipHostMallocMapped));
+      memset(d->h_trace, 0xFF, (size_t)n_slots * 16);
+      d->trace_timeout = 20.0;
+      if (const char* t = getenv("CLD_TRACE_TIMEOUT")) d->trace_timeout = atof(t);
+    }
+  }
   return CLD_OK;
 }
 
 // Enqueue the whole pipeline for n documents already on device d.
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s) {
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (d->ev_used == d->ev_pool.size()) {
-    std::array<hipEvent_t, 3> t{};
+    std::array<hipEvent_t, 4> t{};
     for (auto& e : t) HIP_OK(hipEventCreate(&e));
     d->ev_pool.push_back(t);
   }
   auto& ev = d->ev_pool[d->ev_used++];
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
+  if (d->d_dbg) HIP_OK(hipMemsetAsync(d->d_dbg, 0, 4, s));
   HIP_OK(hipEventRecord(ev[0], s));
   if (d->front == 1)
     HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
   else
     HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, s));
   HIP_OK(hipEventRecord(ev[1], s));
-  HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                            d->d_counters, s));
-  HIP_OK(hipEventRecord(ev[2], s));
-  d->ev[0] = ev[0]; d->ev[1] = ev[1]; d->ev[2] = ev[2];
+  if (d->n_slots > 0) {
+    HIP_OK(cld_launch_long(&d->T, buf, offs, d->d_requeue, out, d->d_slots, d->n_slots, d->d_requeue2,
+                           d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc, s));
+    HIP_OK(hipEventRecord(ev[2], s));
+    HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
+                              d->d_counters, kCtrRequeue2, kCtrDequeue2, s));
+  } else {
+    HIP_OK(hipEventRecord(ev[2], s));
+    HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
+                              d->d_counters, kCtrRequeue, kCtrDequeue, s));
+  }
+  HIP_OK(hipEventRecord(ev[3], s));
+  for (int k = 0; k < 4; ++k) d->ev[k] = ev[k];
   d->last_n = n;
   d->stats_pending = true;
   return CLD_OK;
@@ -300,20 +343,25 @@ int collect_stats(Device* d) {
   uint32_t c[kCtrSlots];
   HIP_OK(hipMemcpyAsync(c, d->d_counters, sizeof(c), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
-  float ms1 = 0, ms2 = 0;
+  float ms1 = 0, ms2 = 0, ms3 = 0;
   (void)hipEventElapsedTime(&ms1, d->ev[0], d->ev[1]);
   (void)hipEventElapsedTime(&ms2, d->ev[1], d->ev[2]);
+  (void)hipEventElapsedTime(&ms3, d->ev[2], d->ev[3]);
   cld_batch_stats& st = d->last;
   memset(&st, 0, sizeof(st));
   st.docs = d->last_n;
-  st.general_docs = c[kCtrRequeue];
+  const uint32_t to_general = d->n_slots > 0 ? c[kCtrRequeue2] : c[kCtrRequeue];
+  st.general_docs = to_general;
+  st.long_docs = c[kCtrRequeue] - to_general;
   st.short_docs = d->last_n - c[kCtrRequeue];
   st.passes[0] = st.short_docs + c[kCtrPass1];
   st.passes[1] = c[kCtrPass2];
   st.passes[2] = c[kCtrPass3];
   st.passes[3] = c[kCtrError];
+  for (int k = 0; k < 8; ++k) st.long_requeue[k] = c[kCtrWhy + k];
   st.short_ms = ms1;
-  st.general_ms = ms2;
+  st.long_ms = ms2;
+  st.general_ms = ms3;
   d->stats_pending = false;
   return c[kCtrError] ? CLD_EIO : CLD_OK;
 }
@@ -333,8 +381,61 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   HIP_OK(hipMemcpyAsync(d->d_offs, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
   int rc = enqueue(d, d->d_buf, d->d_offs, n, d->d_out, d->stream);
   if (rc) return rc;
+  if (d->h_trace) {           // debug: a batch that overruns dumps where every k_long wave is
+                              // (polled before the D2H copy: a pageable copy blocks the host)
+    auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(d->stream) == hipErrorNotReady) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > d->trace_timeout) {
+        fprintf(stderr, "cld_mi355x: batch still running after %.0f s; k_long waves (doc stage value count):\n", el);
+        {
+          int untouched = 0, exited = 0;
+          for (int w = 0; w < d->n_slots; ++w) {
+            volatile uint32_t* t = d->h_trace + 4 * w;
+            untouched += t[3] == 0xFFFFFFFFu;
+            exited += (t[1] & 0xFFFF) == 100;
+          }
+          fprintf(stderr, "  %d waves: %d never started, %d exited; events: %d\n", d->n_slots, untouched, exited,
+                  (int)hipEventQuery(d->ev[1]) * 10 + (int)hipEventQuery(d->ev[2]));
+        }
+        for (int w = 0; w < d->n_slots; ++w) {
+          volatile uint32_t* t = d->h_trace + 4 * w;
+          if (t[3] != 0xFFFFFFFFu && ((t[1] & 0xFFFF) != 100 || w < 2))
+            fprintf(stderr, "  wave %d: doc %u stage %u (active lanes %u, first %u) value %u count %u\n", w, t[0],
+                    t[1] & 0xFFFF, (t[1] >> 16) & 0xFF, t[1] >> 24, t[2], t[3]);
+        }
+        hipStream_t s2;                       // the counters, through a second stream
+        uint32_t* hc = nullptr;
+        if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
+            hipHostMalloc((void**)&hc, kCtrSlots * 4, hipHostMallocCoherent) == hipSuccess &&
+            hipMemcpyAsync(hc, d->d_counters, kCtrSlots * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) {
+          for (int k = 0; k < 200 && hipStreamQuery(s2) == hipErrorNotReady; ++k)
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+          if (hipStreamQuery(s2) == hipSuccess) {
+            fprintf(stderr, "  counters:");
+            for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", hc[k]);
+            fprintf(stderr, "\n");
+          } else {
+            fprintf(stderr, "  counters: copy did not complete\n");
+          }
+        }
+        fflush(stderr);
+        abort();
+      }
+    }
+  }
   HIP_OK(hipMemcpyAsync(out, d->d_out, n * sizeof(cld_result), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
+  if (d->d_dbg) {             // debug: write the dumped words to $CLD_DEBUG_OUT
+    uint32_t cnt = 0;
+    HIP_OK(hipMemcpy(&cnt, d->d_dbg, 4, hipMemcpyDeviceToHost));
+    cnt = std::min<uint32_t>(cnt, (64u << 18) - 1);
+    std::vector<uint32_t> w(cnt + 1);
+    HIP_OK(hipMemcpy(w.data(), d->d_dbg, 4ull * (cnt + 1), hipMemcpyDeviceToHost));
+    const char* path = getenv("CLD_DEBUG_OUT") ? getenv("CLD_DEBUG_OUT") : "/tmp/cld_dbg.bin";
+    if (FILE* f = fopen(path, "wb")) { fwrite(w.data(), 4, w.size(), f); fclose(f); }
+  }
   return collect_stats(d);
 }
 
@@ -411,10 +512,10 @@ int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches
   HIP_OK(hipSetDevice(d->id));
   double a = 0, b = 0;
   for (size_t i = 0; i < d->ev_used; ++i) {
-    HIP_OK(hipEventSynchronize(d->ev_pool[i][2]));
+    HIP_OK(hipEventSynchronize(d->ev_pool[i][3]));
     float x = 0, y = 0;
     HIP_OK(hipEventElapsedTime(&x, d->ev_pool[i][0], d->ev_pool[i][1]));
-    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][2]));
+    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][3]));
     a += x; b += y;
   }
   if (short_ms) *short_ms = a;
@@ -447,7 +548,7 @@ void cld_shutdown(void) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)hipFree(d->d_blob); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
-    (void)hipFree(d->d_requeue); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
+    (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
     delete d;
