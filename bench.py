@@ -166,8 +166,11 @@ def main():
                    "mean_doc_bytes": doc_bytes / n, "parallelism": "document shards, %d rank(s)" % world},
         "input_GBps": doc_bytes * world * args.steps / elapsed / 1e9,
         "passes_hist": [int(x) for x in stats.passes[:3]],
-        "kernels": {"short_ms": short_ms / max(1, launches), "general_ms": general_ms / max(1, launches),
-                    "short_docs": int(stats.short_docs), "general_docs": int(stats.general_docs)},
+        "kernels": {"wave_ms": short_ms / max(1, launches), "long_plus_general_ms": general_ms / max(1, launches),
+                    "last_batch": {"wave_ms": stats.short_ms, "long_ms": stats.long_ms, "general_ms": stats.general_ms,
+                                   "wave_docs": int(stats.short_docs), "long_docs": int(stats.long_docs),
+                                   "general_docs": int(stats.general_docs),
+                                   "long_requeue_reasons": [int(x) for x in stats.long_requeue]}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic},
         "cpu_baseline": cpu,

@@ -65,11 +65,14 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
  * short_ms = wavefront kernel; general_ms = long-document + sequential kernels. */
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
-/* Diagnostics: per-stage shader-clock cycle sums of the wavefront kernel on
- * context `ctx` since the previous call (0 load, 1 span, 2 lower, 3 quad/uni,
- * 4 octa/bi, 5 score, 6 document level); all zero unless the runtime was
- * started with CLD_PROFILE_STAGES=1.  Resets. */
-int cld_stage_cycles(int ctx, uint64_t* cycles8);
+/* Diagnostics: per-stage shader-clock cycle sums on context `ctx` since the
+ * previous call; 16 entries.  [0..7] short-document wavefront kernel (0 load,
+ * 1 span, 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level);
+ * [8..15] long-document kernel (8 classify, 9 span+lowercase, 10 squeeze
+ * test, 11 repeats, 12 word lists + quad chain, 13 quad hits, 14 octa/uni/bi
+ * hits, 15 linearize/chunk/score).  All zero unless the runtime was started
+ * with CLD_PROFILE_STAGES=1.  Resets. */
+int cld_stage_cycles(int ctx, uint64_t* cycles16);
 
 /* Batch detection.  Documents are [buf + offsets[i], buf + offsets[i+1]),
  * i < n (offsets has n+1 entries, non-decreasing).  Each document is scored

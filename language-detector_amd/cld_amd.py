@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libcld_mi355x.so")
+LIB_PATH = os.environ.get("CLD_MI355X_LIB") or os.path.join(HERE, "build", "libcld_mi355x.so")
 TABLES = os.path.join(HERE, "data", "cld2_mi355x.cldt")
 
 RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "i1", 3),
@@ -104,7 +104,7 @@ def kernel_time(ctx=0):
 
 def stage_cycles(ctx=0):
     """Per-stage cycle sums of the wavefront kernel (CLD_PROFILE_STAGES=1)."""
-    c = np.zeros(8, dtype=np.uint64)
+    c = np.zeros(16, dtype=np.uint64)
     rc = lib().cld_stage_cycles(ctx, ctypes.c_void_p(c.ctypes.data))
     if rc != 0:
         raise CldError("cld_stage_cycles failed: %d" % rc)

@@ -41,9 +41,10 @@ hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               hipStream_t s);
 size_t cld_long_slot_bytes();
+int cld_long_waves_per_simd();
 hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
-                           hipStream_t s);
+                           unsigned long long* prof, hipStream_t s);
 }
 #endif

@@ -92,23 +92,30 @@ __global__ __launch_bounds__(64 * WPB, 6) void k_wave(DevTables T, const uint8_t
 // blockIdx.x * WPB + wave and pulls documents from the wave kernel's re-queue
 // list (one atomic per document) until the list is drained -- every wave
 // reaches that exit.  Documents it cannot reproduce go to the k_general list.
-template <int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_long(DevTables T, const uint8_t* __restrict__ buf,
+// LNG_WPS waves per SIMD (4: ~25 VGPRs spill, still faster than 3 spill-free: the kernel is latency-bound)
+#ifndef LNG_WPS
+#define LNG_WPS 4
+#endif
+template <int WPB, bool DIAG>
+__global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const uint8_t* __restrict__ buf,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ list,
                                                   cld_result* __restrict__ out, uint8_t* __restrict__ slots,
                                                   uint32_t* __restrict__ requeue2,
                                                   uint32_t* __restrict__ counters, uint32_t* trace,
-                                                  uint32_t* dbg, uint32_t dbg_doc) {
+                                                  uint32_t* dbg, uint32_t dbg_doc,
+                                                  unsigned long long* prof) {
   __shared__ lng::Smem smem[WPB];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* tr = trace ? trace + 4 * (blockIdx.x * WPB + wv) : nullptr;
+  // wave index through readfirstlane: the slot pointer (and every S.field
+  // address) is then scalar instead of a VGPR pair per field
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  uint32_t* tr = (DIAG && trace) ? trace + 4 * (blockIdx.x * WPB + wv) : nullptr;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::Slot));
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
+  if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
-  lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
+  if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
   for (;;) {
     // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
     // A lane-0-only atomic feeding readfirstlane at the loop head let the
@@ -120,13 +127,14 @@ __global__ __launch_bounds__(64 * WPB) void k_long(DevTables T, const uint8_t* _
     const uint64_t len = b - a;
     int passes = 0;
     if (lane == 0) {
-      smem[wv].dbg = (dbg && i == dbg_doc) ? dbg : nullptr;
+      smem[wv].dbg = (DIAG && dbg && i == dbg_doc) ? dbg : nullptr;
       smem[wv].dbg_pos = 0;
+      smem[wv].prof = DIAG ? prof : nullptr;
     }
     wave::wsync();
     if (exact && len <= (uint64_t)lng::kDocCap)
-      passes = lng::detect(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i);
-    lng::trace(tr, lane, i, 99, passes);
+      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i);
+    if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (lane == 0) {
       if (passes >= 1 && passes <= 2) {
@@ -138,22 +146,29 @@ __global__ __launch_bounds__(64 * WPB) void k_long(DevTables T, const uint8_t* _
       }
     }
   }
-  lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
+  if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
 }
 
 }  // namespace cld
 
 extern "C" {
 size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }
+int cld_long_waves_per_simd() { return LNG_WPS; }
 
 hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
-                           hipStream_t s) {
+                           unsigned long long* prof, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
-  hipLaunchKernelGGL((cld::k_long<kLongWPB>), grid, block, 0, s, *T, buf, offs, list, out, slots, requeue2,
-                     counters, trace, dbg, dbg_doc);
+  // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
+  // they cost the production kernel registers even when switched off
+  if (trace || dbg || prof)
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, *T, buf, offs, list, out, slots,
+                       requeue2, counters, trace, dbg, dbg_doc, prof);
+  else
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, *T, buf, offs, list, out, slots,
+                       requeue2, counters, trace, dbg, dbg_doc, prof);
   return hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ using wave::rdlu;
 using wave::ufl;
 using wave::ufl64;
 using wave::uflu;
+using wave::wmax;
 using wave::wor64;
 using wave::wsum;
 using wave::wsync;
@@ -98,7 +99,22 @@ struct alignas(16) Smem {
   DocTote dt;
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
   uint32_t dbg_pos;
+  unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
 };
+
+#ifndef LNG_PROF_ON
+
+#endif
+// Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
+// 3 repeats, 4 word lists + quad chain, 5 quad hits, 6 octa/uni/bi hits,
+// 7 linearize/chunk/score
+__device__ __forceinline__ void mark(Smem& s, int lane, int stage, long long& t) {
+  if (s.prof) {
+    const long long now = (long long)clock64();
+    if (lane == 0) atomicAdd(&s.prof[stage], (unsigned long long)(now - t));
+    t = now;
+  }
+}
 
 // Debug dump records (u32 words): 'S' span {ul, tb, pass}; 'R' round {off, next,
 // nb, nd, nx, then nb+nd+nx (offset, indirect) pairs}; 'C' chunk {lo, hi, lang1,
@@ -223,24 +239,30 @@ __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lan
   return __ballot(bad != 0) == 0;
 }
 
-// --------------------------------------- stage 1: span text, lowered (fused)
-// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) followed by
-// LowerScriptSpan (:1033-1054).  Span text = ' ' + run + ' ' + run + ' ' ...
-// A run starts at a letter stop of the span script (or Inherited) and ends at
-// the first break character; the gap after it runs to the next letter stop,
-// which continues the span (span script / Inherited) or ends it.  Within a
-// 64-byte window every byte's state is the type of the last event at or
-// before it (break -> gap, continuing letter stop -> run), so all lanes decide
-// at once.  The soft limit (put >= put_soft_limit after a run's space) and the
-// hard limit (put >= kMaxScriptBytes after a character) come from prefix sums
-// of the raw byte count.  The characters go straight through the lowercaser
-// (each one starts and ends in state 0, checked) into lb.
+// The sequential lowercaser for the rare cut-character tail, kept out of
+// line so its state does not count against the kernel's registers.
+__device__ __noinline__ int lower_tail(const DevTables& T, const uint8_t* in, int ilen, uint8_t* out, int olen) {
+  return lower_replace(T, in, ilen, out, olen);
+}
+
+// --------------------------------------- stage 1: span text, then lowercase
+// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) into sb, then
+// LowerScriptSpan (:1033-1054) from sb into lb.  Span text = ' ' + run + ' ' +
+// run + ' ' ... + "   \0".  A run starts at a letter stop of the span script
+// (or Inherited) and ends at the first break character; the gap after it runs
+// to the next letter stop, which continues the span (span script / Inherited)
+// or ends it.  Within a 64-byte window every byte's state is the type of the
+// last event at or before it (break -> gap, continuing letter stop -> run), so
+// all lanes decide at once.  The soft limit (put >= put_soft_limit after a
+// run's space) and the hard limit (put >= kMaxScriptBytes after a character)
+// come from a prefix sum of the byte count.  The two passes keep register
+// pressure low enough for the kernel's occupancy.
 // A final character cut by the document end that lands in a run is copied
-// with NUL bytes (DocView), and the lowercaser stops at its lead byte; that
+// with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
-__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
-                         int& status, int lane) {
+__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, uint8_t* sb, int& next,
+                         int& ulscript, int& status, int lane) {
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
   const int remaining = L - next;
@@ -255,9 +277,9 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   }
   const int ss = ufl(S.sn[q]);
   ulscript = ss;
-  if (lane == 0) lb[0] = ' ';
-  int lpos = 1, put = 1, grow = 0, bad = 0, nxt = L;
-  bool run = false, cut = false;
+  if (lane == 0) sb[0] = ' ';
+  int put = 1, bad = 0, nxt = L, cutpos = -1;
+  bool run = false;
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
     const bool valid = x >= q && x < L;
@@ -281,45 +303,38 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       }
     }
     const uint64_t Bm = __ballot(brk), Om = __ballot(ok);
-    const uint64_t ev_le = (Bm | Om) & mask_le(lane), ev_lt = (Bm | Om) & lanemask_lt(lane);
+    const uint64_t evm = Bm | Om;
+    const uint64_t ev_le = evm & mask_le(lane), ev_lt = evm & lanemask_lt(lane);
     const bool inrun = ev_le ? ((Om >> topbit(ev_le)) & 1) : run;
     const bool prev_run = ev_lt ? ((Om >> topbit(ev_lt)) & 1) : run;
     const bool endc = foreign && (brk || !prev_run);     // a letter stop of another script after a gap
     const bool sep = brk && prev_run;                    // a run ends here: its ' '
     const bool cutc = lead && x + n > L;                 // only the last character
-    const bool chr = lead && inrun && !cutc;
+    const bool chr = lead && inrun;
     const int raw = chr ? n : (sep ? 1 : 0);
     const int pre = excl_scan(raw, lane);
     const uint64_t Em = __ballot(endc);
-    const uint64_t Hm = __ballot(chr && put + pre + n >= kMaxScriptBytes);
-    const uint64_t Cm = __ballot(cutc && lead && inrun);
+    const uint64_t Hm = __ballot(chr && !cutc && put + pre + n >= kMaxScriptBytes);
     const uint64_t Sm = __ballot(sep && put + pre + 1 >= soft);
     const uint64_t stopm = Em | Hm | Sm;
     const int stop = stopm ? __builtin_ctzll(stopm) : 64;
     const bool act = lane <= stop;
     const bool hard_here = lane == stop && ((Hm >> lane) & 1);
-    const bool out_chr = act && chr;
-    const bool out_sep = act && (sep || hard_here);
-    uint64_t o = 0;
-    int olen = 0;
-    if (out_chr) {
-      if (!lower_char(T, dv.p + x, n, o, olen)) {
-        bad = 1;
-        olen = 0;
+    if (act) {
+      const int o = put + pre;
+      if (chr) {
+        for (int k = 0; k < n; ++k) sb[o + k] = dv.at(x + k);
+        if (cutc) cutpos = o;
+        if (hard_here) sb[o + n] = ' ';
+      } else if (sep) {
+        sb[o] = ' ';
       }
-      grow += olen > n ? olen - n : 0;
     }
-    const int tl = olen + (out_sep ? 1 : 0);
-    const int opre = excl_scan(tl, lane);
-    const int otot = rdl(opre + tl, 63);
     put += wsum(act ? raw + (hard_here ? 1 : 0) : 0);
-    if (lpos + otot + 64 > kLB) {
+    if (put + 64 > kMaxScriptBuffer) {
       bad = 1;
       break;
     }
-    for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(o >> (8 * k));
-    if (out_sep) lb[lpos + opre + olen] = ' ';
-    lpos += otot;
     if (stop < 64) {
       const int xs = (w << 6) + stop;
       if ((Hm >> stop) & 1) nxt = find_first_g(S.lsm, xs + rdl(n, stop), L);
@@ -327,44 +342,62 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       else nxt = xs;                                                  // another script's letter stop
       break;
     }
-    const uint64_t ev = Bm | Om;
-    if (ev) run = (Om >> topbit(ev)) & 1;
-    if (Cm) {                                                         // the cut last character
-      cut = true;
-      nxt = L;
-      const int xc = (w << 6) + __builtin_ctzll(Cm);
-      int filled = 0;
-      if (lane == 0) {
-        uint8_t tail[12];
-        const int nc = utf8_len(dv.p[xc]);
-        for (int k = 0; k < nc; ++k) tail[k] = (uint8_t)dv.at(xc + k);
-        for (int k = 0; k < 4; ++k) tail[nc + k] = ' ';               // separator + "   " (ilen stops before \0)
-        filled = lower_replace(T, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
-      }
-      lpos += rdl(filled, 0);
-      put += 1;
-      break;
-    }
+    if (evm) run = (Om >> topbit(evm)) & 1;
     if ((w << 6) + 64 >= L) {                                         // end of document
       if (run) {
-        if (lane == 0) lb[lpos] = ' ';
-        ++lpos;
+        if (lane == 0) sb[put] = ' ';
         ++put;
       }
       nxt = L;
       break;
     }
   }
-  if (!__ballot(bad != 0))
-    for (int k = lane; k < 40; k += 64) lb[lpos + k] = (!cut && k < 3) ? ' ' : 0;   // "   " pad, NULs
-  if (cut) lpos -= 3;                                                 // text_bytes = filled - 3
+  if (lane < 4) sb[put + lane] = lane < 3 ? ' ' : 0;
+  next = nxt;
+  cutpos = (int)wmax((uint32_t)(cutpos + 1)) - 1;
+  gsync();
+  if (__ballot(bad != 0)) {
+    status = -1;
+    return 0;
+  }
+  // LowerScriptSpan: sb[0, put + 3) -> lb, one character per lane; each
+  // character must start and end in state 0 (checked in lower_char).
+  const int ilen = put + 3;
+  const int lim = cutpos >= 0 ? cutpos : ilen;
+  int lpos = 0, grow = 0;
+  for (int w0 = 0; w0 < lim; w0 += 64) {
+    const int p = w0 + lane;
+    uint64_t o = 0;
+    int olen = 0;
+    if (p < lim && (sb[p] & 0xC0) != 0x80) {
+      const int n = utf8_len(sb[p]);
+      if (!lower_char(T, sb + p, n, o, olen)) {
+        bad = 1;
+        olen = 0;
+      }
+      grow += olen > n ? olen - n : 0;
+    }
+    const int opre = excl_scan(olen, lane);
+    const int otot = rdl(opre + olen, 63);
+    if (lpos + otot + 64 > kLB) {
+      bad = 1;
+      break;
+    }
+    for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(o >> (8 * k));
+    lpos += otot;
+  }
+  if (cutpos >= 0) {                                                  // the cut last character
+    int filled = 0;
+    if (lane == 0) filled = lower_tail(T, sb + cutpos, ilen - cutpos, lb + lpos, kMaxScriptLowerBuffer - lpos);
+    lpos += rdl(filled, 0);
+  }
+  for (int k = lane; k < 40; k += 64) lb[lpos + k] = 0;
   // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
   // spans near the 40 KB limit that also grow; re-queue those.
-  if (put + 3 + wsum(grow) > kMaxScriptLowerBuffer - 8) bad = 1;
-  next = nxt;
+  if (ilen + wsum(grow) > kMaxScriptLowerBuffer - 8) bad = 1;
   gsync();
   if (__ballot(bad != 0)) status = -1;
-  return lpos;
+  return lpos - 3;                                                    // text_bytes = filled - 3
 }
 
 // ------------------------------------------------------ predictor (squeeze/repeats)
@@ -860,6 +893,7 @@ __device__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& 
 // entries and lands in the first chunk k with that count < E_k, i.e. with
 // o <= theta_k = be_off[E_k - 2].  Every chunk is therefore one contiguous
 // range of each stream.
+template <bool D>
 __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int lowest, int dummy_off, int lane) {
   const DevTbl& bo = cjk ? T.compat : T.quad;
@@ -1086,7 +1120,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       if (cs1 != 0 && cs1 == close_set(T, lang2)) rd = 100;
       const int rsc = (uint8_t)reliability_expected(actual, expected);
       if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
-      if (s.dbg) {
+      if (D && s.dbg) {
         uint32_t* o = s.dbg + 1 + s.dbg_pos;
         const uint32_t v[18] = {'C', (uint32_t)lo, (uint32_t)hi, (uint32_t)lang1, (uint32_t)lang2, s1, s2,
                                 grams, (uint32_t)rd, (uint32_t)rsc, (uint32_t)bs, (uint32_t)be, (uint32_t)ds,
@@ -1130,6 +1164,7 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
+template <bool D>
 __device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb, int ulscript,
                            int lane, uint32_t* tr, uint32_t doc) {
   const int rt = rtype_of(T, ulscript);
@@ -1140,14 +1175,17 @@ __device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* 
   }
   if (tb <= 1) return true;
   int off = 1;
+  long long t = (D && s.prof) ? (long long)clock64() : 0;
   if (rt == RTypeCJK) {
     while (off < tb) {
       int nb, nd, nx;
-      trace(tr, lane, doc, 20, off);
+      if constexpr (D) trace(tr, lane, doc, 20, off);
       const int next = cjk_round(T, text, tb, S, off, nb, nd, nx, lane);
-      trace(tr, lane, doc, 21, next);
-      dbg_round(S, s, off, next, nb, nd, nx, lane);
-      score_round(T, S, s, ulscript, true, nb, nd, nx, off, next, lane);
+      if constexpr (D) trace(tr, lane, doc, 21, next);
+      if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, lane);
+      if constexpr (D) mark(s, lane, 6, t);
+      score_round<D>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane);
+      if constexpr (D) mark(s, lane, 7, t);
       off = next;
     }
     return true;
@@ -1155,20 +1193,24 @@ __device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* 
   const int start = 1 + (ufl(text[1]) == ' ' ? 1 : 0);
   int nws, nsp;
   if (!word_lists(text, tb, start, S, nws, nsp, lane)) return false;
-  trace(tr, lane, doc, 10, nws);
+  if constexpr (D) trace(tr, lane, doc, 10, nws);
   const int nch = build_chain(text, tb, S, nws, lane);
   if (nch < 0) return false;
-  trace(tr, lane, doc, 11, nch);
+  if constexpr (D) trace(tr, lane, doc, 11, nch);
+  if constexpr (D) mark(s, lane, 4, t);
   int c0 = 0, j0 = 0;
   while (off < tb) {
     int nb, nd, nx;
-    trace(tr, lane, doc, 12, off);
+    if constexpr (D) trace(tr, lane, doc, 12, off);
     const int next = quad_round(T, text, tb, S, nch, c0, nb, lane);
-    trace(tr, lane, doc, 13, next);
+    if constexpr (D) trace(tr, lane, doc, 13, next);
+    if constexpr (D) mark(s, lane, 5, t);
     octa_round(T, text, S, nsp, j0, off, next, nd, nx, lane);
-    trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
-    dbg_round(S, s, off, next, nb, nd, nx, lane);
-    score_round(T, S, s, ulscript, false, nb, nd, nx, off, next, lane);
+    if constexpr (D) trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
+    if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, lane);
+    if constexpr (D) mark(s, lane, 6, t);
+    score_round<D>(T, S, s, ulscript, false, nb, nd, nx, off, next, lane);
+    if constexpr (D) mark(s, lane, 7, t);
     off = next;
   }
   return true;
@@ -1178,6 +1220,7 @@ __device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* 
 // document: pass 1, and pass 2 with Repeats when pass 1 is not good enough.
 // Returns the number of passes, or -reason (kWhy*) to re-queue.
 enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
+template <bool D>
 __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc) {
   const int unk = (int)T.unknown_lang;
@@ -1192,9 +1235,11 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
   }
   if (L > kDocCap - 64) return -kWhyLength;
   const DocView dv{g, L};
-  trace(tr, lane, doc, 1, L);
+  if constexpr (D) trace(tr, lane, doc, 1, L);
+  long long t = (D && s.prof) ? (long long)clock64() : 0;
   if (!classify(T, dv, S, lane)) return -kWhyClassify;
-  trace(tr, lane, doc, 2, 0);
+  if constexpr (D) mark(s, lane, 0, t);
+  if constexpr (D) trace(tr, lane, doc, 2, 0);
   for (int pass = 1; pass <= 2; ++pass) {
     if (lane == 0) s.dt.init();
     if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
@@ -1204,24 +1249,28 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
     int next = 0, total = 0;
     for (;;) {
       int ul = 0, st = 0;
-      trace(tr, lane, doc, 3, next);
-      int tb = next_span(T, dv, S, S.lb[0], next, ul, st, lane);
-      trace(tr, lane, doc, 4, tb);
+      if constexpr (D) trace(tr, lane, doc, 3, next);
+      int tb = next_span(T, dv, S, S.lb[0], S.lb[1], next, ul, st, lane);
+      if constexpr (D) trace(tr, lane, doc, 4, tb);
+      if constexpr (D) mark(s, lane, 1, t);
       if (st == 0) break;
       if (st < 0) return -kWhySpan;
       const uint8_t* text = S.lb[0];
       if (pass == 1) {
         if (tb > 2048 && squeeze_trigger(S, text, lane)) return -kWhySqueeze;   // Squeeze restart: k_general
+        if constexpr (D) mark(s, lane, 2, t);
       } else {
         tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, lane);
         text = S.lb[1];
+        if constexpr (D) mark(s, lane, 3, t);
       }
-      trace(tr, lane, doc, 5, tb);
-      {
+      if constexpr (D) trace(tr, lane, doc, 5, tb);
+      if constexpr (D) {
         const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
         dbg_words(s, lane, v, 4);
       }
-      if (!score_span(T, S, s, text, tb, ul, lane, tr, doc)) return -kWhyCapacity;
+      if (!score_span<D>(T, S, s, text, tb, ul, lane, tr, doc)) return -kWhyCapacity;
+      t = (D && s.prof) ? (long long)clock64() : 0;
       total += tb;
     }
     int res = 1;

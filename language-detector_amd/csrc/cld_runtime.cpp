@@ -270,13 +270,13 @@ int init_device(Device* d) {
   if (const char* e = getenv("CLD_FRONT")) d->front = strcmp(e, "lane") == 0 ? 1 : 0;
   if (const char* e = getenv("CLD_PROFILE_STAGES")) {
     if (atoi(e) > 0) {
-      HIP_OK(hipMalloc(&d->d_prof, 8 * sizeof(unsigned long long)));
-      HIP_OK(hipMemset(d->d_prof, 0, 8 * sizeof(unsigned long long)));
+      HIP_OK(hipMalloc(&d->d_prof, 16 * sizeof(unsigned long long)));
+      HIP_OK(hipMemset(d->d_prof, 0, 16 * sizeof(unsigned long long)));
     }
   }
   HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
   // k_long: one slot per resident wavefront of its persistent grid
-  int waves = 8;
+  int waves = 4 * cld_long_waves_per_simd();   // fill every SIMD at the kernel's occupancy
   if (const char* e = getenv("CLD_LONG_WAVES")) waves = atoi(e);
   if (const char* e = getenv("CLD_LONG")) if (atoi(e) == 0) waves = 0;
   int n_slots = (prop.multiProcessorCount * waves / kLongWPB) * kLongWPB;
@@ -322,7 +322,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     HIP_OK(cld_launch_long(&d->T, buf, offs, d->d_requeue, out, d->d_slots, d->n_slots, d->d_requeue2,
-                           d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc, s));
+                           d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
+                           d->d_prof ? d->d_prof + 8 : nullptr, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               d->d_counters, kCtrRequeue2, kCtrDequeue2, s));
@@ -494,14 +495,14 @@ int cld_init_device(const char* tables_path, int device) {
   return g_init_rc = CLD_OK;
 }
 
-int cld_stage_cycles(int ctx, uint64_t* cycles8) {
-  if (!cycles8 || ctx < 0 || ctx >= (int)g_devs.size()) return CLD_EINVAL;
+int cld_stage_cycles(int ctx, uint64_t* cycles16) {
+  if (!cycles16 || ctx < 0 || ctx >= (int)g_devs.size()) return CLD_EINVAL;
   Device* d = g_devs[ctx];
-  if (!d->d_prof) { memset(cycles8, 0, 8 * sizeof(uint64_t)); return CLD_OK; }
+  if (!d->d_prof) { memset(cycles16, 0, 16 * sizeof(uint64_t)); return CLD_OK; }
   (void)hipSetDevice(d->id);
   HIP_OK(hipStreamSynchronize(d->stream));
-  HIP_OK(hipMemcpy(cycles8, d->d_prof, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_OK(hipMemset(d->d_prof, 0, 8 * sizeof(unsigned long long)));
+  HIP_OK(hipMemcpy(cycles16, d->d_prof, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemset(d->d_prof, 0, 16 * sizeof(unsigned long long)));
   return CLD_OK;
 }
 
