@@ -34,6 +34,7 @@ struct DevTables {
   const uint8_t* rtype;
   const uint16_t* deflang;
   const uint16_t* closest;
+  const uint64_t* cpt;        // per-character properties of 1-3 byte sequences (cld_long.hip, built on device)
   const uint8_t* close_set;
   uint32_t n_expected, l2p_size, n_scripts, n_langs, n_closest;
   uint32_t latin, cyrillic, arabic, common, inherited;

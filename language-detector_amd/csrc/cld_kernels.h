@@ -41,6 +41,8 @@ hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               hipStream_t s);
 size_t cld_long_slot_bytes();
+size_t cld_cpt_entries();
+hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);
 int cld_long_waves_per_simd();
 hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,

@@ -115,6 +115,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
+  if (lane == 0) smem[wv].kscript = -1;
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
   for (;;) {
     // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
@@ -149,9 +150,38 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
 }
 
+// Character property table (lng::cpt_eval over every 1-3 byte sequence).
+__global__ __launch_bounds__(256) void k_build_cpt(DevTables T, uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= lng::kCptSize) return;
+  uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int n;
+  if (i < 128) {
+    b[0] = (uint8_t)i;
+    n = 1;
+  } else if (i < 2176) {
+    const int j = i - 128;
+    b[0] = (uint8_t)(0xC0 | (j >> 6));
+    b[1] = (uint8_t)(0x80 | (j & 63));
+    n = 2;
+  } else {
+    const int j = i - 2176;
+    b[0] = (uint8_t)(0xE0 | (j >> 12));
+    b[1] = (uint8_t)(0x80 | ((j >> 6) & 63));
+    b[2] = (uint8_t)(0x80 | (j & 63));
+    n = 3;
+  }
+  out[i] = lng::cpt_eval(T, b, n);
+}
+
 }  // namespace cld
 
 extern "C" {
+size_t cld_cpt_entries() { return cld::lng::kCptSize; }
+hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(cld::k_build_cpt, dim3((cld::lng::kCptSize + 255) / 256), dim3(256), 0, s, *T, out);
+  return hipGetLastError();
+}
 size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }
 int cld_long_waves_per_simd() { return LNG_WPS; }
 

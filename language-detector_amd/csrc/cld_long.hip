@@ -72,7 +72,8 @@ struct Slot {
   uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
   uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats)
   uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces
-  uint8_t sn[kDocCap + 128];             // GetUTF8LetterScriptNum per document byte
+  uint32_t cls[kDocCap + 64];            // per document byte, see cls_* below
+  uint32_t low[kDocCap + 64];            // lowered bytes of the character starting here (<= 4)
   uint8_t lb[2][kLB];                    // lowered span text; [1] = after CheapRepWords
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
@@ -84,7 +85,9 @@ struct Slot {
   uint16_t x_off[kHB];
   uint32_t x_ind[kHB];
   uint16_t be_off[kEB];
-  uint32_t be_lp[kEB];
+  uint64_t be_add[kEB];                  // tote adds per emission (tote_adds), base / delta / distinct
+  uint64_t d_add[kHB];
+  uint64_t x_add[kHB];
 };
 
 // Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4)
@@ -95,7 +98,10 @@ struct alignas(16) Smem {
   uint16_t E[kMaxCh];                    // base emission number closing chunk k
   uint16_t bst[kMaxCh + 1];
   uint16_t st[2][kMaxCh + 1];            // first delta [0] / distinct [1] emission of chunk k
-  uint32_t ring[2][4];                   // distinct boosts, latn / othr, oldest first
+  uint64_t ring[2][4];                   // distinct boosts (as tote adds), latn / othr, oldest first
+  uint32_t kl[256];                      // per key of the span script: language | close set << 16
+  int16_t ke[256];                       //   and expected score (kAvgDeltaOctaScore) of that language
+  int kscript;                           // script the key table holds (-1: none)
   DocTote dt;
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
   uint32_t dbg_pos;
@@ -141,6 +147,18 @@ __device__ __forceinline__ void trace(uint32_t* tr, int lane, uint32_t doc, uint
     __hip_atomic_fetch_add(&tr[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
+
+// Per-byte class word built by classify():
+//   bits 0-7 script number (GetUTF8LetterScriptNum), 8-15 script of the next
+//   character, 16-18 character length, 19 lead byte, 20 letter stop,
+//   21 cut by the document end, 22 not lowerable here, 24-27 lowered length.
+__device__ __forceinline__ int cls_sn(uint32_t c) { return c & 0xFF; }
+__device__ __forceinline__ int cls_sn2(uint32_t c) { return (c >> 8) & 0xFF; }
+__device__ __forceinline__ int cls_n(uint32_t c) { return (c >> 16) & 7; }
+__device__ __forceinline__ bool cls_lead(uint32_t c) { return (c >> 19) & 1; }
+__device__ __forceinline__ bool cls_cut(uint32_t c) { return (c >> 21) & 1; }
+__device__ __forceinline__ bool cls_nolow(uint32_t c) { return (c >> 22) & 1; }
+__device__ __forceinline__ int cls_olen(uint32_t c) { return (c >> 24) & 15; }
 
 __device__ __forceinline__ int topbit(uint64_t m) { return 63 - __builtin_clzll(m); }
 __device__ __forceinline__ uint64_t mask_le(int lane) { return lane >= 63 ? ~0ull : ((2ull << lane) - 1); }
@@ -204,33 +222,101 @@ __device__ int scan_char(const DevTables& T, const DocView& d, int p, int n, boo
   return tb == tb0 ? 0 : -1;
 }
 
-// Script number per byte (also the 4 NUL bytes after the end, as DocView
-// reads them) and the letter-stop mask; false if the document does not tile
-// into well-formed characters with local scanner behaviour.
+// Character property table: for every well-formed 1-, 2- and 3-byte UTF-8
+// sequence (indexed by its bytes, so overlong forms keep their own entry) the
+// outcome of the three per-character machines -- GetUTF8LetterScriptNum,
+// the ScanToLetterOrSpecial class and the LowerScriptSpan bytes.  Built once
+// per GPU by k_build_cpt from the very device functions below; 4-byte and
+// malformed sequences still run the machines.
+//   bits 0-7 script, 8-9 scan class (0 continue, 1 stop, 3 non-local),
+//   10 lowerable here, 11-14 lowered length, 32-63 lowered bytes
+constexpr int kCptSize = 128 + 2048 + 65536;
+__device__ __forceinline__ int cpt_index(uint32_t b0, uint32_t b1, uint32_t b2, int n) {
+  if (n == 1) return (int)b0;
+  if (n == 2) return 128 + (int)((b0 & 0x1F) << 6 | (b1 & 0x3F));
+  return 2176 + (int)((b0 & 0x0F) << 12 | (b1 & 0x3F) << 6 | (b2 & 0x3F));
+}
+__device__ uint64_t cpt_eval(const DevTables& T, const uint8_t* b, int n) {
+  const DocView dv{b, n};
+  const int sn = script_num(T, dv, 0);
+  const int st = scan_char(T, dv, 0, n, false);
+  uint64_t o = 0;
+  int olen = 0;
+  const bool lowok = lower_char(T, b, n, o, olen) && olen <= 4;
+  return (uint64_t)(sn & 0xFF) | ((uint64_t)(st < 0 ? 3 : st) << 8) | ((uint64_t)lowok << 10) |
+         ((uint64_t)(lowok ? olen : 0) << 11) | ((lowok ? (o & 0xFFFFFFFFull) : 0ull) << 32);
+}
+
+// Per character (lead byte): script number, script of the next character,
+// scanner stop, and the lowered bytes (LowerScriptSpan is per character once
+// each one starts and ends in state 0, checked by lower_char) -- all computed
+// once per document, so the span builder and the second pass only copy.
+// The 8 bytes a lane needs are loaded up front (one round trip), then one
+// property-table lookup per character.  False if the document does not tile
+// into characters with local scanner behaviour.
 __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lane) {
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
-  const int nw = (L + 4 + 63) >> 6;
+  const int nw = (L + 63) >> 6;
   for (int w = 0; w < nw; ++w) {
     const int p = (w << 6) + lane;
     bool ls = false;
-    int sn = 0;
-    if (p < L + 4) sn = script_num(T, dv, p);
+    uint32_t cw = 0, lw = 0;
     if (p < L) {
-      const uint8_t c = dv.at(p);
+      uint32_t b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = dv.at(p + k);
+      const uint32_t c = b[0];
       if ((c & 0xC0) == 0x80) {
         ++conts;
       } else {
-        const int n = utf8_len(c);
+        const int n = utf8_len((uint8_t)c);
         const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
-        for (int k = 1; k < avail; ++k) bad |= ((dv.at(p + k) & 0xC0) != 0x80);
+        bool wf = true;
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+          if (k < avail) wf &= (b[k] & 0xC0) == 0x80;
+        bad |= !wf;
         need += avail - 1;
-        const int st = scan_char(T, dv, p, avail, avail < n);
+        int sn, st, olen = 0;
+        bool lowok;
+        if (avail == n && n <= 3) {
+          const uint64_t e = T.cpt[cpt_index(b[0], b[1], b[2], n)];
+          sn = (int)(e & 0xFF);
+          st = (int)((e >> 8) & 3);
+          if (st == 3) st = -1;
+          lowok = (e >> 10) & 1;
+          olen = (int)((e >> 11) & 15);
+          lw = (uint32_t)(e >> 32);
+        } else {                                   // 4-byte or cut: run the machines
+          sn = script_num(T, dv, p);
+          st = scan_char(T, dv, p, avail, avail < n);
+          uint64_t o = 0;
+          lowok = avail == n && lower_char(T, dv.p + p, n, o, olen) && olen <= 4;
+          if (!lowok) olen = 0;
+          lw = (uint32_t)o;
+        }
+        // script of the next character (its bytes are b[n..n+3]; NULs past the end)
+        int sn2;
+        const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
+        const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
+        const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
+        const int n2 = utf8_len((uint8_t)c2);
+        if (c2 < 0x80) sn2 = (int)(T.cpt[c2] & 0xFF);
+        else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) sn2 = (int)(T.cpt[cpt_index(c2, d1, 0, 2)] & 0xFF);
+        else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80)
+          sn2 = (int)(T.cpt[cpt_index(c2, d1, d2, 3)] & 0xFF);
+        else sn2 = script_num(T, dv, p + n);
         if (st < 0) bad = 1;
         ls = st > 0 && sn != 0;
+        cw = (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
+             ((uint32_t)(avail < n) << 21) | ((uint32_t)!lowok << 22) | ((uint32_t)olen << 24);
       }
     }
-    if (p < L + 4) S.sn[p] = (uint8_t)sn;
+    if (p < L) {
+      S.cls[p] = cw;
+      S.low[p] = lw;
+    }
     const uint64_t m = __ballot(ls);
     if (lane == 0) S.lsm[w] = m;
   }
@@ -245,24 +331,24 @@ __device__ __noinline__ int lower_tail(const DevTables& T, const uint8_t* in, in
   return lower_replace(T, in, ilen, out, olen);
 }
 
-// --------------------------------------- stage 1: span text, then lowercase
-// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) into sb, then
-// LowerScriptSpan (:1033-1054) from sb into lb.  Span text = ' ' + run + ' ' +
-// run + ' ' ... + "   \0".  A run starts at a letter stop of the span script
-// (or Inherited) and ends at the first break character; the gap after it runs
-// to the next letter stop, which continues the span (span script / Inherited)
-// or ends it.  Within a 64-byte window every byte's state is the type of the
-// last event at or before it (break -> gap, continuing letter stop -> run), so
-// all lanes decide at once.  The soft limit (put >= put_soft_limit after a
-// run's space) and the hard limit (put >= kMaxScriptBytes after a character)
-// come from a prefix sum of the byte count.  The two passes keep register
-// pressure low enough for the kernel's occupancy.
+// --------------------------------------- stage 1: span text, lowered
+// GetOneScriptSpan (getonescriptspan.cc:799-1027, plain text) followed by
+// LowerScriptSpan (:1033-1054), straight into lb.  Span text = ' ' + run +
+// ' ' + run + ' ' ... + "   \0".  A run starts at a letter stop of the span
+// script (or Inherited) and ends at the first break character; the gap after
+// it runs to the next letter stop, which continues the span (span script /
+// Inherited) or ends it.  Within a 64-byte window every byte's state is the
+// type of the last event at or before it (break -> gap, continuing letter
+// stop -> run), so all lanes decide at once.  The soft limit (put >=
+// put_soft_limit after a run's space) and the hard limit (put >=
+// kMaxScriptBytes after a character) come from a prefix sum of the raw byte
+// count; the lowered bytes were precomputed per character by classify().
 // A final character cut by the document end that lands in a run is copied
 // with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
-__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, uint8_t* sb, int& next,
-                         int& ulscript, int& status, int lane) {
+__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
+                         int& status, int lane) {
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
   const int remaining = L - next;
@@ -275,29 +361,30 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     status = 0;
     return 0;
   }
-  const int ss = ufl(S.sn[q]);
+  const int ss = ufl(cls_sn(S.cls[q]));
   ulscript = ss;
-  if (lane == 0) sb[0] = ' ';
-  int put = 1, bad = 0, nxt = L, cutpos = -1;
+  if (lane == 0) lb[0] = ' ';
+  int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
     const bool valid = x >= q && x < L;
-    const uint8_t c = valid ? dv.p[x] : (uint8_t)0;
-    const bool lead = valid && (c & 0xC0) != 0x80;
-    const int n = utf8_len(c);
+    const uint32_t cw = valid ? S.cls[x] : 0u;
+    const uint32_t lw = valid ? S.low[x] : 0u;
+    const bool lead = cls_lead(cw);
+    const int n = cls_n(cw);
     bool brk = false, ok = false, foreign = false;
     if (lead) {
-      const int sc = S.sn[x];
+      const int sc = cls_sn(cw);
       if (sc != ss && sc != inherited) {
         if (sc == common) {
           brk = true;
         } else {
-          const int sc2 = S.sn[x + n];
+          const int sc2 = cls_sn2(cw);
           brk = sc2 != common && sc2 != ss;
         }
       }
-      if ((S.lsm[w] >> lane) & 1) {
+      if ((cw >> 20) & 1) {
         if (sc == ss || sc == inherited) ok = true;
         else foreign = true;
       }
@@ -309,7 +396,7 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     const bool prev_run = ev_lt ? ((Om >> topbit(ev_lt)) & 1) : run;
     const bool endc = foreign && (brk || !prev_run);     // a letter stop of another script after a gap
     const bool sep = brk && prev_run;                    // a run ends here: its ' '
-    const bool cutc = lead && x + n > L;                 // only the last character
+    const bool cutc = cls_cut(cw);                       // only the last character
     const bool chr = lead && inrun;
     const int raw = chr ? n : (sep ? 1 : 0);
     const int pre = excl_scan(raw, lane);
@@ -320,18 +407,19 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     const int stop = stopm ? __builtin_ctzll(stopm) : 64;
     const bool act = lane <= stop;
     const bool hard_here = lane == stop && ((Hm >> lane) & 1);
-    if (act) {
-      const int o = put + pre;
-      if (chr) {
-        for (int k = 0; k < n; ++k) sb[o + k] = dv.at(x + k);
-        if (cutc) cutpos = o;
-        if (hard_here) sb[o + n] = ' ';
-      } else if (sep) {
-        sb[o] = ' ';
-      }
-    }
+    const bool out_chr = act && chr && !cutc;
+    if (out_chr && cls_nolow(cw)) bad = 1;
+    const int olen = out_chr ? cls_olen(cw) : 0;
+    grow += olen > n ? olen - n : 0;
+    const int tl = olen + ((act && (sep || hard_here)) ? 1 : 0);
+    const int opre = excl_scan(tl, lane);
+    if (out_chr)
+      for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(lw >> (8 * k));
+    if (act && (sep || hard_here)) lb[lpos + opre + olen] = ' ';
+    if (act && chr && cutc) cutx = x;
+    lpos += rdl(opre + tl, 63);
     put += wsum(act ? raw + (hard_here ? 1 : 0) : 0);
-    if (put + 64 > kMaxScriptBuffer) {
+    if (lpos + 64 > kLB || put + 64 > kMaxScriptBuffer) {
       bad = 1;
       break;
     }
@@ -344,60 +432,38 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
     if (evm) run = (Om >> topbit(evm)) & 1;
     if ((w << 6) + 64 >= L) {                                         // end of document
-      if (run) {
-        if (lane == 0) sb[put] = ' ';
+      if (run && wmax((uint32_t)(cutx + 1)) == 0) {                 // (a cut character brings its own)
+        if (lane == 0) lb[lpos] = ' ';
+        ++lpos;
         ++put;
       }
       nxt = L;
       break;
     }
   }
-  if (lane < 4) sb[put + lane] = lane < 3 ? ' ' : 0;
   next = nxt;
-  cutpos = (int)wmax((uint32_t)(cutpos + 1)) - 1;
-  gsync();
-  if (__ballot(bad != 0)) {
-    status = -1;
-    return 0;
-  }
-  // LowerScriptSpan: sb[0, put + 3) -> lb, one character per lane; each
-  // character must start and end in state 0 (checked in lower_char).
-  const int ilen = put + 3;
-  const int lim = cutpos >= 0 ? cutpos : ilen;
-  int lpos = 0, grow = 0;
-  for (int w0 = 0; w0 < lim; w0 += 64) {
-    const int p = w0 + lane;
-    uint64_t o = 0;
-    int olen = 0;
-    if (p < lim && (sb[p] & 0xC0) != 0x80) {
-      const int n = utf8_len(sb[p]);
-      if (!lower_char(T, sb + p, n, o, olen)) {
-        bad = 1;
-        olen = 0;
-      }
-      grow += olen > n ? olen - n : 0;
-    }
-    const int opre = excl_scan(olen, lane);
-    const int otot = rdl(opre + olen, 63);
-    if (lpos + otot + 64 > kLB) {
-      bad = 1;
-      break;
-    }
-    for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(o >> (8 * k));
-    lpos += otot;
-  }
-  if (cutpos >= 0) {                                                  // the cut last character
+  cutx = (int)wmax((uint32_t)(cutx + 1)) - 1;
+  if (cutx >= 0) {                               // the cut last character: lowercaser tail
     int filled = 0;
-    if (lane == 0) filled = lower_tail(T, sb + cutpos, ilen - cutpos, lb + lpos, kMaxScriptLowerBuffer - lpos);
+    if (lane == 0) {
+      uint8_t tail[12];
+      const int nc = utf8_len(dv.p[cutx]);
+      for (int k = 0; k < nc; ++k) tail[k] = (uint8_t)dv.at(cutx + k);
+      for (int k = 0; k < 4; ++k) tail[nc + k] = ' ';                 // separator + "   " (ilen stops before \0)
+      filled = lower_tail(T, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
+    }
     lpos += rdl(filled, 0);
+    for (int k = lane; k < 40; k += 64) lb[lpos + k] = 0;
+    lpos -= 3;                                                        // text_bytes = filled - 3
+  } else {
+    for (int k = lane; k < 40; k += 64) lb[lpos + k] = k < 3 ? ' ' : 0;   // "   " (lowered pads), NULs
   }
-  for (int k = lane; k < 40; k += 64) lb[lpos + k] = 0;
   // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
   // spans near the 40 KB limit that also grow; re-queue those.
-  if (ilen + wsum(grow) > kMaxScriptLowerBuffer - 8) bad = 1;
+  if (put + 3 + wsum(grow) > kMaxScriptLowerBuffer - 8) bad = 1;
   gsync();
   if (__ballot(bad != 0)) status = -1;
-  return lpos - 3;                                                    // text_bytes = filled - 3
+  return lpos;
 }
 
 // ------------------------------------------------------ predictor (squeeze/repeats)
@@ -883,6 +949,31 @@ __device__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& 
   return next;
 }
 
+// ProcessProbV2Tote (cldutil.cc:128-138) precomputed per emission: the three
+// (key, score) tote adds of a langprob, packed k1 | s1 << 8 | k2 << 16 |
+// s2 << 24 | k3 << 32 | s3 << 40 (bytes 5..7 of its kLgProbV2Tbl row).
+__device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
+  return (uint64_t)((lp >> 8) & 0xFF) | ((uint64_t)((e >> 8) & 0xFF) << 8) | ((uint64_t)((lp >> 16) & 0xFF) << 16) |
+         ((uint64_t)((e >> 16) & 0xFF) << 24) | ((uint64_t)(lp >> 24) << 32) | ((uint64_t)(e >> 24) << 40);
+}
+
+// Per-key language, close set and expected score for a span script
+// (FromPerScriptNumber, close sets, kAvgDeltaOctaScore: lang_script.cc:328-341,
+// 261-310; scoreonescriptspan.cc:75-80), so a chunk summary reads only LDS.
+__device__ void key_table(const DevTables& T, Smem& s, int ulscript, int lane) {
+  if (s.kscript == ulscript) return;
+  const int ls4 = lscript4(T, ulscript);
+  for (int k = lane; k < 256; k += 64) {
+    const int lang = from_per_script_number(T, ulscript, (uint8_t)k);
+    const int esub = lang * 4 + ls4;
+    s.kl[k] = (uint32_t)(uint16_t)lang | ((uint32_t)close_set(T, lang) << 16);
+    s.ke[k] = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : (int16_t)0;
+  }
+  if (lane == 0) s.kscript = ulscript;
+  wsync();
+}
+
 // ------------------------------------- linearize + chunk + score (one round)
 // LinearizeAll / ChunkAll / ScoreAllHits (scoreonescriptspan.cc:856-1031,
 // 208-302) without materialising linear[].  Linear order = the seed (offset
@@ -933,11 +1024,11 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     eb = rdl(o + c, 63);
     if (l1) {
       S.be_off[o] = (uint16_t)off;
-      S.be_lp[o] = l1;
+      S.be_add[o] = tote_adds(T, l1);
     }
     if (l2) {
       S.be_off[o + 1] = (uint16_t)off;
-      S.be_lp[o + 1] = l2;
+      S.be_add[o + 1] = tote_adds(T, l2);
     }
   }
   // delta / distinct emissions, compacted in place (ind -> langprob)
@@ -950,7 +1041,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     ed = rdl(o + (lp != 0), 63);
     if (lp) {
       S.d_off[o] = off;
-      S.d_ind[o] = lp;
+      S.d_add[o] = tote_adds(T, lp);
     }
   }
   for (int j0 = 0; j0 < nx; j0 += 64) {
@@ -961,7 +1052,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     ex = rdl(o + (lp != 0), 63);
     if (lp) {
       S.x_off[o] = off;
-      S.x_ind[o] = lp;
+      S.x_add[o] = tote_adds(T, lp);
     }
   }
   // chunk plan from the base-hit count (ChunkAll :978-1031)
@@ -1040,7 +1131,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     s.lo[k] = m;
   }
   wsync();
-  const uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
+  const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   for (int k = 0; k < K; ++k) {
     reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
@@ -1052,27 +1143,24 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     const int tot = seedn + nB + nD + nX + kMaxBoosts;
     uint64_t gm = 0;
     for (int t = lane; t < tot; t += 64) {
-      uint32_t lp;
+      uint64_t a;
       int u = t;
       if (u < seedn) {
-        lp = seed;
+        a = seed;
       } else if ((u -= seedn) < nB) {
-        lp = S.be_lp[bs + u];
+        a = S.be_add[bs + u];
       } else if ((u -= nB) < nD) {
-        lp = S.d_ind[ds + u];
+        a = S.d_add[ds + u];
       } else if ((u -= nD) < nX) {
-        lp = S.x_ind[xs + u];
+        a = S.x_add[xs + u];
       } else {                               // boosts: the last four distinct langprobs so far
         const int v = xe - kMaxBoosts + (u - nX);
-        lp = v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_ind[v];
-        if (lp == 0) continue;
+        a = v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_add[v];
       }
-      // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row
-      const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
-      const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
-      if (k1) { atomicAdd(&s.tote[k1], (e >> 8) & 0xFF); gm |= 1ull << (k1 >> 2); }
-      if (k2) { atomicAdd(&s.tote[k2], (e >> 16) & 0xFF); gm |= 1ull << (k2 >> 2); }
-      if (k3) { atomicAdd(&s.tote[k3], e >> 24); gm |= 1ull << (k3 >> 2); }
+      const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
+      if (k1) { atomicAdd(&s.tote[k1], (uint32_t)(a >> 8) & 0xFF); gm |= 1ull << (k1 >> 2); }
+      if (k2) { atomicAdd(&s.tote[k2], (uint32_t)(a >> 24) & 0xFF); gm |= 1ull << (k2 >> 2); }
+      if (k3) { atomicAdd(&s.tote[k3], (uint32_t)(a >> 40) & 0xFF); gm |= 1ull << (k3 >> 2); }
     }
     gm = wor64(gm);
     const int score_count = nB + seedn;
@@ -1104,20 +1192,19 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       const int lo = lo_k == kInf ? dummy_off : (int)lo_k;
       int hi = dummy_off;
       if (k + 1 < K && s.lo[k + 1] != kInf) hi = (int)s.lo[k + 1];
-      const int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
-      const int lang2 = from_per_script_number(T, ulscript, (uint8_t)key3[1]);
+      const uint32_t i1 = s.kl[(uint8_t)key3[0]], i2 = s.kl[(uint8_t)key3[1]];
+      const int lang1 = (int)(i1 & 0xFFFF), lang2 = (int)(i2 & 0xFFFF);
       const int len = hi - lo;
       const int sc1 = key3[0] >= 0 ? (int)sc3[0] : 0;
       const int sc2 = key3[1] >= 0 ? (int)sc3[1] : 0;
       int actual = 0;
       if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
-      const int esub = lang1 * 4 + lscript4(T, ulscript);
-      const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+      const int expected = s.ke[(uint8_t)key3[0]];
       const uint16_t bytes = (uint16_t)len, grams = (uint16_t)score_count;
       const uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
       int rd = (uint8_t)reliability_delta(s1, s2, grams);
-      const int cs1 = close_set(T, lang1);
-      if (cs1 != 0 && cs1 == close_set(T, lang2)) rd = 100;
+      const int cs1 = (int)(i1 >> 16);
+      if (cs1 != 0 && cs1 == (int)(i2 >> 16)) rd = 100;
       const int rsc = (uint8_t)reliability_expected(actual, expected);
       if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
       if (D && s.dbg) {
@@ -1134,10 +1221,10 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   }
   // the ring keeps the last four distinct langprobs
   if (lane == 0) {
-    uint32_t r4[4];
+    uint64_t r4[4];
     for (int i = 0; i < 4; ++i) {
       const int u = ex - kMaxBoosts + i;
-      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : S.x_ind[u];
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : S.x_add[u];
     }
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
@@ -1174,6 +1261,7 @@ __device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* 
     return true;
   }
   if (tb <= 1) return true;
+  key_table(T, s, ulscript, lane);
   int off = 1;
   long long t = (D && s.prof) ? (long long)clock64() : 0;
   if (rt == RTypeCJK) {
@@ -1250,7 +1338,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
     for (;;) {
       int ul = 0, st = 0;
       if constexpr (D) trace(tr, lane, doc, 3, next);
-      int tb = next_span(T, dv, S, S.lb[0], S.lb[1], next, ul, st, lane);
+      int tb = next_span(T, dv, S, S.lb[0], next, ul, st, lane);
       if constexpr (D) trace(tr, lane, doc, 4, tb);
       if constexpr (D) mark(s, lane, 1, t);
       if (st == 0) break;

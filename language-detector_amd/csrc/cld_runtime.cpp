@@ -258,6 +258,13 @@ int init_device(Device* d) {
   HIP_OK(hipMalloc(&d->d_blob, g_tab.blob.size()));
   HIP_OK(hipMemcpy(d->d_blob, g_tab.blob.data(), g_tab.blob.size(), hipMemcpyHostToDevice));
   d->T = device_tables(g_tab.offs, d->d_blob);
+  {  // per-character property table for the long-document kernel, built from the uploaded machines
+    uint64_t* cpt = nullptr;
+    HIP_OK(hipMalloc(&cpt, cld_cpt_entries() * sizeof(uint64_t)));
+    HIP_OK(cld_build_cpt(&d->T, cpt, d->stream));
+    HIP_OK(hipStreamSynchronize(d->stream));
+    d->T.cpt = cpt;
+  }
   HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->id));
@@ -548,7 +555,7 @@ void cld_shutdown(void) {
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
-    (void)hipFree(d->d_blob); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
+    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
