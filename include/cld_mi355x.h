@@ -39,6 +39,20 @@ typedef struct cld_result {
 #define CLD_ENOMEM (-12)
 #define CLD_EIO (-5)
 
+/* cld_detect_batch flags: the service's text preparation, applied on the GPU
+ * before detection (handlers.go:150-151).
+ *   CLD_FLAG_STRIP_EXTRAS  StripExtras (handlers.go:198-210): keep the
+ *                          strings.Fields words (unicode.IsSpace separators)
+ *                          that start with neither "@" nor "http", each
+ *                          followed by one ' '.
+ *   CLD_FLAG_CSTRING       cut each document at its first NUL byte, as the
+ *                          cgo hand-off does (main.go:77-81: C.CString, then
+ *                          strlen in wrapper.cc:8).
+ * STRIP_EXTRAS | CSTRING = exactly the text Detect_language() sees for one
+ * request item of POST / (handlers.go:150-151). */
+#define CLD_FLAG_STRIP_EXTRAS 1u
+#define CLD_FLAG_CSTRING 2u
+
 /* wrapper.h:8 -- returns a static ISO code; never NULL; UNKNOWN -> "en"
  * (compact_lang_det.cc:91-93).  Input is NUL-terminated, length = strlen
  * (wrapper.cc:8).  Thread-safe; concurrent callers are coalesced into GPU
@@ -81,7 +95,8 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * CLD2::DetectLanguage(buffer, length, ...)).  `out` is caller-allocated
  * (n entries).  Host buffers; not retained after return.  Blocks until the
  * results are in `out`.  Documents are sharded across the initialised GPUs
- * by byte count.  flags must be 0 (reserved).  Thread-safe. */
+ * by byte count.  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING (above).
+ * Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
                      cld_result* out, uint32_t flags);
 
@@ -91,6 +106,19 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
  * benchmark to time the path with inputs already resident in HBM. */
 int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets,
                             size_t n, cld_result* d_out, void* stream);
+
+/* cld_detect_batch_device with text preparation flags.  buf_bytes bounds
+ * d_offsets[n] (the prepared copy is staged in a device buffer of
+ * buf_bytes + n bytes).  Asynchronous like cld_detect_batch_device. */
+int cld_detect_batch_device_ex(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,
+                               uint64_t buf_bytes, cld_result* d_out, uint32_t flags, void* stream);
+
+/* The preparation step alone, on GPU 0 (host buffers): out_buf receives the
+ * prepared documents back to back (capacity >= offsets[n]-offsets[0] + n
+ * bytes), out_offsets[0..n] their offsets.  flags: CLD_FLAG_STRIP_EXTRAS and/or
+ * CLD_FLAG_CSTRING.  Blocks until the result is on the host. */
+int cld_prepare_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, uint32_t flags,
+                      uint8_t* out_buf, uint64_t* out_offsets);
 
 /* LanguageCode / LanguageName (lang_script.cc:212-217, :205-210). */
 const char* cld_language_code(int lang);
@@ -109,6 +137,36 @@ typedef struct cld_batch_stats {
                                 state, 3 span/lowercase, 4 Squeeze restart, 5 capacity */
 } cld_batch_stats;
 int cld_last_batch_stats(int device, cld_batch_stats* st);
+
+/* ---- Run-time table loading (CLD2 dynamic data, cld2_dynamic_data.h:22-147).
+ * A "cld2_data_file00" image carries the scoring tables of ScoringTables
+ * (CJK unigram machine, kAvgDeltaOctaScore, compat/deltabi/distinctbi/quad/
+ * quad2/deltaocta/distinctocta); the other tables stay the built-in ones.
+ * Loading re-uploads the tables to every initialised GPU (after draining
+ * in-flight work) and applies to every later call.  Not to be called
+ * concurrently with detection calls (the reference's loaders are not either).
+ *
+ *   cld_load_data_from_file         replaces CLD2::loadDataFromFile
+ *                                   (compact_lang_det.h:393, impl.cc:108-121)
+ *   cld_load_data_from_raw_address  replaces CLD2::loadDataFromRawAddress
+ *                                   (compact_lang_det.h:406, impl.cc:123-136)
+ *   cld_unload_data                 replaces CLD2::unloadData (compact_lang_det.h:413);
+ *                                   here it restores the built-in tables
+ *   cld_is_data_dynamic             1 while data-file tables are in use
+ *                                   (cf. CLD2::isDataDynamic, compact_lang_det.h:426)
+ * They return CLD_OK or CLD_EINVAL (malformed file: bad marker, header or
+ * file size mismatch as in cld2_dynamic_data_loader.cc:41-146, or a block /
+ * indirect index outside the file); a failed load keeps the tables in use. */
+int cld_load_data_from_file(const char* path);
+int cld_load_data_from_raw_address(const void* raw, uint32_t length);
+int cld_unload_data(void);
+int cld_is_data_dynamic(void);
+
+/* Host-only helpers (no GPU): write the tables in use as a CLDT blob, and
+ * convert a cld2 data file over a base CLDT (NULL = the built-in one) into a
+ * CLDT file -- the form the test oracle reads. */
+int cld_export_tables(const char* out_cldt_path);
+int cld_convert_data_file(const char* cld2_data_file, const char* base_cldt, const char* out_cldt_path);
 
 /* Build / table identity string ("cld-mi355x <ver> tables=<date> ..."). */
 const char* cld_version(void);

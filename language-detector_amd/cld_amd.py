@@ -3,8 +3,9 @@
 Mirrors the reference's caller-facing interface for this path:
   detect_language(text) -> ISO code       main.go:77-81 Detect_language / wrapper.cc:7-16
   detect_batch(docs)    -> cld_result[]   one DetectLanguageSummaryV2 per document
-  strip_extras(text)                      handlers.go:198-210 StripExtras (the caller-side
-                                          preprocessing the HTTP handler applies first)
+  prepare_batch(docs, flags)              handlers.go:150-151: StripExtras (handlers.go:198-210)
+                                          + the cgo C-string cut, as a GPU kernel
+  load_data_from_file(path)               CLD2::loadDataFromFile (run-time tables)
 There is no CPU fallback: if the HIP library or a GPU is missing, calls raise.
 """
 import ctypes
@@ -16,6 +17,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CLD_MI355X_LIB") or os.path.join(HERE, "build", "libcld_mi355x.so")
 TABLES = os.path.join(HERE, "data", "cld2_mi355x.cldt")
+FLAG_STRIP_EXTRAS = 1      # include/cld_mi355x.h CLD_FLAG_STRIP_EXTRAS
+FLAG_CSTRING = 2           # include/cld_mi355x.h CLD_FLAG_CSTRING
 
 RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "i1", 3),
                          ("is_reliable", "u1"), ("text_bytes", "<i4"), ("normalized3", "<f8", 3)])
@@ -24,7 +27,10 @@ assert RESULT_DTYPE.itemsize == 40
 # Every symbol include/cld_mi355x.h declares (checked by tests/test_capi.py)
 EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cld_detect_batch",
            "cld_detect_batch_device", "cld_plan_shards", "cld_kernel_time", "cld_language_code",
-           "cld_language_name", "cld_last_batch_stats", "cld_version", "cld_stage_cycles")
+           "cld_language_name", "cld_last_batch_stats", "cld_version", "cld_stage_cycles",
+           "cld_load_data_from_file", "cld_load_data_from_raw_address", "cld_unload_data",
+           "cld_is_data_dynamic", "cld_export_tables", "cld_convert_data_file",
+           "cld_detect_batch_device_ex", "cld_prepare_batch")
 
 
 class BatchStats(ctypes.Structure):
@@ -66,8 +72,55 @@ def lib():
         L.cld_plan_shards.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.cld_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+        L.cld_prepare_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        L.cld_detect_batch_device_ex.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.cld_load_data_from_file.argtypes = [ctypes.c_char_p]
+        L.cld_load_data_from_raw_address.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.cld_export_tables.argtypes = [ctypes.c_char_p]
+        L.cld_convert_data_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         _lib = L
     return _lib
+
+
+def load_data_from_file(path):
+    """CLD2::loadDataFromFile (compact_lang_det.h:393): scoring tables from a cld2_data_file00."""
+    rc = lib().cld_load_data_from_file(path.encode())
+    if rc != 0:
+        raise CldError("cld_load_data_from_file(%s) failed: %d" % (path, rc))
+
+
+def load_data_from_raw_address(data):
+    """CLD2::loadDataFromRawAddress (compact_lang_det.h:406) over a bytes-like image."""
+    b = bytes(data)
+    rc = lib().cld_load_data_from_raw_address(ctypes.c_char_p(b), len(b))
+    if rc != 0:
+        raise CldError("cld_load_data_from_raw_address failed: %d" % rc)
+
+
+def unload_data():
+    rc = lib().cld_unload_data()
+    if rc != 0:
+        raise CldError("cld_unload_data failed: %d" % rc)
+
+
+def is_data_dynamic():
+    return bool(lib().cld_is_data_dynamic())
+
+
+def export_tables(path):
+    rc = lib().cld_export_tables(path.encode())
+    if rc != 0:
+        raise CldError("cld_export_tables failed: %d" % rc)
+
+
+def convert_data_file(data_file, out_cldt, base_cldt=None):
+    """cld2_data_file00 + base CLDT -> CLDT file (host only, no GPU)."""
+    rc = lib().cld_convert_data_file(data_file.encode(), base_cldt.encode() if base_cldt else None,
+                                     out_cldt.encode())
+    if rc != 0:
+        raise CldError("cld_convert_data_file(%s) failed: %d" % (data_file, rc))
 
 
 def init(tables=None, n_devices=0):
@@ -120,7 +173,9 @@ def pack(docs):
     return buf, offs
 
 
-def detect_batch(docs=None, buf=None, offsets=None):
+def detect_batch(docs=None, buf=None, offsets=None, flags=0):
+    """One DetectLanguageSummaryV2 per document; flags = FLAG_STRIP_EXTRAS | FLAG_CSTRING
+    prepares each text as POST / does before detecting (handlers.go:150-151)."""
     if docs is not None:
         buf, offsets = pack(docs)
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -130,7 +185,7 @@ def detect_batch(docs=None, buf=None, offsets=None):
     if n == 0:
         return out
     bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
-    rc = lib().cld_detect_batch(bptr, offsets.ctypes.data, n, out.ctypes.data, 0)
+    rc = lib().cld_detect_batch(bptr, offsets.ctypes.data, n, out.ctypes.data, flags)
     if rc != 0:
         raise CldError("cld_detect_batch failed: %d" % rc)
     return out
@@ -160,16 +215,40 @@ def language_code(lang):
     return lib().cld_language_code(int(lang)).decode()
 
 
+ENGLISH, UNKNOWN_LANGUAGE = 0, 26     # generated_language.h Language enum values
+
+
+def result_code(r):
+    """compact_lang_det.cc:91-93 + wrapper.cc:14: the ISO code detect_language() returns
+    for a cld_result (UNKNOWN -> ENGLISH)."""
+    lang = int(r["summary_lang"])
+    return language_code(ENGLISH if lang == UNKNOWN_LANGUAGE else lang)
+
+
 def language_name(lang):
     return lib().cld_language_name(int(lang)).decode()
 
 
+def prepare_batch(docs=None, buf=None, offsets=None, flags=FLAG_STRIP_EXTRAS | FLAG_CSTRING):
+    """handlers.go:150-151 text preparation on the GPU (cld_prepare_batch):
+    StripExtras (handlers.go:198-210) and/or the cgo C-string cut.  -> (buf, offsets)."""
+    if docs is not None:
+        buf, offsets = pack(docs)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(int(offsets[-1] - offsets[0]) + n + 1, dtype=np.uint8)
+    oo = np.zeros(n + 1, dtype=np.uint64)
+    bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+    rc = lib().cld_prepare_batch(bptr, offsets.ctypes.data, n, flags, out.ctypes.data, oo.ctypes.data)
+    if rc != 0:
+        raise CldError("cld_prepare_batch failed: %d" % rc)
+    return out[:int(oo[-1])], oo
+
+
 def strip_extras(text):
-    """handlers.go:198-210: drop words starting with '@' or 'http', rejoin with
-    a trailing space after every kept word (strings.Fields semantics)."""
-    out = []
-    for w in text.split():
-        if w.startswith("@") or w.startswith("http"):
-            continue
-        out.append(w + " ")
-    return "".join(out)
+    """handlers.go:198-210 StripExtras for one text (GPU kernel, no C-string cut)."""
+    b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+    out, oo = prepare_batch([b], flags=FLAG_STRIP_EXTRAS)
+    r = bytes(out[:int(oo[1])])
+    return r.decode("utf-8", "surrogateescape") if isinstance(text, str) else r

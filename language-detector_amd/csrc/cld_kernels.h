@@ -44,6 +44,11 @@ size_t cld_long_slot_bytes();
 size_t cld_cpt_entries();
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);
 int cld_long_waves_per_simd();
+size_t cld_strip_scratch_bytes(int n);
+hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,
+                                    uint64_t* out_offs, void* scratch, hipStream_t s);
+hipError_t cld_launch_strip_write(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,
+                                  const uint64_t* out_offs, uint8_t* out, hipStream_t s);
 hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,

@@ -67,8 +67,11 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
 }
 
 // One wavefront per document of <= CAP bytes, WPB documents per workgroup.
+#ifndef WAVE_WPS
+#define WAVE_WPS 6
+#endif
 template <int CAP, int WPB>
-__global__ __launch_bounds__(64 * WPB, 6) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
                                                    const uint64_t* __restrict__ offs, int n,
                                                    cld_result* __restrict__ out,
                                                    uint32_t* __restrict__ requeue_list,

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "cld_device.h"
+#include "cld_dynamic_data.h"
 #include "cld_kernels.h"
 #include "cldt_format.h"
 
@@ -106,18 +107,27 @@ std::vector<std::string> strings(const std::vector<uint8_t>& b, uint32_t id) {
   return out;
 }
 
-int load_tables(const char* path, HostTables* t) {
+int read_file(const char* path, std::vector<uint8_t>* out) {
   FILE* f = fopen(path, "rb");
-  if (!f) { fprintf(stderr, "cld_mi355x: cannot open tables %s\n", path); return CLD_EINVAL; }
+  if (!f) return CLD_EINVAL;
   fseek(f, 0, SEEK_END);
   long n = ftell(f);
   fseek(f, 0, SEEK_SET);
-  t->blob.resize((size_t)n);
-  size_t got = fread(t->blob.data(), 1, (size_t)n, f);
+  if (n < 0) { fclose(f); return CLD_EIO; }
+  out->resize((size_t)n);
+  size_t got = fread(out->data(), 1, (size_t)n, f);
   fclose(f);
-  if (got != (size_t)n || n < (long)sizeof(cldt_file_header)) return CLD_EINVAL;
+  return got == (size_t)n ? CLD_OK : CLD_EIO;
+}
+
+// Parse a CLDT blob (already in t->blob) into table offsets; `label` names it in cld_version().
+int parse_tables(HostTables* t, const std::string& label) {
+  const long n = (long)t->blob.size();
+  if (n < (long)sizeof(cldt_file_header)) return CLD_EINVAL;
   const cldt_file_header* fh = (const cldt_file_header*)t->blob.data();
-  if (fh->magic != CLDT_MAGIC || fh->version != CLDT_VERSION) return CLD_EINVAL;
+  if (fh->magic != CLDT_MAGIC || fh->version != CLDT_VERSION ||
+      fh->section_table_offset + (uint64_t)fh->n_sections * sizeof(cldt_section) > (uint64_t)n)
+    return CLD_EINVAL;
   const uint8_t* m = section(t->blob, CLDT_META, nullptr, nullptr);
   if (!m) return CLD_EINVAL;
   memcpy(&t->meta, m, sizeof(t->meta));
@@ -164,8 +174,14 @@ int load_tables(const char* path, HostTables* t) {
   t->codes = strings(t->blob, CLDT_LANG_CODES);
   t->names = strings(t->blob, CLDT_LANG_NAMES);
   const cldt_table_header* q = (const cldt_table_header*)section(t->blob, CLDT_QUAD, nullptr, nullptr);
-  t->version = "cld-mi355x 1.0 tables=" + std::string(path) + " quad_build=" + std::to_string(q->build_date);
+  t->version = "cld-mi355x 1.0 tables=" + label + " quad_build=" + std::to_string(q->build_date);
   return CLD_OK;
+}
+
+int load_tables(const char* path, HostTables* t) {
+  int rc = read_file(path, &t->blob);
+  if (rc) { fprintf(stderr, "cld_mi355x: cannot read tables %s\n", path); return CLD_EINVAL; }
+  return parse_tables(t, path);
 }
 
 template <class P>
@@ -215,6 +231,9 @@ struct Device {
   uint8_t* d_buf = nullptr; size_t buf_cap = 0;
   uint64_t* d_offs = nullptr; size_t offs_cap = 0;
   cld_result* d_out = nullptr; size_t out_cap = 0;
+  uint8_t* d_sbuf = nullptr; size_t sbuf_cap = 0;        // prepared text (CLD_FLAG_STRIP_EXTRAS / CSTRING)
+  uint64_t* d_soffs = nullptr; size_t soffs_cap = 0;
+  uint8_t* d_sscr = nullptr; size_t sscr_cap = 0;
   hipEvent_t ev[4]{};
   std::vector<std::array<hipEvent_t, 4>> ev_pool;   // one set per enqueue since reset
   size_t ev_used = 0;
@@ -229,6 +248,8 @@ bool g_inited = false;
 int g_init_rc = CLD_ENODEV;
 HostTables g_tab;
 std::vector<Device*> g_devs;
+bool g_dynamic = false;       // g_tab came from a cld2 dynamic data file (cld_load_data_*)
+std::string g_base_path;      // the CLDT the static tables were read from
 
 std::string default_tables_path() {
   if (const char* e = getenv("CLD_MI355X_TABLES")) return e;
@@ -252,19 +273,32 @@ int grow(T** p, size_t* cap, size_t need) {
   return CLD_OK;
 }
 
+// Table blob -> HBM (once per GPU, and again when dynamic data replaces the tables).
+// The caller holds d->mu or owns d exclusively; the stream is drained first.
+int upload_tables(Device* d, const HostTables& t) {
+  HIP_OK(hipSetDevice(d->id));
+  HIP_OK(hipDeviceSynchronize());   // batches enqueued on caller streams may still read the old blob
+  uint8_t* blob = nullptr;
+  uint64_t* cpt = nullptr;
+  HIP_OK(hipMalloc(&blob, t.blob.size()));
+  HIP_OK(hipMemcpy(blob, t.blob.data(), t.blob.size(), hipMemcpyHostToDevice));
+  DevTables T = device_tables(t.offs, blob);
+  // per-character property table for the long-document kernel, built from the uploaded machines
+  HIP_OK(hipMalloc(&cpt, cld_cpt_entries() * sizeof(uint64_t)));
+  HIP_OK(cld_build_cpt(&T, cpt, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  T.cpt = cpt;
+  if (d->d_blob) (void)hipFree(d->d_blob);
+  if (d->T.cpt) (void)hipFree((void*)d->T.cpt);
+  d->d_blob = blob;
+  d->T = T;
+  return CLD_OK;
+}
+
 int init_device(Device* d) {
   HIP_OK(hipSetDevice(d->id));
   HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-  HIP_OK(hipMalloc(&d->d_blob, g_tab.blob.size()));
-  HIP_OK(hipMemcpy(d->d_blob, g_tab.blob.data(), g_tab.blob.size(), hipMemcpyHostToDevice));
-  d->T = device_tables(g_tab.offs, d->d_blob);
-  {  // per-character property table for the long-document kernel, built from the uploaded machines
-    uint64_t* cpt = nullptr;
-    HIP_OK(hipMalloc(&cpt, cld_cpt_entries() * sizeof(uint64_t)));
-    HIP_OK(cld_build_cpt(&d->T, cpt, d->stream));
-    HIP_OK(hipStreamSynchronize(d->stream));
-    d->T.cpt = cpt;
-  }
+  if (int rc = upload_tables(d, g_tab)) return rc;
   HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->id));
@@ -306,6 +340,20 @@ int init_device(Device* d) {
       if (const char* t = getenv("CLD_TRACE_TIMEOUT")) d->trace_timeout = atof(t);
     }
   }
+  return CLD_OK;
+}
+
+constexpr uint32_t kPrepFlags = CLD_FLAG_STRIP_EXTRAS | CLD_FLAG_CSTRING;
+
+// Text preparation (handlers.go:150-151) on device d: documents [buf, offs) ->
+// prepared documents in d->d_sbuf / d->d_soffs.  cap_bytes bounds offs[n].
+int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, uint64_t cap_bytes,
+                    uint32_t flags, hipStream_t s) {
+  if (grow(&d->d_sbuf, &d->sbuf_cap, std::max<size_t>(cap_bytes + n, 1))) return CLD_ENOMEM;
+  if (grow(&d->d_soffs, &d->soffs_cap, n + 1)) return CLD_ENOMEM;
+  if (grow(&d->d_sscr, &d->sscr_cap, cld_strip_scratch_bytes((int)n))) return CLD_ENOMEM;
+  HIP_OK(cld_launch_strip_offsets(buf, offs, (int)n, flags & kPrepFlags, d->d_soffs, d->d_sscr, s));
+  HIP_OK(cld_launch_strip_write(buf, offs, (int)n, flags & kPrepFlags, d->d_soffs, d->d_sbuf, s));
   return CLD_OK;
 }
 
@@ -375,7 +423,7 @@ int collect_stats(Device* d) {
 }
 
 // Host batch on one device: H2D, kernels, D2H.
-int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out) {
+int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
@@ -387,7 +435,13 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   for (size_t i = 0; i <= n; ++i) rel[i] = offs[i] - base;
   if (bytes) HIP_OK(hipMemcpyAsync(d->d_buf, buf + base, bytes, hipMemcpyHostToDevice, d->stream));
   HIP_OK(hipMemcpyAsync(d->d_offs, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
-  int rc = enqueue(d, d->d_buf, d->d_offs, n, d->d_out, d->stream);
+  int rc;
+  if (flags & kPrepFlags) {
+    if ((rc = enqueue_prepare(d, d->d_buf, d->d_offs, n, bytes, flags, d->stream))) return rc;
+    rc = enqueue(d, d->d_sbuf, d->d_soffs, n, d->d_out, d->stream);
+  } else {
+    rc = enqueue(d, d->d_buf, d->d_offs, n, d->d_out, d->stream);
+  }
   if (rc) return rc;
   if (d->h_trace) {           // debug: a batch that overruns dumps where every k_long wave is
                               // (polled before the D2H copy: a pageable copy blocks the host)
@@ -448,6 +502,42 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
 }
 
 // ------------------------------------------------ detect_language batching
+// Host copy of the tables: the CLDT at `tables_path` (or the default), unless
+// a cld2 dynamic data file was loaded first (cld_load_data_*).  Caller holds g_init_mu.
+int host_tables(const char* tables_path) {
+  if (!g_tab.blob.empty()) return CLD_OK;
+  g_base_path = tables_path ? tables_path : default_tables_path();
+  int rc = load_tables(g_base_path.c_str(), &g_tab);
+  if (rc) g_tab = HostTables();
+  return rc;
+}
+
+// Replace the scoring tables by a cld2 dynamic data image (compact_lang_det_impl.cc:108-136:
+// loadDataFromFile / loadDataFromRawAddress).  Unlike the reference, a failed
+// load keeps the tables in use and returns an error instead of leaving none.
+int load_dynamic(const uint8_t* data, size_t len, const std::string& label) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  int rc = host_tables(nullptr);
+  if (rc) return rc;
+  HostTables nt;
+  std::string err;
+  if (cld::cld2_data_to_cldt(data, len, g_tab.blob.data(), g_tab.blob.size(), &nt.blob, &err) != 0) {
+    fprintf(stderr, "WARNING: Dynamic data loading failed. (%s)\n", err.c_str());
+    return CLD_EINVAL;
+  }
+  if ((rc = parse_tables(&nt, label)) != CLD_OK) {
+    fprintf(stderr, "WARNING: Dynamic data loading failed. (tables rejected)\n");
+    return rc;
+  }
+  for (Device* d : g_devs) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    if ((rc = upload_tables(d, nt)) != CLD_OK) return rc;
+  }
+  g_tab = std::move(nt);
+  g_dynamic = true;
+  return CLD_OK;
+}
+
 struct Pending {
   const char* text;
   size_t len;
@@ -467,8 +557,7 @@ int cld_init(const char* tables_path, int n_devices) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   if (g_inited) return g_init_rc;
   g_inited = true;
-  std::string path = tables_path ? tables_path : default_tables_path();
-  int rc = load_tables(path.c_str(), &g_tab);
+  int rc = host_tables(tables_path);
   if (rc) return g_init_rc = rc;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -490,8 +579,7 @@ int cld_init_device(const char* tables_path, int device) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   if (g_inited) return g_init_rc;
   g_inited = true;
-  std::string path = tables_path ? tables_path : default_tables_path();
-  int rc = load_tables(path.c_str(), &g_tab);
+  int rc = host_tables(tables_path);
   if (rc) return g_init_rc = rc;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return g_init_rc = CLD_ENODEV;
@@ -557,17 +645,20 @@ void cld_shutdown(void) {
     (void)hipStreamSynchronize(d->stream);
     (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
+    (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
     delete d;
   }
   g_devs.clear();
+  g_tab = HostTables();
+  g_dynamic = false;
   g_inited = false;
   g_init_rc = CLD_ENODEV;
 }
 
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_result* out, uint32_t flags) {
-  if (flags != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
+  if ((flags & ~kPrepFlags) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
   if (n > 0x7FFFFFFFu) return CLD_EINVAL;
   for (size_t i = 0; i < n; ++i)
@@ -578,12 +669,12 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   // Shard by byte count (+ a per-document weight) at document boundaries.
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
-  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out);
+  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, flags);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
-    th.emplace_back([&, k] { rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k]); });
+    th.emplace_back([&, k] { rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], flags); });
   }
   for (auto& t : th) t.join();
   for (int r : rcs) if (r) return r;
@@ -602,6 +693,49 @@ int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   if (d->ev_used >= 4096) d->ev_used = 0;     // bounded when callers never read timings
   return enqueue(d, d_buf, d_offsets, n, d_out, s);
+}
+
+int cld_detect_batch_device_ex(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,
+                               uint64_t buf_bytes, cld_result* d_out, uint32_t flags, void* stream) {
+  if ((flags & ~kPrepFlags) != 0) return CLD_EINVAL;
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  if (device < 0 || device >= (int)g_devs.size() || n > 0x7FFFFFFFu) return CLD_EINVAL;
+  if (n == 0) return CLD_OK;
+  Device* d = g_devs[device];
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  if (d->ev_used >= 4096) d->ev_used = 0;
+  if (!(flags & kPrepFlags)) return enqueue(d, d_buf, d_offsets, n, d_out, s);
+  if ((rc = enqueue_prepare(d, d_buf, d_offsets, n, buf_bytes, flags, s))) return rc;
+  return enqueue(d, d->d_sbuf, d->d_soffs, n, d_out, s);
+}
+
+int cld_prepare_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, uint32_t flags,
+                      uint8_t* out_buf, uint64_t* out_offsets) {
+  if ((flags & ~kPrepFlags) != 0 || !offsets || !out_offsets || (n > 0 && (!buf || !out_buf))) return CLD_EINVAL;
+  if (n > 0x7FFFFFFFu) return CLD_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return CLD_EINVAL;
+  if (n == 0) { out_offsets[0] = 0; return CLD_OK; }
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  Device* d = g_devs[0];
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  const uint64_t base = offsets[0], bytes = offsets[n] - offsets[0];
+  if (grow(&d->d_buf, &d->buf_cap, std::max<size_t>(bytes, 1))) return CLD_ENOMEM;
+  if (grow(&d->d_offs, &d->offs_cap, n + 1)) return CLD_ENOMEM;
+  std::vector<uint64_t> rel(n + 1);
+  for (size_t i = 0; i <= n; ++i) rel[i] = offsets[i] - base;
+  if (bytes) HIP_OK(hipMemcpyAsync(d->d_buf, buf + base, bytes, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(d->d_offs, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
+  if ((rc = enqueue_prepare(d, d->d_buf, d->d_offs, n, bytes, flags, d->stream))) return rc;
+  HIP_OK(hipMemcpyAsync(out_offsets, d->d_soffs, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  if (out_offsets[n]) HIP_OK(hipMemcpy(out_buf, d->d_sbuf, out_offsets[n], hipMemcpyDeviceToHost));
+  return CLD_OK;
 }
 
 int cld_last_batch_stats(int device, cld_batch_stats* st) {
@@ -629,6 +763,70 @@ const char* cld_language_name(int lang) {
 const char* cld_version(void) {
   cld_init(nullptr, 0);
   return g_tab.version.c_str();
+}
+
+int cld_load_data_from_file(const char* path) {
+  std::vector<uint8_t> data;
+  if (!path || read_file(path, &data) != CLD_OK) {
+    fprintf(stderr, "WARNING: Dynamic data loading failed. (cannot read %s)\n", path ? path : "(null)");
+    return CLD_EINVAL;
+  }
+  return load_dynamic(data.data(), data.size(), std::string("cld2-data-file:") + path);
+}
+
+int cld_load_data_from_raw_address(const void* raw, uint32_t length) {
+  if (!raw) return CLD_EINVAL;
+  return load_dynamic((const uint8_t*)raw, length, "cld2-data-raw");
+}
+
+int cld_unload_data(void) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (!g_dynamic) return CLD_OK;
+  HostTables nt;
+  int rc = load_tables(g_base_path.c_str(), &nt);
+  if (rc) return rc;
+  for (Device* d : g_devs) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    if ((rc = upload_tables(d, nt)) != CLD_OK) return rc;
+  }
+  g_tab = std::move(nt);
+  g_dynamic = false;
+  return CLD_OK;
+}
+
+int cld_is_data_dynamic(void) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  return g_dynamic ? 1 : 0;
+}
+
+int cld_export_tables(const char* out_path) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  int rc = host_tables(nullptr);
+  if (rc) return rc;
+  FILE* f = out_path ? fopen(out_path, "wb") : nullptr;
+  if (!f) return CLD_EINVAL;
+  size_t w = fwrite(g_tab.blob.data(), 1, g_tab.blob.size(), f);
+  return (fclose(f) == 0 && w == g_tab.blob.size()) ? CLD_OK : CLD_EIO;
+}
+
+int cld_convert_data_file(const char* data_file, const char* base_cldt, const char* out_cldt) {
+  std::vector<uint8_t> data, base, out;
+  if (!data_file || !out_cldt) return CLD_EINVAL;
+  if (read_file(data_file, &data) != CLD_OK) return CLD_EINVAL;
+  const std::string bp = base_cldt ? base_cldt : default_tables_path();
+  if (read_file(bp.c_str(), &base) != CLD_OK) return CLD_EINVAL;
+  std::string err;
+  if (cld::cld2_data_to_cldt(data.data(), data.size(), base.data(), base.size(), &out, &err) != 0) {
+    fprintf(stderr, "cld_mi355x: %s: %s\n", data_file, err.c_str());
+    return CLD_EINVAL;
+  }
+  HostTables check;   // the result must be a blob the runtime accepts
+  check.blob = out;
+  if (parse_tables(&check, out_cldt) != CLD_OK) return CLD_EINVAL;
+  FILE* f = fopen(out_cldt, "wb");
+  if (!f) return CLD_EINVAL;
+  size_t w = fwrite(out.data(), 1, out.size(), f);
+  return (fclose(f) == 0 && w == out.size()) ? CLD_OK : CLD_EIO;
 }
 
 // wrapper.cc:7-16.  Concurrent callers are coalesced: the first caller to

@@ -1714,3 +1714,86 @@ int cldo_lower(const char* in, int len, char* out, int olen) {
   return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen);
 }
 int cldo_script_num(const char* s) { return script_num((const uint8_t*)s); }
+
+/* ------------------------------------------------ service text preparation
+ * handlers.go:150-151: textStr = StripExtras(textStr); Detect_language(textStr)
+ *   StripExtras  handlers.go:198-210 -- for each word of strings.Fields(text)
+ *                not HasPrefix "@" / "http": result += word + " "
+ *   Detect_language main.go:77-81 -- C.CString + strlen (wrapper.cc:8): the
+ *                text ends at its first NUL.
+ * strings.Fields (Go 1.x strings.go) splits on unicode.IsSpace runes while
+ * ranging over the string rune by rune; the rune decoder is Go's
+ * utf8.DecodeRuneInString: an invalid or truncated sequence yields U+FFFD with
+ * width 1.  Restated sequentially, rune by rune (the HIP kernel uses a
+ * byte-parallel formulation; this is its independent check). */
+static int go_decode_rune(const uint8_t* s, int64_t n, int64_t i, uint32_t* r) {
+  const uint32_t b0 = s[i];
+  if (b0 < 0x80) { *r = b0; return 1; }
+  int w = 0;
+  uint32_t lo = 0x80, hi = 0xBF;
+  if (b0 >= 0xC2 && b0 <= 0xDF) w = 2;
+  else if (b0 == 0xE0) { w = 3; lo = 0xA0; }
+  else if (b0 >= 0xE1 && b0 <= 0xEC) w = 3;
+  else if (b0 == 0xED) { w = 3; hi = 0x9F; }
+  else if (b0 >= 0xEE && b0 <= 0xEF) w = 3;
+  else if (b0 == 0xF0) { w = 4; lo = 0x90; }
+  else if (b0 >= 0xF1 && b0 <= 0xF3) w = 4;
+  else if (b0 == 0xF4) { w = 4; hi = 0x8F; }
+  if (w == 0 || i + w > n) { *r = 0xFFFD; return 1; }
+  const uint32_t b1 = s[i + 1];
+  if (b1 < lo || b1 > hi) { *r = 0xFFFD; return 1; }
+  for (int k = 2; k < w; ++k)
+    if (s[i + k] < 0x80 || s[i + k] > 0xBF) { *r = 0xFFFD; return 1; }
+  if (w == 2) *r = ((b0 & 0x1F) << 6) | (b1 & 0x3F);
+  else if (w == 3) *r = ((b0 & 0x0F) << 12) | ((b1 & 0x3F) << 6) | (s[i + 2] & 0x3F);
+  else *r = ((b0 & 0x07) << 18) | ((b1 & 0x3F) << 12) | ((s[i + 2] & 0x3F) << 6) | (s[i + 3] & 0x3F);
+  return w;
+}
+
+static int go_is_space(uint32_t r) {   /* unicode.IsSpace */
+  if (r <= 0xFF) return r == ' ' || (r >= '\t' && r <= '\r') || r == 0x85 || r == 0xA0;
+  return r == 0x1680 || (r >= 0x2000 && r <= 0x200A) || r == 0x2028 || r == 0x2029 || r == 0x202F ||
+         r == 0x205F || r == 0x3000;
+}
+
+/* One document -> prepared bytes in out (capacity n + 1); returns the length. */
+static int64_t prepare_one(const uint8_t* s, int64_t n, int strip, int cstr, uint8_t* out) {
+  int64_t o = 0;
+  if (!strip) {
+    memcpy(out, s, (size_t)n);
+    o = n;
+  } else {
+    int64_t i = 0;
+    while (i < n) {
+      uint32_t r;
+      int w = go_decode_rune(s, n, i, &r);
+      if (go_is_space(r)) { i += w; continue; }
+      const int64_t ws = i;                     /* a word: runes up to the next space */
+      while (i < n) {
+        w = go_decode_rune(s, n, i, &r);
+        if (go_is_space(r)) break;
+        i += w;
+      }
+      const int64_t wl = i - ws;
+      const int drop = s[ws] == '@' || (wl >= 4 && memcmp(s + ws, "http", 4) == 0);
+      if (!drop) { memcpy(out + o, s + ws, (size_t)wl); o += wl; out[o++] = ' '; }
+    }
+  }
+  if (cstr) {
+    const uint8_t* z = memchr(out, 0, (size_t)o);
+    if (z) o = z - out;
+  }
+  return o;
+}
+
+int cldo_prepare_batch(const char* buf, const uint64_t* offsets, int n, int flags, char* out,
+                       uint64_t* out_offsets) {
+  uint64_t o = 0;
+  out_offsets[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const int64_t len = (int64_t)(offsets[i + 1] - offsets[i]);
+    o += (uint64_t)prepare_one((const uint8_t*)buf + offsets[i], len, flags & 1, flags & 2, (uint8_t*)out + o);
+    out_offsets[i + 1] = o;
+  }
+  return 0;
+}

@@ -34,6 +34,10 @@ void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg);
 int cldo_detect(cldo_ctx* c, const char* text, int len, cldo_result* r);
 const char* cldo_detect_language(cldo_ctx* c, const char* text);
 int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_result* out, int threads);
+/* handlers.go:150-151 text preparation: flags 1 = StripExtras, 2 = C-string cut.
+ * out capacity: offsets[n]-offsets[0] + n bytes. */
+int cldo_prepare_batch(const char* buf, const uint64_t* offsets, int n, int flags, char* out,
+                       uint64_t* out_offsets);
 const char* cldo_language_code(int lang);
 const char* cldo_language_name(int lang);
 int cldo_meta(int which);

@@ -52,6 +52,8 @@ class Oracle:
         lib.cldo_detect_language.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         lib.cldo_detect_language.restype = ctypes.c_char_p
         lib.cldo_detect_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        lib.cldo_prepare_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]
         lib.cldo_language_code.restype = ctypes.c_char_p
         lib.cldo_language_name.restype = ctypes.c_char_p
         lib.cldo_score_linear.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -101,6 +103,18 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("cldo_detect_batch rc=%d" % rc)
         return out
+
+    def prepare_batch(self, buf, offsets, flags):
+        """handlers.go:150-151 (StripExtras = 1, C-string cut = 2) -> (buf, offsets)."""
+        buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(int(offsets[-1] - offsets[0]) + n + 1, dtype=np.uint8)
+        oo = np.zeros(n + 1, dtype=np.uint64)
+        rel = offsets - offsets[0]
+        self.lib.cldo_prepare_batch(ctypes.c_void_p(buf.ctypes.data + int(offsets[0])), rel.ctypes.data, n,
+                                    int(flags), out.ctypes.data, oo.ctypes.data)
+        return out[:int(oo[-1])], oo
 
     def score_linear(self, ulscript, score_cjk, next_base, offsets, types, langprobs, dummy_offset, ring=None):
         n = len(offsets)

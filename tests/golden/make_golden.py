@@ -193,7 +193,25 @@ def main():
     readme = "This is an example input message."
     kats.append({"text": readme, "expected": "en", "source": "README.md:19"})
     kats.append({"text": "This is a valid input test.", "expected": "en", "source": "main_test.go:124-142"})
-    json.dump({"source": "main_test.go:144-305", "kats": kats},
+    # main_test.go HTTP cases: method, path, request body, expected status and body
+    http_cases = []
+    for m in re.finditer(r'func (Test\w+)\(t \*testing\.T\) \{(.*?)\n\}', mt, re.S):
+        name, fn = m.group(1), m.group(2)
+        st = re.search(r'assert\.Equal\(t, (\d+), resp\.StatusCode', fn)
+        exp = re.search(r'expected := `([^`]*)`', fn)
+        if not st or not exp:
+            continue
+        req = re.search(r'strings\.NewReader\(`([^`]*)`\)', fn)
+        get = re.search(r'http\.Get\(serverUrl( \+ "(\w+)")?\)', fn)
+        http_cases.append({"test": name, "method": "POST" if req else "GET",
+                           "path": "/" + (get.group(2) or "" if get else ""),
+                           "body": req.group(1) if req else "", "status": int(st.group(1)),
+                           "expected": exp.group(1)})
+    # the known-language map the service answers names from (main.go:114-124, LANG_FILE)
+    known = json.load(open(os.path.join(REF, "data", "cld_codes.json"), encoding="utf-8"))
+    json.dump({"source": "main_test.go:144-305 (kats), main_test.go:52-345 (http_cases), "
+                         "data/cld_codes.json (known_languages)",
+               "kats": kats, "http_cases": http_cases, "known_languages": sorted(known.items())},
               open(os.path.join(HERE, "main_test.json"), "w"), ensure_ascii=False, indent=1)
     print("html docs", len(docs), "matched", sum(1 for d in docs if d["var"]),
           "test pairs", len(test_list), "verbose spans", len(verbose), "kats", len(kats))

@@ -33,9 +33,3 @@ def test_result_record_layout():
     assert cld_amd.RESULT_DTYPE.itemsize == 40
     assert [cld_amd.RESULT_DTYPE.fields[f][1] for f in ("lang3", "summary_lang", "percent3", "is_reliable",
                                                        "text_bytes", "normalized3")] == [0, 6, 8, 11, 12, 16]
-
-
-def test_strip_extras_matches_handler():
-    # handlers.go:198-210 and main_test.go:307-345 inputs
-    assert cld_amd.strip_extras("RT @x: @y al fin de semana") == "RT al fin de semana "
-    assert cld_amd.strip_extras("see http://a.b/c now") == "see now "
