@@ -40,6 +40,8 @@ hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               hipStream_t s);
+hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
+                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s);
 size_t cld_long_slot_bytes();
 size_t cld_cpt_entries();
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);

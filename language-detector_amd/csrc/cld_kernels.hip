@@ -153,6 +153,53 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
 }
 
+// Longest-first order for k_long's persistent grid (LPT list scheduling):
+// documents land in 1 KB length buckets, longest bucket first, so the last
+// documents a wave picks up are short ones and the grid drains evenly.  The
+// order inside a bucket is whatever the atomics give; a document's result
+// never depends on which wave scored it or when.
+constexpr int kLenBuckets = 64;
+__device__ __forceinline__ uint32_t len_bucket(uint64_t len) {
+  const uint64_t b = len >> 10;
+  return (uint32_t)(kLenBuckets - 1) - (uint32_t)(b < kLenBuckets - 1 ? b : kLenBuckets - 1);
+}
+
+__global__ __launch_bounds__(256) void k_len_hist(const uint64_t* __restrict__ offs,
+                                                 const uint32_t* __restrict__ list,
+                                                 const uint32_t* __restrict__ counters,
+                                                 uint8_t* __restrict__ key, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kLenBuckets];
+  if (threadIdx.x < kLenBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t total = counters[kCtrRequeue];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+    const uint32_t i = list[k];
+    const uint32_t b = len_bucket(offs[i + 1] - offs[i]);
+    key[k] = (uint8_t)b;
+    atomicAdd(&h[b], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kLenBuckets && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_len_scatter(const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ counters,
+                                                    const uint8_t* __restrict__ key,
+                                                    const uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
+  __shared__ uint32_t base[kLenBuckets];
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int b = 0; b < kLenBuckets; ++b) { base[b] = s; s += hist[b]; }
+  }
+  __syncthreads();
+  const uint32_t total = counters[kCtrRequeue];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+    const uint32_t b = key[k];
+    sorted[base[b] + atomicAdd(&cursor[b], 1u)] = list[k];
+  }
+}
+
 // Character property table (lng::cpt_eval over every 1-3 byte sequence).
 __global__ __launch_bounds__(256) void k_build_cpt(DevTables T, uint64_t* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -183,6 +230,16 @@ extern "C" {
 size_t cld_cpt_entries() { return cld::lng::kCptSize; }
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(cld::k_build_cpt, dim3((cld::lng::kCptSize + 255) / 256), dim3(256), 0, s, *T, out);
+  return hipGetLastError();
+}
+hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
+                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s) {
+  // hist2: 2 * kLenBuckets u32 (histogram, then scatter cursors), zeroed here
+  hipError_t e = hipMemsetAsync(hist2, 0, 2 * cld::kLenBuckets * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cld::k_len_hist, dim3(512), dim3(256), 0, s, offs, list, counters, key, hist2);
+  hipLaunchKernelGGL(cld::k_len_scatter, dim3(512), dim3(256), 0, s, list, counters, key, hist2,
+                     hist2 + cld::kLenBuckets, sorted);
   return hipGetLastError();
 }
 size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }

@@ -220,6 +220,10 @@ struct Device {
   int n_slots = 0;
   uint32_t* d_requeue2 = nullptr;
   size_t requeue2_cap = 0;
+  bool long_order = true;       // k_long takes its list longest first (CLD_LONG_ORDER=0: arrival order)
+  uint32_t* d_lsorted = nullptr; size_t lsorted_cap = 0;   // k_long list, longest first
+  uint8_t* d_lkey = nullptr; size_t lkey_cap = 0;          // length bucket per re-queued document
+  uint32_t* d_lhist = nullptr;                             // bucket histogram + scatter cursors
   uint32_t* h_trace = nullptr;  // CLD_TRACE=1: pinned host progress words, 4 per k_long wave
   uint32_t* d_dbg = nullptr;    // CLD_DEBUG_DOC=i: k_long dumps document i's rounds/chunks
   uint32_t dbg_doc = 0xFFFFFFFFu;
@@ -300,6 +304,8 @@ int init_device(Device* d) {
   HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   if (int rc = upload_tables(d, g_tab)) return rc;
   HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
+  HIP_OK(hipMalloc(&d->d_lhist, 256 * sizeof(uint32_t)));
+  if (const char* e = getenv("CLD_LONG_ORDER")) d->long_order = atoi(e) != 0;
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->id));
   d->stride = (cld_general_work_bytes() + 255) & ~(uint64_t)255;
@@ -361,6 +367,10 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s) {
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  if (d->n_slots > 0 && d->long_order) {
+    if (grow(&d->d_lsorted, &d->lsorted_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+    if (grow(&d->d_lkey, &d->lkey_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+  }
   if (d->ev_used == d->ev_pool.size()) {
     std::array<hipEvent_t, 4> t{};
     for (auto& e : t) HIP_OK(hipEventCreate(&e));
@@ -376,7 +386,12 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
-    HIP_OK(cld_launch_long(&d->T, buf, offs, d->d_requeue, out, d->d_slots, d->n_slots, d->d_requeue2,
+    const uint32_t* list = d->d_requeue;
+    if (d->long_order) {
+      HIP_OK(cld_launch_order_long(offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
+      list = d->d_lsorted;
+    }
+    HIP_OK(cld_launch_long(&d->T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, s));
     HIP_OK(hipEventRecord(ev[2], s));
@@ -644,7 +659,7 @@ void cld_shutdown(void) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
-    (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
+    (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
