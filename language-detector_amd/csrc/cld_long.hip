@@ -231,11 +231,7 @@ __device__ int scan_char(const DevTables& T, const DocView& d, int p, int n, boo
 //   bits 0-7 script, 8-9 scan class (0 continue, 1 stop, 3 non-local),
 //   10 lowerable here, 11-14 lowered length, 32-63 lowered bytes
 constexpr int kCptSize = 128 + 2048 + 65536;
-__device__ __forceinline__ int cpt_index(uint32_t b0, uint32_t b1, uint32_t b2, int n) {
-  if (n == 1) return (int)b0;
-  if (n == 2) return 128 + (int)((b0 & 0x1F) << 6 | (b1 & 0x3F));
-  return 2176 + (int)((b0 & 0x0F) << 12 | (b1 & 0x3F) << 6 | (b2 & 0x3F));
-}
+using wave::cpt_index;
 __device__ uint64_t cpt_eval(const DevTables& T, const uint8_t* b, int n) {
   const DocView dv{b, n};
   const int sn = script_num(T, dv, 0);

@@ -178,6 +178,16 @@ __device__ __forceinline__ int find_first(const uint64_t* m, int from, int L) {
   }
 }
 
+// Index of a 1-3 byte sequence in the per-character property table T.cpt
+// (built on device by k_build_cpt from lng::cpt_eval; layout in cld_long.hip):
+// bits 0-7 script, 8-9 scan class (0 continue, 1 stop, 3 non-local), 10
+// lowerable with <= 4 output bytes, 11-14 lowered length, 32-63 lowered bytes.
+__device__ __forceinline__ int cpt_index(uint32_t b0, uint32_t b1, uint32_t b2, int n) {
+  if (n == 1) return (int)b0;
+  if (n == 2) return 128 + (int)((b0 & 0x1F) << 6 | (b1 & 0x3F));
+  return 2176 + (int)((b0 & 0x0F) << 12 | (b1 & 0x3F) << 6 | (b2 & 0x3F));
+}
+
 // ------------------------------------------------------- stage 0: document
 // Loads the document, computes script numbers and scanner stops per byte
 // and checks that the per-character formulation below reproduces the
@@ -190,6 +200,45 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
   for (int p = lane; p < C::DOC; p += 64) s.doc[p] = p < L ? g[p] : (uint8_t)0;
   wsync();
   DocView dv{s.doc, L};
+  // Fast path: every character is a complete, well-formed 1-3 byte sequence
+  // whose scanner class is local (continue or stop) -- then one property-table
+  // lookup per character gives its script and whether the scan stops on it,
+  // the same per-character formulation k_long's classify() uses.  Anything
+  // else takes the state-machine path below, unchanged.
+  {
+    int slow = 0, conts = 0, need = 0;
+    for (int w = 0; w < C::NM; ++w) {
+      const int p = w * 64 + lane;
+      bool ls = false;
+      if (p < L) {
+        const uint32_t c = s.doc[p];
+        if ((c & 0xC0) == 0x80) {
+          ++conts;
+        } else {
+          const int n = utf8_len((uint8_t)c);
+          const uint32_t b1 = s.doc[p + 1], b2 = s.doc[p + 2];
+          if (n > 3 || p + n > L || (n >= 2 && (b1 & 0xC0) != 0x80) || (n == 3 && (b2 & 0xC0) != 0x80)) {
+            slow = 1;
+          } else {
+            need += n - 1;
+            const uint64_t e = T.cpt[cpt_index(c, b1, b2, n)];
+            const int st = (int)((e >> 8) & 3);
+            slow |= st == 3;
+            s.sn[p] = (uint8_t)e;
+            ls = st == 1 && (e & 0xFF) != 0;
+          }
+        }
+      }
+      const uint64_t m = __ballot(ls);
+      if (lane == 0) s.lsm[w] = m;
+    }
+    slow |= (wsum(conts) != wsum(need)) ? 1 : 0;
+    if (__ballot(slow != 0) == 0) {
+      if (lane < 4) s.sn[L + lane] = (uint8_t)script_num(T, dv, L + lane);
+      wsync();
+      return true;
+    }
+  }
   for (int p = lane; p < L + 4; p += 64) s.sn[p] = (uint8_t)script_num(T, dv, p);
   for (int p = lane; p < L; p += 64) s.a.nx[p] = (uint16_t)(p + scan_to_letter_or_special(T, dv, p, L - p));
   wsync();
@@ -379,7 +428,19 @@ __device__ int lower_span(const DevTables& T, Smem<CAP>& s, int text_bytes, int 
     uint64_t o = 0;
     int olen = 0;
     if (p < ilen && (s.u.sbuf[p] & 0xC0) != 0x80) {
-      if (!lower_char(T, &s.u.sbuf[p], utf8_len(s.u.sbuf[p]), o, olen)) { bad = 1; olen = 0; }
+      // one property-table lookup per 1-3 byte character (the table holds
+      // lower_char's result when it is <= 4 bytes); the machine otherwise
+      const int n = utf8_len(s.u.sbuf[p]);
+      const uint32_t b1 = s.u.sbuf[p + 1], b2 = s.u.sbuf[p + 2];
+      const bool wf = n <= 3 && (n < 2 || (b1 & 0xC0) == 0x80) && (n < 3 || (b2 & 0xC0) == 0x80);
+      const uint64_t e = wf ? T.cpt[cpt_index(s.u.sbuf[p], b1, b2, n)] : 0ull;
+      if ((e >> 10) & 1) {
+        olen = (int)((e >> 11) & 15);
+        o = e >> 32;
+      } else if (!lower_char(T, &s.u.sbuf[p], n, o, olen)) {
+        bad = 1;
+        olen = 0;
+      }
     }
     const int pre = excl_scan(olen, lane);
     const int tot = rdl(pre + olen, 63);
