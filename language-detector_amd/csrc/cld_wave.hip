@@ -895,6 +895,52 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   return true;
 }
 
+// DocTote::Sort(3) (tote.cc:221-250) across lanes 0-23, one lane per slot.
+// Pass s of the reference's partial bubble sort swaps slot s with every later
+// slot whose value beats the current holder (strictly): the holders are the
+// running-maximum records r1 < ... < rm of slots s+1..23.  Afterwards slot s
+// has rm's entry, r1 has s's, and rj has r(j-1)'s; nothing else moves.
+// Unused slots count as value -1 (the reference sets that as it scans).
+__device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
+  const bool in = lane < 24;
+  uint32_t key = in ? dt.key[lane] : kUnusedKey;
+  int val = in ? dt.value[lane] : -1, sc = in ? dt.score[lane] : 0, rl = in ? dt.rel[lane] : 0;
+  if (key == kUnusedKey) val = -1;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    // exclusive running max of slots p..lane-1
+    int m = (in && lane >= p) ? val : INT_MIN;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {
+      const int y = __shfl_up(m, d, 64);
+      if (lane >= d) m = m > y ? m : y;
+    }
+    int ex = __shfl_up(m, 1, 64);
+    if (lane == 0) ex = INT_MIN;
+    const uint64_t R = __ballot(in && lane > p && val > ex);
+    if (R) {
+      int src = lane;
+      if (lane == p) src = 63 - __builtin_clzll(R);
+      else if ((R >> lane) & 1) {
+        const uint64_t below = R & lanemask_lt(lane);
+        src = below ? 63 - __builtin_clzll(below) : p;
+      }
+      key = (uint32_t)__shfl((int)key, src, 64);
+      val = __shfl(val, src, 64);
+      sc = __shfl(sc, src, 64);
+      rl = __shfl(rl, src, 64);
+    }
+  }
+  if (in) {
+    dt.key[lane] = (uint16_t)key;
+    dt.value[lane] = val;
+    dt.score[lane] = sc;
+    dt.rel[lane] = rl;
+  }
+  if (lane == 0) dt.sorted = 1;
+  wsync();
+}
+
 // ------------------------------------------------------ the document
 template <int CAP>
 __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
@@ -958,28 +1004,44 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     }
     total += tb;
   }
-  // document level (compact_lang_det_impl.cc:1997-2065), lane 0
+  // document level (compact_lang_det_impl.cc:1997-2065).  Lanes 0-23 hold
+  // the DocTote slots: the partial sort runs across them, and the close-pair
+  // and unreliable-language passes run (on lane 0, as written) only when a
+  // slot they could change exists -- otherwise they are no-ops there too.
+  DocTote& dt = s.dt;
+  if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
+    if (lane == 0) refine_scored_close_pairs(T, dt);
+    wsync();
+  }
+  sort3_wave(dt, lane);
   int ok = 1;
+  Extract x;
   if (lane == 0) {
-    DocTote& dt = s.dt;
-    refine_scored_close_pairs(T, dt);
-    dt.sort3();
-    Extract x;
     extract_lang_etc(T, dt, total, x);
     const bool good = total <= 256 || (x.reliable && x.pct3[0] >= 70) || (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
-    if (!good) {
-      ok = 0;
-    } else {
-      remove_unreliable_languages(T, dt);
-      dt.sort3();
-      extract_lang_etc(T, dt, total, x);
+    if (!good) ok = 0;
+  }
+  ok = rdl(ok, 0);
+  if (ok) {
+    bool unrel = false;
+    if (lane < 24) {
+      const int bytes = dt.value[lane];
+      unrel = dt.key[lane] != kUnusedKey && bytes != 0 && dt.rel[lane] / bytes < 41;
+    }
+    if (__ballot(unrel)) {
+      if (lane == 0) remove_unreliable_languages(T, dt);
+      wsync();
+      sort3_wave(dt, lane);
+      if (lane == 0) extract_lang_etc(T, dt, total, x);
+    }
+    if (lane == 0) {
       bool rel;
       const int summary = calc_summary_lang(T, total, x, rel);
       write_result(out, x, summary, rel);
     }
   }
   mark(6);
-  return rdl(ok, 0) != 0;
+  return ok != 0;
 }
 
 }  // namespace wave

@@ -122,3 +122,45 @@ def test_detect_language_abi_concurrent(gpu, oracle, kats):
     assert got == want
     assert gpu.detect_language(" 私はガラスを食べられます。それは私を傷つけません。") == "ja"
     assert gpu.detect_language("") == "en"
+
+
+CLOSE_GROUPS = [["da", "no"], ["es", "gl"], ["cs", "sk"], ["id", "ms"], ["hr", "sr", "bs"], ["pt", "gl"],
+                ["en", "fr", "de", "it", "es"], ["ro", "it"], ["sw", "rw"], ["tl", "ceb"]]
+
+
+def mixed_short_docs(n, seed=0xC1D2_00AA):
+    """Short (<= 256 B) documents mixing words of 2-4 languages in random
+    proportions, half of them from a close set: they exercise the document
+    level -- close pairs (RefineScoredClosePairs), unreliable languages
+    (RemoveUnreliableLanguages) and the top-3 sort -- inside the wave kernel."""
+    with open(os.path.join(ROOT, "language-detector_amd", "data", "vocab.json"), encoding="utf-8") as f:
+        vocab = json.load(f)
+    latin = [l for l in vocab if l not in ("un",) and len(vocab[l]) >= 100]
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(n):
+        if rng.random() < 0.5:
+            langs = list(CLOSE_GROUPS[rng.integers(len(CLOSE_GROUPS))])
+        else:
+            langs = list(rng.choice(latin, size=rng.integers(2, 5), replace=False))
+        w = rng.dirichlet(np.ones(len(langs)) * 0.7)
+        out, size = [], 0
+        target = int(rng.integers(20, 250))
+        while True:
+            lang = langs[rng.choice(len(langs), p=w)]
+            word = vocab[lang][rng.integers(len(vocab[lang]))]
+            b = len(word.encode("utf-8")) + 1
+            if size + b > target:
+                break
+            out.append(word)
+            size += b
+        docs.append(" ".join(out))
+    return docs
+
+
+def test_mixed_language_short_documents(gpu, oracle):
+    buf, offs = gpu.pack(mixed_short_docs(40000))
+    got = check(gpu, oracle, buf, offs, "mixed-language short documents")
+    # the mixture must reach the document-level passes the wave kernel gates
+    assert (got["percent3"][:, 1] > 0).sum() > 5000
+    assert (~got["is_reliable"].astype(bool)).sum() > 1000
