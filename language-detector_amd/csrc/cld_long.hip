@@ -1357,28 +1357,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
       t = (D && s.prof) ? (long long)clock64() : 0;
       total += tb;
     }
-    int res = 1;
-    if (lane == 0) {
-      DocTote& dt = s.dt;
-      refine_scored_close_pairs(T, dt);
-      dt.sort3();
-      Extract x;
-      extract_lang_etc(T, dt, total, x);
-      const bool good = pass == 2 || total <= 256 || (x.reliable && x.pct3[0] >= 70) ||
-                        (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
-      if (!good) {
-        res = 2;
-      } else {
-        remove_unreliable_languages(T, dt);
-        dt.sort3();
-        extract_lang_etc(T, dt, total, x);
-        bool rel;
-        const int summary = calc_summary_lang(T, total, x, rel);
-        write_result(out, x, summary, rel);
-      }
-    }
-    res = rdl(res, 0);
-    wsync();
+    const int res = wave::finish_document(T, s.dt, total, pass == 2, out, lane) ? 1 : 2;
     if (res == 1) return pass;
   }
   return 0;

@@ -941,6 +941,50 @@ __device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
   wsync();
 }
 
+// Document level (compact_lang_det_impl.cc:1997-2065).  Lanes 0-23 hold the
+// DocTote slots: the partial sort runs across them, and the close-pair and
+// unreliable-language passes run (on lane 0, as written) only when a slot
+// they could change exists -- otherwise they are no-ops there too.  Returns 1
+// with the result written, or 0 when the first pass is not good enough and the
+// Repeats pass must follow (never when `final`).
+__device__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
+                               int lane) {
+  if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
+    if (lane == 0) refine_scored_close_pairs(T, dt);
+    wsync();
+  }
+  sort3_wave(dt, lane);
+  int ok = 1;
+  Extract x;
+  if (lane == 0) {
+    extract_lang_etc(T, dt, total, x);
+    const bool good = final || total <= 256 || (x.reliable && x.pct3[0] >= 70) ||
+                      (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
+    if (!good) ok = 0;
+  }
+  ok = rdl(ok, 0);
+  if (ok) {
+    bool unrel = false;
+    if (lane < 24) {
+      const int bytes = dt.value[lane];
+      unrel = dt.key[lane] != kUnusedKey && bytes != 0 && dt.rel[lane] / bytes < 41;
+    }
+    if (__ballot(unrel)) {
+      if (lane == 0) remove_unreliable_languages(T, dt);
+      wsync();
+      sort3_wave(dt, lane);
+      if (lane == 0) extract_lang_etc(T, dt, total, x);
+    }
+    if (lane == 0) {
+      bool rel;
+      const int summary = calc_summary_lang(T, total, x, rel);
+      write_result(out, x, summary, rel);
+    }
+  }
+  wsync();
+  return ok;
+}
+
 // ------------------------------------------------------ the document
 template <int CAP>
 __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
@@ -1004,42 +1048,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     }
     total += tb;
   }
-  // document level (compact_lang_det_impl.cc:1997-2065).  Lanes 0-23 hold
-  // the DocTote slots: the partial sort runs across them, and the close-pair
-  // and unreliable-language passes run (on lane 0, as written) only when a
-  // slot they could change exists -- otherwise they are no-ops there too.
-  DocTote& dt = s.dt;
-  if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
-    if (lane == 0) refine_scored_close_pairs(T, dt);
-    wsync();
-  }
-  sort3_wave(dt, lane);
-  int ok = 1;
-  Extract x;
-  if (lane == 0) {
-    extract_lang_etc(T, dt, total, x);
-    const bool good = total <= 256 || (x.reliable && x.pct3[0] >= 70) || (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
-    if (!good) ok = 0;
-  }
-  ok = rdl(ok, 0);
-  if (ok) {
-    bool unrel = false;
-    if (lane < 24) {
-      const int bytes = dt.value[lane];
-      unrel = dt.key[lane] != kUnusedKey && bytes != 0 && dt.rel[lane] / bytes < 41;
-    }
-    if (__ballot(unrel)) {
-      if (lane == 0) remove_unreliable_languages(T, dt);
-      wsync();
-      sort3_wave(dt, lane);
-      if (lane == 0) extract_lang_etc(T, dt, total, x);
-    }
-    if (lane == 0) {
-      bool rel;
-      const int summary = calc_summary_lang(T, total, x, rel);
-      write_result(out, x, summary, rel);
-    }
-  }
+  const int ok = finish_document(T, s.dt, total, false, out, lane);
   mark(6);
   return ok != 0;
 }
