@@ -43,6 +43,10 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
   return ((uint64_t)rdlu((uint32_t)(v >> 32), l) << 32) | rdlu((uint32_t)v, l);
 }
 
+__device__ __forceinline__ uint64_t rdl_shfl64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)v, l, 64);
+}
+
 // Order LDS traffic between lanes of one wavefront (no workgroup barrier:
 // the waves of a workgroup work on different documents).
 __device__ __forceinline__ void wsync() {
@@ -467,29 +471,66 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   const uint8_t* text = s.lbuf;
   int start = 1;
   if (text[start] == ' ') ++start;
-  for (int p = start + lane; p < limit; p += 64) {
-    int e = p;
-    e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-    int mid = e;
-    e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-    int nxt = (text[e] == ' ') ? e : mid;
-    if (nxt < limit) nxt += adv_space_vowel(text[nxt]);
-    else nxt = limit;
-    s.a.nxq[p] = (uint16_t)nxt;
+  // The chain never jumps over a space: it enters every word at its first
+  // byte, and a word's entries depend on that word alone (k_long's
+  // build_chain).  One lane walks one word; a prefix sum places the entries.
+  uint16_t* wst = s.a.nxq;               // word starts
+  uint16_t* chn = s.a.nxq + C::NB;       // chain entries, in order
+  int nws = 0;
+  for (int w0 = start; w0 < limit; w0 += 64) {
+    const int x = w0 + lane;
+    const bool isws = x < limit && (x == start || text[x - 1] == ' ');
+    const uint64_t m = __ballot(isws);
+    if (isws) {
+      const int k = nws + __popcll(m & lanemask_lt(lane));
+      if (k < C::NB) wst[k] = (uint16_t)x;
+    }
+    nws += __popcll(m);
+  }
+  if (nws > C::NB) return -1;
+  wsync();
+  int n = 0;
+#pragma unroll
+  for (int r = 0; r < C::NR; ++r) {
+    const int i = r * 64 + lane;
+    int cnt = 0, w = 0;
+    if (i < nws) {
+      w = wst[i];
+      int src = w;
+      for (;;) {
+        ++cnt;
+        int e = src;
+        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+        const int mid = e;
+        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+        if (text[e] == ' ' || mid >= limit) break;
+        src = mid + adv_space_vowel(text[mid]);
+        if (src >= limit) break;
+      }
+    }
+    const int pre = n + excl_scan(cnt, lane);
+    const int tot = rdl(pre + cnt, 63);
+    if (tot > C::NB) return -1;
+    if (cnt) {
+      int src = w, k = pre;
+      for (;;) {
+        chn[k++] = (uint16_t)src;
+        int e = src;
+        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+        const int mid = e;
+        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
+        if (text[e] == ' ' || mid >= limit) break;
+        src = mid + adv_space_vowel(text[mid]);
+        if (src >= limit) break;
+      }
+    }
+    n = tot;
   }
   wsync();
-  // scalar chain walk; chain entry i lives in lane i&63 of register i>>6
   int cp[C::NR];
 #pragma unroll
-  for (int r = 0; r < C::NR; ++r) cp[r] = 0;
-  int n = 0, src = start;
-  while (src < limit) {
-    if (n >= C::NB) return -1;
-    put_lane(cp, n >> 6, n & 63, src);
-    ++n;
-    src = ufl(s.a.nxq[src]);
-  }
-  const int end = src;
+  for (int r = 0; r < C::NR; ++r) cp[r] = chn[r * 64 + lane];
+  const int end = n == 0 ? start : limit;
   // hashes and probes per chain entry
   uint32_t h[C::NR], pr[C::NR];
   bool hit[C::NR];
@@ -516,22 +557,46 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
       hit[r] = probs != 0;
     }
   }
-  // scalar repeat filter: drop a hit equal to either of the last two hits
+  // repeat filter: drop a hit equal to either of the last two kept hits.
+  // Assume every hit is kept: then a hit's two predecessors are the previous
+  // hit lanes; from the first hit that equals one of them, resolve in order.
   uint64_t keep[C::NR];
-  uint64_t hitm[C::NR];
+  uint32_t A = 0, B = 0;                  // last two kept hashes (the reference's pq0/pq1 as a set)
 #pragma unroll
-  for (int r = 0; r < C::NR; ++r) { keep[r] = 0; hitm[r] = __ballot(hit[r]); }
-  uint32_t pq0 = 0, pq1 = 0;
-  int npq = 0;
-  for (int i = 0; i < n; ++i) {
-    const int l = i & 63, r = i >> 6;
-    const uint32_t hv = rdlu(pick(h, r), l);
-    if (hv == pq0 || hv == pq1) continue;
-    const uint64_t hm = pick(hitm, r);
-    if (!((hm >> l) & 1)) continue;
-    if (npq == 0) pq0 = hv; else pq1 = hv;
-    npq ^= 1;
-    or_bit(keep, r, l);
+  for (int r = 0; r < C::NR; ++r) {
+    const uint64_t hm = __ballot(hit[r]);
+    const uint32_t hv = h[r];
+    const uint64_t hb = hm & lanemask_lt(lane);
+    const int q1 = hb ? 63 - __builtin_clzll(hb) : -1;
+    const uint64_t hb2 = q1 > 0 ? (hb & lanemask_lt(q1)) : 0ull;
+    const int q2 = hb2 ? 63 - __builtin_clzll(hb2) : -1;
+    const uint32_t h1 = (uint32_t)__shfl((int)hv, q1 < 0 ? lane : q1, 64);
+    const uint32_t h2 = (uint32_t)__shfl((int)hv, q2 < 0 ? lane : q2, 64);
+    const uint32_t a = q1 < 0 ? A : h1;
+    const uint32_t b = q1 < 0 ? B : (q2 < 0 ? A : h2);
+    const uint64_t cm = __ballot(hit[r] && (hv == a || hv == b));
+    uint64_t k = hm;
+    if (cm) {
+      const int f = __builtin_ctzll(cm);
+      k = hm & lanemask_lt(f);
+      uint32_t xA = rdlu(a, f), xB = rdlu(b, f);
+      for (uint64_t rest = hm & ~lanemask_lt(f); rest; rest &= rest - 1) {
+        const int l = __builtin_ctzll(rest);
+        const uint32_t v = rdlu(hv, l);
+        if (v == xA || v == xB) continue;
+        xB = xA;
+        xA = v;
+        k |= 1ull << l;
+      }
+      A = xA;
+      B = xB;
+    } else if (hm) {
+      const int t1 = 63 - __builtin_clzll(hm);
+      const uint64_t r2 = hm & ~(1ull << t1);
+      B = r2 ? rdlu(hv, 63 - __builtin_clzll(r2)) : A;
+      A = rdlu(hv, t1);
+    }
+    keep[r] = k;
   }
   int base = 0;
 #pragma unroll
@@ -591,23 +656,48 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
       wh[r] = octa_hash40(text + a, we - a);
     }
   }
-  // scalar repeat filter (updates the pair partner even when probes miss)
+  // repeat filter (updates the pair partner even when probes miss): every word
+  // takes part; assume none repeats, so a word's two predecessors are the
+  // previous two lanes; from the first repeat, resolve in order.
   uint64_t keep[C::NR];
-  uint32_t tlo[C::NR], thi[C::NR];
+  uint32_t tlo[C::NR], thi[C::NR];        // pair partner = the previous kept word
+  uint64_t A = 0, B = 0;                  // last two kept word hashes (po0/po1 as a set)
 #pragma unroll
-  for (int r = 0; r < C::NR; ++r) { keep[r] = 0; tlo[r] = 0; thi[r] = 0; }
-  uint64_t po0 = 0, po1 = 0;
-  int npo = 0;
-  for (int i = 0; i < nw; ++i) {
-    const int l = i & 63, r = i >> 6;
-    const uint64_t v = rdl64(pick(wh, r), l);
-    if (v == po0 || v == po1) continue;
-    uint64_t tph;
-    if (npo == 0) { po0 = v; tph = po1; } else { po1 = v; tph = po0; }
-    npo ^= 1;
-    or_bit(keep, r, l);
-    put_lane(tlo, r, l, (uint32_t)tph);
-    put_lane(thi, r, l, (uint32_t)(tph >> 32));
+  for (int r = 0; r < C::NR; ++r) {
+    const int i = r * 64 + lane;
+    const bool v = i < nw;
+    const uint64_t vm = __ballot(v);
+    keep[r] = 0; tlo[r] = 0; thi[r] = 0;
+    if (!vm) continue;
+    const int nv = __popcll(vm);
+    const uint64_t w = wh[r];
+    const uint64_t h1 = rdl_shfl64(w, lane >= 1 ? lane - 1 : lane), h2 = rdl_shfl64(w, lane >= 2 ? lane - 2 : lane);
+    const uint64_t pa = lane >= 1 ? h1 : A;
+    const uint64_t pb = lane >= 2 ? h2 : (lane == 1 ? A : B);
+    const uint64_t cm = __ballot(v && (w == pa || w == pb));
+    uint64_t k = vm;
+    uint64_t tp = pa;
+    if (cm) {
+      const int f = __builtin_ctzll(cm);
+      k = vm & lanemask_lt(f);
+      uint64_t xA = rdl64(pa, f), xB = rdl64(pb, f);
+      for (int l = f; l < nv; ++l) {
+        const uint64_t hv = rdl64(w, l);
+        if (hv == xA || hv == xB) continue;
+        if (lane == l) tp = xA;
+        xB = xA;
+        xA = hv;
+        k |= 1ull << l;
+      }
+      A = xA;
+      B = xB;
+    } else {
+      B = nv >= 2 ? rdl64(w, nv - 2) : A;
+      A = rdl64(w, nv - 1);
+    }
+    keep[r] = k;
+    tlo[r] = (uint32_t)tp;
+    thi[r] = (uint32_t)(tp >> 32);
   }
   // probes and ordered compaction: X gets (pair @ prior word, word @ word), D gets (word @ word)
   int xb = 0, db = 0;
