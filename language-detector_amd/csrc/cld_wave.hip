@@ -79,38 +79,39 @@ __device__ __forceinline__ void or_bit(uint64_t (&a)[N], int r, int l) {
   for (int i = 0; i < N; ++i) if (r == i) a[i] |= 1ull << l;
 }
 
+// Wavefront scans and reductions on DPP (no LDS round trip): Hillis-Steele
+// inside each 16-lane row (row_shr 1, 2, 4, 8), then row 0's total into row 1
+// and row 2's into row 3 (row_bcast:15), then lane 31 into rows 2-3
+// (row_bcast:31).  Lanes without a source keep the identity (bound_ctrl off,
+// old = identity).  Called with all 64 lanes active.
+constexpr int kDppRowShr = 0x110, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+template <class Op>
+__device__ __forceinline__ uint32_t dpp_scan_incl(uint32_t x, uint32_t id, Op op) {
+  const int xi = (int)x;
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, xi, kDppRowShr | 1, 0xF, 0xF, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, kDppRowShr | 2, 0xF, 0xF, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, kDppRowShr | 4, 0xF, 0xF, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, kDppRowShr | 8, 0xF, 0xF, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, kDppRowBcast15, 0xA, 0xF, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, kDppRowBcast31, 0xC, 0xF, false));
+  return x;
+}
+struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMax { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };
+struct OpMin { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
+struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+
 __device__ __forceinline__ int excl_scan(int v, int lane) {
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x - v;
+  (void)lane;
+  return (int)dpp_scan_incl((uint32_t)v, 0u, OpAdd()) - v;
 }
-__device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-__device__ __forceinline__ uint32_t wmax(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64); v = o > v ? o : v; }
-  return v;
-}
-__device__ __forceinline__ uint32_t wmin(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64); v = o < v ? o : v; }
-  return v;
-}
+__device__ __forceinline__ int wsum(int v) { return rdl((int)dpp_scan_incl((uint32_t)v, 0u, OpAdd()), 63); }
+__device__ __forceinline__ uint32_t wmax(uint32_t v) { return rdlu(dpp_scan_incl(v, 0u, OpMax()), 63); }
+__device__ __forceinline__ uint32_t wmin(uint32_t v) { return rdlu(dpp_scan_incl(v, 0xFFFFFFFFu, OpMin()), 63); }
 __device__ __forceinline__ uint64_t wor64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64);
-    uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
-    v |= ((uint64_t)hi << 32) | lo;
-  }
-  return v;
+  const uint32_t lo = rdlu(dpp_scan_incl((uint32_t)v, 0u, OpOr()), 63);
+  const uint32_t hi = rdlu(dpp_scan_incl((uint32_t)(v >> 32), 0u, OpOr()), 63);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // Per-wave capacities for documents of at most CAP bytes.  Anything that
