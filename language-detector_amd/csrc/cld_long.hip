@@ -801,7 +801,7 @@ __device__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int
       wh = octa_hash40(text + a, we - a);
     }
     // filter (every word takes part): fast path assumes no drop in this block
-    const uint64_t h1 = shfl64(wh, lane >= 1 ? lane - 1 : lane), h2 = shfl64(wh, lane >= 2 ? lane - 2 : lane);
+    const uint64_t h1 = wave::wshr1_64(wh), h2 = wave::wshr1_64(h1);   // lanes - 1, - 2 (used from lanes 1, 2 on)
     const uint64_t pa = lane >= 1 ? h1 : A;
     const uint64_t pb = lane >= 2 ? h2 : (lane == 1 ? A : B);
     const uint64_t cm = __ballot(v && (wh == pa || wh == pb));
@@ -1108,8 +1108,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
         }
         ch = lo;
       }
-      const int up = __shfl(ch, lane - 1, 64);          // all lanes: ?: would run it with lane 0 off
-      const int prev = lane == 0 ? pch : up;
+      const int prev = (int)wave::wshr1((uint32_t)ch, (uint32_t)pch);   // lane - 1's chunk; lane 0: the last block's
       if (i < n)
         for (int k = prev + 1; k <= ch; ++k) s.st[pass][k] = (uint16_t)i;
       pch = rdl(ch, 63);

@@ -43,9 +43,6 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
   return ((uint64_t)rdlu((uint32_t)(v >> 32), l) << 32) | rdlu((uint32_t)v, l);
 }
 
-__device__ __forceinline__ uint64_t rdl_shfl64(uint64_t v, int l) {
-  return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)v, l, 64);
-}
 
 // Order LDS traffic between lanes of one wavefront (no workgroup barrier:
 // the waves of a workgroup work on different documents).
@@ -100,6 +97,15 @@ struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { re
 struct OpMax { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };
 struct OpMin { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
 struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+
+// Value of lane-1 (wave_shr:1); lane 0 gets `first`.
+constexpr int kDppWaveShr1 = 0x138;
+__device__ __forceinline__ uint32_t wshr1(uint32_t x, uint32_t first) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)x, kDppWaveShr1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t wshr1_64(uint64_t x) {
+  return ((uint64_t)wshr1((uint32_t)(x >> 32), (uint32_t)(x >> 32)) << 32) | wshr1((uint32_t)x, (uint32_t)x);
+}
 
 __device__ __forceinline__ int excl_scan(int v, int lane) {
   (void)lane;
@@ -672,7 +678,7 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
     if (!vm) continue;
     const int nv = __popcll(vm);
     const uint64_t w = wh[r];
-    const uint64_t h1 = rdl_shfl64(w, lane >= 1 ? lane - 1 : lane), h2 = rdl_shfl64(w, lane >= 2 ? lane - 2 : lane);
+    const uint64_t h1 = wshr1_64(w), h2 = wshr1_64(h1);   // lanes - 1, - 2 (used from lanes 1, 2 on)
     const uint64_t pa = lane >= 1 ? h1 : A;
     const uint64_t pb = lane >= 2 ? h2 : (lane == 1 ? A : B);
     const uint64_t cm = __ballot(v && (w == pa || w == pb));
@@ -999,15 +1005,9 @@ __device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
   if (key == kUnusedKey) val = -1;
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
-    // exclusive running max of slots p..lane-1
-    int m = (in && lane >= p) ? val : INT_MIN;
-#pragma unroll
-    for (int d = 1; d < 32; d <<= 1) {
-      const int y = __shfl_up(m, d, 64);
-      if (lane >= d) m = m > y ? m : y;
-    }
-    int ex = __shfl_up(m, 1, 64);
-    if (lane == 0) ex = INT_MIN;
+    // exclusive running max of slots p..lane-1 (values biased to unsigned)
+    const uint32_t m = dpp_scan_incl((in && lane >= p) ? (uint32_t)val ^ 0x80000000u : 0u, 0u, OpMax());
+    const int ex = (int)(wshr1(m, 0u) ^ 0x80000000u);
     const uint64_t R = __ballot(in && lane > p && val > ex);
     if (R) {
       int src = lane;
