@@ -95,9 +95,11 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
 // blockIdx.x * WPB + wave and pulls documents from the wave kernel's re-queue
 // list (one atomic per document) until the list is drained -- every wave
 // reaches that exit.  Documents it cannot reproduce go to the k_general list.
-// LNG_WPS waves per SIMD (4: ~25 VGPRs spill, still faster than 3 spill-free: the kernel is latency-bound)
+// LNG_WPS waves per SIMD.  The kernel is latency-bound on its HBM slots:
+// more resident waves beat the extra spills (C3, 30K pages: 4 -> 496K, 5 ->
+// 538K, 6 -> 553K, 7 -> 578K, 8 -> 541K docs/s; profiles/round1e_*).
 #ifndef LNG_WPS
-#define LNG_WPS 4
+#define LNG_WPS 7
 #endif
 template <int WPB, bool DIAG>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const uint8_t* __restrict__ buf,
