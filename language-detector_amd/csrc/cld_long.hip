@@ -323,8 +323,10 @@ __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lan
 
 // The sequential lowercaser for the rare cut-character tail, kept out of
 // line so its state does not count against the kernel's registers.
-__device__ __noinline__ int lower_tail(const DevTables& T, const uint8_t* in, int ilen, uint8_t* out, int olen) {
-  return lower_replace(T, in, ilen, out, olen);
+// The machine goes by value: a reference into the kernel's DevTables
+// argument would make every wave copy the whole struct to scratch at entry.
+__device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, uint8_t* out, int olen) {
+  return lower_replace_sm(sm, in, ilen, out, olen);
 }
 
 // --------------------------------------- stage 1: span text, lowered
@@ -446,7 +448,7 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       const int nc = utf8_len(dv.p[cutx]);
       for (int k = 0; k < nc; ++k) tail[k] = (uint8_t)dv.at(cutx + k);
       for (int k = 0; k < 4; ++k) tail[nc + k] = ' ';                 // separator + "   " (ilen stops before \0)
-      filled = lower_tail(T, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
+      filled = lower_tail(T.lower, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
     }
     lpos += rdl(filled, 0);
     for (int k = lane; k < 40; k += 64) lb[lpos + k] = 0;

@@ -181,8 +181,7 @@ __device__ int scan_to_letter_or_special(const DevTables& T, const DocView& d, i
 // `olen` is the reference's logical output capacity (kMaxScriptLowerBuffer);
 // the physical buffer only needs 1.5x the input (max per-char expansion of
 // this table, verified by tests/test_tables.py) plus padding.
-__device__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen) {
-  const DevSM& sm = T.lower;
+__device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, uint8_t* out0, int olen) {
   const int sh = (int)sm.shift;
   const int nEntries = 1 << sh;
   int total_filled = 0;
@@ -284,6 +283,10 @@ __device__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, u
     in += consumed; inlen -= consumed; out += filled; outlen -= filled;
   }
   return total_filled;
+}
+
+__device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen) {
+  return lower_replace_sm(T.lower, in0, ilen, out0, olen);
 }
 
 // ------------------------------------------------------------ lang/script
