@@ -296,38 +296,60 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
   if (q >= L) { next = L; return 0; }
   const int spanscript = ufl(s.sn[q]);
   ulscript = spanscript;
-  for (int w = q >> 6; w < C::NM; ++w) {
-    int p = w * 64 + lane;
-    bool b = false;
-    if (p >= q && p < L && (s.doc[p] & 0xC0) != 0x80) {
-      int sc = s.sn[p];
+  // All lanes at once, one 64-byte window at a time.  Events: B = a character
+  // the letters loop breaks on, O = a letter stop of the span script (or
+  // Inherited), F = a letter stop of another script.  In a run only B matters
+  // (it ends the run: ' '), in a gap only letter stops (O starts the next run,
+  // F ends the span), and B and O never coincide -- so a byte is in a run iff
+  // the last B/O event at or before it is an O (the carried state if none).
+  if (lane == 0) s.u.sbuf[0] = ' ';
+  int put = 1, take = L;
+  bool run = true;                                   // q is an O event
+  for (int w = q >> 6; w < C::NM && w * 64 < L; ++w) {
+    const int x = w * 64 + lane;
+    const bool valid = x >= q && x < L;
+    const uint32_t c = valid ? s.doc[x] : 0u;
+    const bool lead = valid && (c & 0xC0) != 0x80;
+    bool brk = false, ok = false, foreign = false;
+    if (lead) {
+      const int sc = s.sn[x];
       if (sc != spanscript && sc != inherited) {
         if (sc == common) {
-          b = true;
+          brk = true;
         } else {
-          int sc2 = s.sn[p + utf8_len(s.doc[p])];
-          if (sc2 != common && sc2 != spanscript) b = true;
+          const int sc2 = s.sn[x + utf8_len((uint8_t)c)];
+          brk = sc2 != common && sc2 != spanscript;
         }
       }
+      if ((s.lsm[w] >> lane) & 1) {
+        if (sc == spanscript || sc == inherited) ok = true;
+        else foreign = true;
+      }
     }
-    uint64_t m = __ballot(b);
-    if (lane == 0) s.brk[w] = m;
+    const uint64_t Bm = __ballot(brk), Om = __ballot(ok);
+    const uint64_t evm = Bm | Om;
+    const uint64_t ev_le = evm & (lane == 63 ? ~0ull : ((2ull << lane) - 1)), ev_lt = evm & lanemask_lt(lane);
+    const bool inrun = ev_le ? ((Om >> (63 - __builtin_clzll(ev_le))) & 1) : run;
+    const bool prev_run = ev_lt ? ((Om >> (63 - __builtin_clzll(ev_lt))) & 1) : run;
+    const uint64_t Em = __ballot(foreign && (brk || !prev_run));   // F while in a gap: the span ends here
+    const int stop = Em ? __builtin_ctzll(Em) : 64;
+    const bool cp = valid && inrun && lane < stop;
+    const bool sep = brk && prev_run && lane <= stop;
+    const int cnt = (cp ? 1 : 0) + (sep ? 1 : 0);
+    const int pos = put + excl_scan(cnt, lane);
+    if (cp) s.u.sbuf[pos] = (uint8_t)c;
+    if (sep) s.u.sbuf[pos] = ' ';
+    put = rdl(pos + cnt, 63);
+    if (stop < 64) {
+      take = w * 64 + stop;
+      run = false;
+      break;
+    }
+    if (evm) run = (Om >> (63 - __builtin_clzll(evm))) & 1;
   }
-  wsync();
-  if (lane == 0) s.u.sbuf[0] = ' ';
-  int put = 1, p = q, take;
-  for (;;) {
-    const int b = find_first<C::NM>(s.brk, p, L);
-    for (int i = lane; i < b - p; i += 64) s.u.sbuf[put + i] = s.doc[p + i];
-    put += b - p;
+  if (run) {                                         // the document ended inside a run
     if (lane == 0) s.u.sbuf[put] = ' ';
     ++put;
-    if (b >= L) { take = L; break; }
-    const int q2 = find_first<C::NM>(s.lsm, b, L);
-    if (q2 >= L) { take = L; break; }
-    const int sc = ufl(s.sn[q2]);
-    if (sc != spanscript && sc != inherited) { take = q2; break; }
-    p = q2;
   }
   if (lane < 4) s.u.sbuf[put + lane] = lane < 3 ? ' ' : 0;
   next = take;

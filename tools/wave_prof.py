@@ -26,7 +26,7 @@ def main():
         cld_amd.detect_batch(buf=buf, offsets=offs)
         st = cld_amd.last_stats(0)
         c = cld_amd.stage_cycles(0).astype(np.float64)
-        nw = max(1, st.short_docs)
+        nw = max(1, st.short_docs // 64)          # k_wave samples one document in 64
         print("%s: %d docs, wave kernel %.3f ms, long %.3f ms (%d docs), general %.3f ms (%d docs)" %
               (cfg, n, st.short_ms, st.long_ms, st.long_docs, st.general_ms, st.general_docs))
         tot = c[:7].sum()
