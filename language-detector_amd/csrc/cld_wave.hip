@@ -829,6 +829,10 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   const DevTbl& xob = cjk ? T.distinctbi : T.distinctocta;
   const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
 
+  // the first 64 delta/distinct langprob gathers are issued together with the
+  // base ones, so the three table reads share one L2 round trip
+  const uint32_t dpre = lane < nd ? ind_at(dob, s.d_ind[lane]) : 0u;
+  const uint32_t xpre = lane < nx ? ind_at(xob, s.x_ind[lane]) : 0u;
   // base hits -> base emissions (1 or 2 langprobs each, zeros dropped), in order
   int eb = 0;
   for (int j0 = 0; j0 < nb; j0 += 64) {
@@ -859,7 +863,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   int ed = 0, ex = 0;
   for (int j0 = 0; j0 < nd; j0 += 64) {
     const int j = j0 + lane;
-    uint32_t lp = j < nd ? ind_at(dob, s.d_ind[j]) : 0u;
+    uint32_t lp = j0 == 0 ? dpre : j < nd ? ind_at(dob, s.d_ind[j]) : 0u;
     const int o = ed + excl_scan(lp != 0, lane);
     uint16_t off = j < nd ? s.d_off[j] : 0;
     if (lp) { s.d_off[o] = off; s.d_ind[o] = lp; }
@@ -867,7 +871,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   }
   for (int j0 = 0; j0 < nx; j0 += 64) {
     const int j = j0 + lane;
-    uint32_t lp = j < nx ? ind_at(xob, s.x_ind[j]) : 0u;
+    uint32_t lp = j0 == 0 ? xpre : j < nx ? ind_at(xob, s.x_ind[j]) : 0u;
     const int o = ex + excl_scan(lp != 0, lane);
     uint16_t off = j < nx ? s.x_off[j] : 0;
     if (lp) { s.x_off[o] = off; s.x_ind[o] = lp; }
@@ -926,6 +930,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   ring_sel = rs;
   // X emissions with chunk <= k, for the boosts (X is in linear order)
   int xc = 0;
+  int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
   for (int k = 0; k < K; ++k) {
     // zero the tote
     reinterpret_cast<uint2*>(s.u.tote)[lane] = make_uint2(0, 0);
@@ -977,29 +982,43 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
       best = wmax(best);
       if (best) { key3[r] = 255 - (int)(best & 0xFF); sc3[r] = (best >> 8) - 1; }
     }
-    if (lane == 0) {
-      const uint32_t lo_k = s.lo[k];
-      const int lo = lo_k == 0xFFFFFFFFu ? dummy_off : (int)lo_k;
-      int hi = dummy_off;
-      if (k + 1 < K && s.lo[k + 1] != 0xFFFFFFFFu) hi = (int)s.lo[k + 1];
-      const int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
-      const int lang2 = from_per_script_number(T, ulscript, (uint8_t)key3[1]);
-      const int len = hi - lo;
-      const int sc1 = key3[0] >= 0 ? (int)sc3[0] : 0;
-      const int sc2 = key3[1] >= 0 ? (int)sc3[1] : 0;
-      int actual = 0;
-      if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
-      const int esub = lang1 * 4 + lscript4(T, ulscript);
-      const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
-      const uint16_t bytes = (uint16_t)len, grams = (uint16_t)score_count;
-      const uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
-      int rd = (uint8_t)reliability_delta(s1, s2, grams);
-      const int cs1 = close_set(T, lang1);
-      if (cs1 != 0 && cs1 == close_set(T, lang2)) rd = 100;
-      const int rsc = (uint8_t)reliability_expected(actual, expected);
-      if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
+    // lane k keeps chunk k's top two; the summaries are made after the loop
+    if (lane == k) {
+      ck1 = key3[0]; ck2 = key3[1];
+      cs1 = key3[0] >= 0 ? (int)sc3[0] : 0;
+      cs2 = key3[1] >= 0 ? (int)sc3[1] : 0;
+      cgr = score_count;
     }
     wsync();
+  }
+  // SetChunkSummary (scoreonescriptspan.cc:60-96) for every chunk at once, one
+  // lane per chunk; the DocTote adds then run in chunk order on lane 0
+  int sum_lang = 0, sum_bytes = 0, sum_rel = 0;
+  if (lane < K) {
+    const uint32_t lo_k = s.lo[lane];
+    const int lo = lo_k == 0xFFFFFFFFu ? dummy_off : (int)lo_k;
+    int hi = dummy_off;
+    if (lane + 1 < K && s.lo[lane + 1] != 0xFFFFFFFFu) hi = (int)s.lo[lane + 1];
+    const int lang1 = from_per_script_number(T, ulscript, (uint8_t)ck1);
+    const int lang2 = from_per_script_number(T, ulscript, (uint8_t)ck2);
+    const int len = hi - lo;
+    int actual = 0;
+    if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
+    const int esub = lang1 * 4 + lscript4(T, ulscript);
+    const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+    const uint16_t bytes = (uint16_t)len, grams = (uint16_t)cgr;
+    const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2;
+    int rd = (uint8_t)reliability_delta(s1, s2, grams);
+    const int c1 = close_set(T, lang1);
+    if (c1 != 0 && c1 == close_set(T, lang2)) rd = 100;
+    const int rsc = (uint8_t)reliability_expected(actual, expected);
+    sum_lang = (uint16_t)lang1; sum_bytes = bytes; sum_rel = rd < rsc ? rd : rsc;
+    cs1 = s1;
+  }
+  const int nsum = K < kMaxSummaries ? K : kMaxSummaries;
+  for (int k = 0; k < nsum; ++k) {
+    const int l1 = rdl(sum_lang, k), by = rdl(sum_bytes, k), sc = rdl(cs1, k), rl = rdl(sum_rel, k);
+    if (lane == 0) s.dt.add((uint16_t)l1, by, sc, rl);
   }
   // the ring keeps the last four distinct langprobs
   if (lane == 0) {
