@@ -78,7 +78,10 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
                                                    uint32_t* __restrict__ counters,
                                                    unsigned long long* __restrict__ prof) {
   __shared__ wave::Smem<CAP> smem[WPB];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index through readfirstlane: the document pointer, its length, the
+  // result pointer and the LDS base are then scalars, not VGPRs live across
+  // the whole document
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int i = blockIdx.x * WPB + wv;
   if (i >= n) return;
   const uint64_t a = offs[i], b = offs[i + 1];

@@ -1199,6 +1199,11 @@ __device__ __forceinline__ bool is_figs(const DevTables& T, int l) {
 }
 __device__ __forceinline__ bool is_efigs(const DevTables& T, int l) { return l == (int)T.english || is_figs(T, l); }
 
+// a[i] for a runtime i in 0..2 as selects, so Extract stays in registers
+// (a dynamically indexed member array would put the whole struct in scratch)
+template <class V>
+__device__ __forceinline__ V sel3(const V (&a)[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
+
 // CalcSummaryLang :1414-1522
 __device__ int calc_summary_lang(const DevTables& T, int total, const Extract& x, bool& rel) {
   const int unk = (int)T.unknown_lang, en = (int)T.english;
@@ -1215,13 +1220,13 @@ __device__ int calc_summary_lang(const DevTables& T, int total, const Extract& x
       for (int j = i + 1; j < 3; ++j) active[j - 1] = active[j];
       --slot_count;
       ret_pct = (x.pct3[0] * 100) / (101 - ignore);
-      summary = x.lang3[active[0]];
-      if (x.pct3[active[0]] < 2) rel = false;
+      summary = sel3(x.lang3, active[0]);
+      if (sel3(x.pct3, active[0]) < 2) rel = false;
     }
   }
-  int second_bytes = (total * x.pct3[active[1]]) / 100;
-  int l0 = x.lang3[active[0]], l1 = x.lang3[active[1]];
-  int p0 = x.pct3[active[0]], p1 = x.pct3[active[1]];
+  int second_bytes = (total * sel3(x.pct3, active[1])) / 100;
+  int l0 = sel3(x.lang3, active[0]), l1 = sel3(x.lang3, active[1]);
+  int p0 = sel3(x.pct3, active[0]), p1 = sel3(x.pct3, active[1]);
   if (l0 == en && l1 != en && l1 != unk && p1 >= 17 && second_bytes >= 15) {
     ignore += p0; ret_pct = (p1 * 100) / (101 - ignore); summary = l1;
     if (p1 < 2) rel = false;
