@@ -102,9 +102,11 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
 // reaches that exit.  Documents it cannot reproduce go to the k_general list.
 // LNG_WPS waves per SIMD.  The kernel is latency-bound on its HBM slots:
 // more resident waves beat the extra spills (C3, 30K pages: 4 -> 496K, 5 ->
-// 538K, 6 -> 553K, 7 -> 578K, 8 -> 541K docs/s; profiles/round1e_*).
+// 538K, 6 -> 553K, 7 -> 578K, 8 -> 541K docs/s; profiles/round1e_*).  After
+// round 1j's lane-parallel chunk summaries 8 wins (C3 100K pages: 6 -> 566K,
+// 7 -> 738K, 8 -> 754K docs/s; profiles/round1j_ab_long/).  9 does not fit.
 #ifndef LNG_WPS
-#define LNG_WPS 7
+#define LNG_WPS 8
 #endif
 template <int WPB, bool DIAG>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const uint8_t* __restrict__ buf,

@@ -1130,6 +1130,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   wsync();
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
+  int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
   for (int k = 0; k < K; ++k) {
     reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
     const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
@@ -1184,38 +1185,57 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
         sc3[r] = (best >> 8) - 1;
       }
     }
+    // lane k keeps chunk k's top two keys and scores; the summaries are made after the loop
+    if (lane == k) {
+      ck1 = key3[0]; ck2 = key3[1];
+      cs1 = key3[0] >= 0 ? (int)sc3[0] : 0;
+      cs2 = key3[1] >= 0 ? (int)sc3[1] : 0;
+      cgr = score_count;
+    }
+    wsync();
+  }
+  // SetChunkSummary (scoreonescriptspan.cc:60-96) for every chunk at once, one
+  // lane per chunk (K <= kMaxCh = 64); the DocTote adds then run in chunk order on lane 0
+  int lo = 0, hi = 0, lang1 = 0, lang2 = 0, rd = 0, rsc = 0;
+  if (lane < K) {
+    const uint32_t lo_k = s.lo[lane];
+    lo = lo_k == kInf ? dummy_off : (int)lo_k;
+    hi = dummy_off;
+    if (lane + 1 < K && s.lo[lane + 1] != kInf) hi = (int)s.lo[lane + 1];
+    const uint32_t i1 = s.kl[(uint8_t)ck1], i2 = s.kl[(uint8_t)ck2];
+    lang1 = (int)(i1 & 0xFFFF); lang2 = (int)(i2 & 0xFFFF);
+    const int len = hi - lo;
+    int actual = 0;
+    if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
+    const int expected = s.ke[(uint8_t)ck1];
+    const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2, grams = (uint16_t)cgr;
+    rd = (uint8_t)reliability_delta(s1, s2, grams);
+    const int c1 = (int)(i1 >> 16);
+    if (c1 != 0 && c1 == (int)(i2 >> 16)) rd = 100;
+    rsc = (uint8_t)reliability_expected(actual, expected);
+    cs1 = s1; cs2 = s2; cgr = grams;
+  }
+  for (int k = 0; k < K; ++k) {
+    const int l1 = rdl(lang1, k), l0 = rdl(lo, k), h0 = rdl(hi, k), sc = rdl(cs1, k);
+    const int r1 = rdl(rd, k), r2 = rdl(rsc, k);
     if (lane == 0) {
-      const uint32_t lo_k = s.lo[k];
-      const int lo = lo_k == kInf ? dummy_off : (int)lo_k;
-      int hi = dummy_off;
-      if (k + 1 < K && s.lo[k + 1] != kInf) hi = (int)s.lo[k + 1];
-      const uint32_t i1 = s.kl[(uint8_t)key3[0]], i2 = s.kl[(uint8_t)key3[1]];
-      const int lang1 = (int)(i1 & 0xFFFF), lang2 = (int)(i2 & 0xFFFF);
-      const int len = hi - lo;
-      const int sc1 = key3[0] >= 0 ? (int)sc3[0] : 0;
-      const int sc2 = key3[1] >= 0 ? (int)sc3[1] : 0;
-      int actual = 0;
-      if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
-      const int expected = s.ke[(uint8_t)key3[0]];
-      const uint16_t bytes = (uint16_t)len, grams = (uint16_t)score_count;
-      const uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
-      int rd = (uint8_t)reliability_delta(s1, s2, grams);
-      const int cs1 = (int)(i1 >> 16);
-      if (cs1 != 0 && cs1 == (int)(i2 >> 16)) rd = 100;
-      const int rsc = (uint8_t)reliability_expected(actual, expected);
-      if (k < kMaxSummaries) s.dt.add((uint16_t)lang1, bytes, s1, rd < rsc ? rd : rsc);
+      const uint16_t bytes = (uint16_t)(h0 - l0);
+      if (k < kMaxSummaries) s.dt.add((uint16_t)l1, bytes, sc, r1 < r2 ? r1 : r2);
       if (D && s.dbg) {
+        const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
+        const int ds = s.st[0][k], de = s.st[0][k + 1], xs = s.st[1][k], xe = s.st[1][k + 1];
         uint32_t* o = s.dbg + 1 + s.dbg_pos;
-        const uint32_t v[18] = {'C', (uint32_t)lo, (uint32_t)hi, (uint32_t)lang1, (uint32_t)lang2, s1, s2,
-                                grams, (uint32_t)rd, (uint32_t)rsc, (uint32_t)bs, (uint32_t)be, (uint32_t)ds,
+        const uint32_t v[18] = {'C', (uint32_t)l0, (uint32_t)h0, (uint32_t)l1, (uint32_t)rdl(lang2, k),
+                                (uint32_t)sc, (uint32_t)rdl(cs2, k), (uint32_t)rdl(cgr, k), (uint32_t)r1,
+                                (uint32_t)r2, (uint32_t)bs, (uint32_t)be, (uint32_t)ds,
                                 (uint32_t)de, (uint32_t)xs, (uint32_t)xe, (uint32_t)s.theta[k], (uint32_t)(eb << 16 | K)};
         for (int i = 0; i < 18; ++i) o[i] = v[i];
         s.dbg_pos += 18;
         s.dbg[0] = s.dbg_pos;
       }
     }
-    wsync();
   }
+  wsync();
   // the ring keeps the last four distinct langprobs
   if (lane == 0) {
     uint64_t r4[4];
