@@ -99,7 +99,7 @@ struct OpMin { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { re
 struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
 
 // Value of lane-1 (wave_shr:1); lane 0 gets `first`.
-constexpr int kDppWaveShr1 = 0x138;
+constexpr int kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
 __device__ __forceinline__ uint32_t wshr1(uint32_t x, uint32_t first) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)x, kDppWaveShr1, 0xF, 0xF, false);
 }
@@ -208,7 +208,24 @@ __device__ __forceinline__ int cpt_index(uint32_t b0, uint32_t b1, uint32_t b2, 
 template <int CAP>
 __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane) {
   using C = Cfg<CAP>;
-  for (int p = lane; p < C::DOC; p += 64) s.doc[p] = p < L ? g[p] : (uint8_t)0;
+  static_assert(CAP == 256 && C::DOC == 288, "one aligned dword per lane covers the document");
+  {
+    // aligned dword loads of only the words that overlap [g, g+L) (never past
+    // the buffer), realigned with the next lane's word, bytes >= L zeroed
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(g);
+    const int sh = (int)(ga & 3);
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(ga - (uintptr_t)sh);
+    const int nw = (L + sh + 3) >> 2;                    // <= 65
+    const uint32_t w0 = lane < nw ? gw[lane] : 0u;
+    const uint32_t w64 = nw > 64 ? gw[64] : 0u;
+    // lane + 1's word (DPP wave_shl:1); lane 63 keeps `old` = word 64
+    const uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp((int)w64, (int)w0, kDppWaveShl1, 0xF, 0xF, false);
+    const uint32_t v = sh == 0 ? w0 : __builtin_amdgcn_alignbyte(nxt, w0, (uint32_t)sh);
+    const int nb = L - 4 * lane;
+    const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+    reinterpret_cast<uint32_t*>(s.doc)[lane] = v & keep;
+    if (lane < (C::DOC - 256) / 4) reinterpret_cast<uint32_t*>(s.doc)[64 + lane] = 0u;
+  }
   wsync();
   DocView dv{s.doc, L};
   // Fast path: every character is a complete, well-formed 1-3 byte sequence
