@@ -150,11 +150,11 @@ struct Smem {
   uint8_t sn[C::DOC];                 // script number at each byte position (GetUTF8LetterScriptNum)
   uint64_t lsm[C::NM];                // letter stops: char start, scanner stops there, script != 0
   uint64_t brk[C::NM];                // letters that end a run for the current span script
-  union alignas(16) {
-    uint8_t sbuf[C::SB];              // span text (raw)
-    uint32_t tote[128];               // chunk tote: two 16-bit keys per word (see kToteNoCarry)
-  } u;
-  uint8_t lbuf[C::LB];                // lowered span text
+  alignas(16) uint8_t sbuf[C::SB];    // span text (raw)
+  union alignas(16) {                 // scoring reads only hit offsets, never the span text:
+    uint8_t lbuf[C::LB];              //   lowered span text
+    uint32_t tote[128];               //   chunk tote: two 16-bit keys per word (see kToteNoCarry)
+  };
   union alignas(16) {                 // stage-local arrays
     uint16_t nx[CAP];                 // load: p + ScanToLetterOrSpecial(p, L - p)
     uint16_t nxq[C::LB];              // quad hits: next quad start for a quad starting at p
@@ -319,7 +319,7 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
   // (it ends the run: ' '), in a gap only letter stops (O starts the next run,
   // F ends the span), and B and O never coincide -- so a byte is in a run iff
   // the last B/O event at or before it is an O (the carried state if none).
-  if (lane == 0) s.u.sbuf[0] = ' ';
+  if (lane == 0) s.sbuf[0] = ' ';
   int put = 1, take = L;
   bool run = true;                                   // q is an O event
   for (int w = q >> 6; w < C::NM && w * 64 < L; ++w) {
@@ -354,8 +354,8 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
     const bool sep = brk && prev_run && lane <= stop;
     const int cnt = (cp ? 1 : 0) + (sep ? 1 : 0);
     const int pos = put + excl_scan(cnt, lane);
-    if (cp) s.u.sbuf[pos] = (uint8_t)c;
-    if (sep) s.u.sbuf[pos] = ' ';
+    if (cp) s.sbuf[pos] = (uint8_t)c;
+    if (sep) s.sbuf[pos] = ' ';
     put = rdl(pos + cnt, 63);
     if (stop < 64) {
       take = w * 64 + stop;
@@ -365,10 +365,10 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
     if (evm) run = (Om >> (63 - __builtin_clzll(evm))) & 1;
   }
   if (run) {                                         // the document ended inside a run
-    if (lane == 0) s.u.sbuf[put] = ' ';
+    if (lane == 0) s.sbuf[put] = ' ';
     ++put;
   }
-  if (lane < 4) s.u.sbuf[put + lane] = lane < 3 ? ' ' : 0;
+  if (lane < 4) s.sbuf[put + lane] = lane < 3 ? ' ' : 0;
   next = take;
   wsync();
   return put;
@@ -477,17 +477,17 @@ __device__ int lower_span(const DevTables& T, Smem<CAP>& s, int text_bytes, int 
     const int p = w0 + lane;
     uint64_t o = 0;
     int olen = 0;
-    if (p < ilen && (s.u.sbuf[p] & 0xC0) != 0x80) {
+    if (p < ilen && (s.sbuf[p] & 0xC0) != 0x80) {
       // one property-table lookup per 1-3 byte character (the table holds
       // lower_char's result when it is <= 4 bytes); the machine otherwise
-      const int n = utf8_len(s.u.sbuf[p]);
-      const uint32_t b1 = s.u.sbuf[p + 1], b2 = s.u.sbuf[p + 2];
+      const int n = utf8_len(s.sbuf[p]);
+      const uint32_t b1 = s.sbuf[p + 1], b2 = s.sbuf[p + 2];
       const bool wf = n <= 3 && (n < 2 || (b1 & 0xC0) == 0x80) && (n < 3 || (b2 & 0xC0) == 0x80);
-      const uint64_t e = wf ? T.cpt[cpt_index(s.u.sbuf[p], b1, b2, n)] : 0ull;
+      const uint64_t e = wf ? T.cpt[cpt_index(s.sbuf[p], b1, b2, n)] : 0ull;
       if ((e >> 10) & 1) {
         olen = (int)((e >> 11) & 15);
         o = e >> 32;
-      } else if (!lower_char(T, &s.u.sbuf[p], n, o, olen)) {
+      } else if (!lower_char(T, &s.sbuf[p], n, o, olen)) {
         bad = 1;
         olen = 0;
       }
@@ -950,7 +950,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
   for (int k = 0; k < K; ++k) {
     // zero the tote
-    reinterpret_cast<uint2*>(s.u.tote)[lane] = make_uint2(0, 0);
+    reinterpret_cast<uint2*>(s.tote)[lane] = make_uint2(0, 0);
     wsync();
     uint64_t gm = 0;
     int cnt = 0;
@@ -958,9 +958,9 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     auto add = [&](uint32_t lp) {
       const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
       const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
-      if (k1) { atomicAdd(&s.u.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
-      if (k2) { atomicAdd(&s.u.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
-      if (k3) { atomicAdd(&s.u.tote[k3 >> 1], (e >> 24) << ((k3 & 1) * 16)); gm |= 1ull << (k3 >> 2); }
+      if (k1) { atomicAdd(&s.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
+      if (k2) { atomicAdd(&s.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
+      if (k3) { atomicAdd(&s.tote[k3 >> 1], (e >> 24) << ((k3 & 1) * 16)); gm |= 1ull << (k3 >> 2); }
     };
     if (k == 0 && lane == 0) { add(seed); ++cnt; }
     for (int t = lane; t < eb; t += 64)
@@ -981,7 +981,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     const int score_count = wsum(cnt);
     wsync();
     // top three keys of the in-use groups: (score desc, key asc)
-    const uint2 v2 = reinterpret_cast<const uint2*>(s.u.tote)[lane];
+    const uint2 v2 = reinterpret_cast<const uint2*>(s.tote)[lane];
     const bool inuse = (gm >> lane) & 1;
     uint32_t cand[4] = {v2.x & 0xFFFF, v2.x >> 16, v2.y & 0xFFFF, v2.y >> 16};
     int key3[3] = {-1, -1, -1};
