@@ -67,9 +67,11 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
 }
 
 // One wavefront per document of <= CAP bytes, WPB documents per workgroup.
-// WAVE_WPS waves per SIMD: 7 blocks of 22720 B LDS fit the CU's 160 KB (the
-// chunk tote overlays the lowered span text), and 72 VGPRs hold without spills
-// (C2 126M docs/s at 6 -> 130M at 7; profiles/round1n_ab_wave7/).
+// WAVE_WPS waves per SIMD: 7 blocks of 20352 B LDS fit the CU's 160 KB (the
+// chunk tote overlays the lowered span text; raw span text, base hits and
+// chunk ids share one buffer), and 72 VGPRs hold without spills (C2 126M
+// docs/s at 6 -> 130M at 7, profiles/round1n_ab_wave7/; with the smaller
+// block 139M at 7 vs 137M at 8, which also fits: profiles/round1o_ab_wave8/).
 #ifndef WAVE_WPS
 #define WAVE_WPS 7
 #endif

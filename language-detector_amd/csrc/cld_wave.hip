@@ -150,7 +150,17 @@ struct Smem {
   uint8_t sn[C::DOC];                 // script number at each byte position (GetUTF8LetterScriptNum)
   uint64_t lsm[C::NM];                // letter stops: char start, scanner stops there, script != 0
   uint64_t brk[C::NM];                // letters that end a run for the current span script
-  alignas(16) uint8_t sbuf[C::SB];    // span text (raw)
+  union alignas(16) {                 // one span's life: raw text -> base hits -> chunk ids
+    uint8_t sbuf[C::SB];              //   span text (raw); dead once lowered
+    struct {                          //   base hits before expansion (hit streams -> scoring)
+      uint32_t b_ind[C::NB];
+      uint16_t b_off[C::NB];
+    };
+    struct {                          //   chunk of each delta/distinct emission, written after
+      uint8_t d_ch[C::ND];            //   the base hits are expanded (scoring only)
+      uint8_t x_ch[C::NX];
+    };
+  };
   union alignas(16) {                 // scoring reads only hit offsets, never the span text:
     uint8_t lbuf[C::LB];              //   lowered span text
     uint32_t tote[128];               //   chunk tote: two 16-bit keys per word (see kToteNoCarry)
@@ -165,10 +175,8 @@ struct Smem {
       uint8_t be_ch[C::NE];
     } e;
   } a;
-  uint16_t b_off[C::NB]; uint32_t b_ind[C::NB];   // base hits before expansion
   uint16_t d_off[C::ND]; uint32_t d_ind[C::ND];   // delta hits; compacted in place to emissions
   uint16_t x_off[C::NX]; uint32_t x_ind[C::NX];   // distinct hits; likewise
-  uint8_t d_ch[C::ND], x_ch[C::NX];
   uint16_t E[C::MAXCH];               // cumulative base-emission count closing each chunk
   uint32_t lo[C::MAXCH];
   uint32_t ring[2][4];                // distinct boosts, latn / othr, oldest first
