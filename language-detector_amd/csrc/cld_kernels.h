@@ -11,7 +11,10 @@
 constexpr int kShortCap = 256;
 // Wavefront-per-document bucket (cld_wave.hip)
 constexpr int kWaveCap = 256;
-constexpr int kWaveWPB = 4;
+#ifndef WAVE_WPB
+#define WAVE_WPB 1
+#endif
+constexpr int kWaveWPB = WAVE_WPB;   // waves (documents) per workgroup
 // Largest kLgProbV2Tbl score byte the packed wave tote accepts (runtime checks the blob)
 constexpr int kMaxLgProbScore = 16;
 constexpr int kShortSB = 2 * kShortCap + 64;

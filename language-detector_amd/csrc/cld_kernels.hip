@@ -67,13 +67,15 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
 }
 
 // One wavefront per document of <= CAP bytes, WPB documents per workgroup.
-// WAVE_WPS waves per SIMD: 7 blocks of 20352 B LDS fit the CU's 160 KB (the
-// chunk tote overlays the lowered span text; raw span text, base hits and
-// chunk ids share one buffer), and 72 VGPRs hold without spills (C2 126M
-// docs/s at 6 -> 130M at 7, profiles/round1n_ab_wave7/; with the smaller
-// block 139M at 7 vs 137M at 8, which also fits: profiles/round1o_ab_wave8/).
+// One wave (document) per workgroup (WAVE_WPB, cld_kernels.h): a block's LDS
+// is released as soon as its own document is done, not when the slowest of
+// four is (C2 139M -> 167M docs/s; profiles/round1q_ab_wpb/).  WAVE_WPS waves
+// per SIMD: 8 blocks of 5088 B LDS per SIMD fit the CU's 160 KB (the chunk
+// tote overlays the lowered span text; raw span text, base hits and chunk
+// ids share one buffer) and 64 VGPRs hold without spills (7 -> 8 waves:
+// C2 167M -> 169M, profiles/round1q_ab_wps8/).
 #ifndef WAVE_WPS
-#define WAVE_WPS 7
+#define WAVE_WPS 8
 #endif
 template <int CAP, int WPB>
 __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const uint8_t* __restrict__ buf,
