@@ -89,7 +89,11 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   // result pointer and the LDS base are then scalars, not VGPRs live across
   // the whole document
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int i = blockIdx.x * WPB + wv;
+  // XCD-aware: workgroups go round-robin over the 8 XCDs, so block b's
+  // documents come from slice b & 7 of the batch.  Neighbouring documents
+  // then share an XCD (and its L2) for the lines they share.
+  const int per = ((n + WPB - 1) / WPB + 7) >> 3;          // blocks per XCD slice
+  const int i = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * WPB + wv;
   if (i >= n) return;
   const uint64_t a = offs[i], b = offs[i + 1];
   const int64_t len = (int64_t)(b - a);
@@ -286,7 +290,8 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  dim3 grid((n + kWaveWPB - 1) / kWaveWPB), block(64 * kWaveWPB);
+  const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
+  dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
                      requeue_list, counters, prof);
   return hipGetLastError();
