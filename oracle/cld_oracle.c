@@ -1710,6 +1710,31 @@ int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* type
 }
 
 /* Table-property probes used by tests (not part of the restated path). */
+/* Test hooks for the hash pins (oracle/hashcheck/, tests/test_hash_pins.py):
+ * kind 0 QuadHashV2 (cldutil_shared.cc:196), 1 BiHashV2 (:107),
+ * 2 OctaHash40 (:348).  w[-1] and w[n] are read, as the reference does. */
+uint64_t cldo_gram_hash(int kind, const char* w, int n) {
+  const uint8_t* p = (const uint8_t*)w;
+  if (kind == 0) return quad_hash_v2(p, n);
+  if (kind == 1) return bi_hash_v2(p, n);
+  return octa_hash40(p, n);
+}
+uint64_t cldo_pair_hash(uint64_t a, uint64_t b) { return pair_hash(a, b); }
+/* QuadHashV3Lookup4 / OctaHashV3Lookup4 on one of the loaded tables, named
+ * by its CLDT section id; returns the matching bucket keyvalue or 0. */
+uint32_t cldo_probe(int section, uint64_t h) {
+  switch (section) {
+    case CLDT_CJK_COMPAT: return quad_lookup(&T.compat, (uint32_t)h);
+    case CLDT_DELTA_BI: return quad_lookup(&T.deltabi, (uint32_t)h);
+    case CLDT_DISTINCT_BI: return quad_lookup(&T.distinctbi, (uint32_t)h);
+    case CLDT_QUAD: return quad_lookup(&T.quad, (uint32_t)h);
+    case CLDT_QUAD2: return quad_lookup(&T.quad2, (uint32_t)h);
+    case CLDT_DELTA_OCTA: return octa_lookup(&T.deltaocta, h);
+    case CLDT_DISTINCT_OCTA: return octa_lookup(&T.distinctocta, h);
+    default: return 0;
+  }
+}
+
 int cldo_lower(const char* in, int len, char* out, int olen) {
   return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen);
 }

@@ -50,6 +50,9 @@ int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* type
                       int n_chunks, uint32_t* ring, cldo_chunk* out);
 
 int cldo_lower(const char* in, int len, char* out, int olen);
+uint64_t cldo_gram_hash(int kind, const char* w, int n);   /* 0 quad, 1 bi, 2 octa */
+uint64_t cldo_pair_hash(uint64_t a, uint64_t b);
+uint32_t cldo_probe(int cldt_section, uint64_t hash);
 int cldo_script_num(const char* s);
 
 #ifdef __cplusplus
