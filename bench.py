@@ -1,16 +1,26 @@
 #!/usr/bin/env python3
-"""bench.py -- batched CLD2 DetectLanguage on MI355X (BASELINE.json metric).
+"""bench.py -- batched CLD2 DetectLanguage on MI355X (BASELINE.json metric:
+"docs/sec + input GB/s at 1/2/4/8 MI355X, 140B tweets and 16KB pages").
 
 A "step" is one pass of the hot path (DetectLanguageSummaryV2 per document,
 compact_lang_det_impl.cc:1707-2106) over one batch of synthetic documents that
-is already resident in HBM.  Default workload = BASELINE.json configs[1]
-(1M ~140-byte tweets on one MI355X); --config c3/c4/c5 selects the others.
+is already resident in HBM.  The headline is C2 (BASELINE.json configs[1]:
+1M ~140-byte tweets on one MI355X); the same run measures the metric's second
+half, C3 (configs[2]: 100K 16 KB pages), as the "c3" sub-object, and the
+host-memory path (cld_detect_batch: pinned staging, chunked upload / kernels /
+download on three streams) on C2 as "host_path".  --config c3/c4/c5 makes
+another config the headline instead.
 
 One process per GPU (torch.distributed, RCCL backend for the barrier and the
 max-over-ranks timing only -- the path itself has no collective): each rank
 scores its own shard of documents (weak scaling).  Rank 0 prints one JSON line.
 
+Tables: the synthetic Q1 quadgram table, opted into explicitly
+(CLD_MI355X_TABLES) so every quadgram branch does work; the library's own
+default is the empty Q0 table (the real quadchrome table is a missing blob).
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+                    [--no-sub] [--no-host] [--no-cpu-baseline]
 """
 import argparse
 import json
@@ -22,35 +32,64 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "language-detector_amd"))
+os.environ.setdefault("CLD_MI355X_TABLES", os.path.join(ROOT, "language-detector_amd", "data", "cld2_synth_q1.cldt"))
 
 CONFIGS = {
-    "c2": dict(docs=1_000_000, workload="C2: 1M synthetic tweets, U[100,180] B, 16 Latin-script languages "
-                                        "(BASELINE.json configs[1])"),
-    "c3": dict(docs=100_000, workload="C3: 100K synthetic 16 KB pages, Latin/Cyrillic/Arabic/Devanagari "
-                                      "paragraphs (configs[2])"),
-    "c4": dict(docs=1_000_000, workload="C4: 1M synthetic ~150 B zh/zh-Hant/ja/ko documents (configs[3])"),
-    "c5": dict(docs=1_000_000, workload="C5 shard: lognormal lengths (median 140 B, p99 ~16 KB, cap 64 KB), "
-                                        "mixed scripts (configs[4], one GPU's share)"),
+    "c2": dict(docs=1_000_000, steps=20, kernel=0, name="k_wave",
+               workload="C2: 1M synthetic tweets, U[100,180] B, 16 Latin-script languages (BASELINE.json configs[1])"),
+    "c3": dict(docs=100_000, steps=3, kernel=1, name="k_long",
+               workload="C3: 100K synthetic 16 KB pages, Latin/Cyrillic/Arabic/Devanagari paragraphs (configs[2])"),
+    "c4": dict(docs=1_100_000, steps=5, kernel=0, name="k_wave",
+               workload="C4: 1M ~150 B + 100K ~4 KB synthetic zh/zh-Hant/ja/ko documents (configs[3])"),
+    "c5": dict(docs=1_000_000, steps=5, kernel=1, name="k_long",
+               workload="C5 shard: lognormal lengths (median 140 B, p99 ~16 KB, cap 64 KB), mixed scripts "
+                        "(configs[4], one GPU's share)"),
 }
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 ALG_BYTES_PER_DOC = 8 + 40      # + document bytes: offset + result record
+# Issue ceilings (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 at 2.4 GHz; a wave64
+# VALU instruction issues over 2 cycles on its SIMD; one scalar unit per CU)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2      # wave-instructions / s
+SALU_PEAK = 256 * 2.4e9              # wave-instructions / s
+FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
 
 
-def cpu_baseline(cfg, buf, offs, gpu_out, seconds):
-    """Reference CPU restatement (oracle/) on the host cores, bounded sample.
-    Also checks the GPU results of that sample bit-for-bit (checker role)."""
+def host_cores():
+    """Cores this process may actually use: the affinity mask, capped by a
+    cgroup CPU quota (the GPU box grants a share of a bigger machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, os.cpu_count(), model
+
+
+def cpu_baseline(cfg, buf, offs, gpu_out, seconds, sample_docs):
+    """The oracle (oracle/cld_oracle.c, the C restatement) on the host cores,
+    bounded sample.  Also checks the GPU results of that sample bit-for-bit
+    (checker role)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import Oracle
     ob = Oracle()
-    threads = int(os.environ.get("CLD_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    cores, nproc, model = host_cores()
+    threads = int(os.environ.get("CLD_CPU_THREADS", cores))
     n = len(offs) - 1
-    sample = min(n, 200_000)
+    sample = min(n, sample_docs)
     o = offs[:sample + 1]
     b = buf[:int(o[-1])]
     ref = ob.detect_batch(b, o, threads=threads)            # warm + parity sample
-    same = True
-    for f in ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3"):
-        same &= bool(np.array_equal(ref[f], gpu_out[f][:sample]))
+    same = all(bool(np.array_equal(ref[f], gpu_out[f][:sample])) for f in FIELDS)
     docs, t0 = 0, time.perf_counter()
     while True:
         ob.detect_batch(b, o, threads=threads)
@@ -59,20 +98,133 @@ def cpu_baseline(cfg, buf, offs, gpu_out, seconds):
         if dt >= seconds:
             break
     return {"value": docs / dt, "unit": "docs/s", "cores": threads, "kind": "port",
-            "sample": "%d %s documents (%.1f MB), %d passes in %.1f s, oracle/cld_oracle.c x%d pthreads"
+            "input_GBps": docs / sample * float(o[-1]) / dt / 1e9,
+            "sample": "%d %s documents (%.1f MB), %d passes in %.1f s, oracle/cld_oracle.c x %d threads"
                       % (sample, cfg, o[-1] / 1e6, docs // sample, dt, threads),
+            "host": {"nproc": nproc, "usable_cores": cores, "cpu_model": model},
             "gpu_bit_exact_on_sample": same}
+
+
+def pmc_summary(cfg):
+    """Per-launch counters of the dominant kernel from the committed rocprofv3
+    PMC summary of this tree (profiles/pmc_current.json, tools/pmc_session.sh)."""
+    path = os.path.join(ROOT, "profiles", "pmc_current.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get(cfg)
+
+
+def measure(cfg_name, n, steps, warmup, rank, dist, dev):
+    import torch
+    import cld_amd
+    import corpus
+    cfg = CONFIGS[cfg_name]
+    buf, offs = corpus.GENERATORS[cfg_name](n, seed=corpus.SEEDS[cfg_name] + 7919 * rank)
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+
+    def step():
+        cld_amd.detect_batch_device(0, d_buf.data_ptr(), d_offs.data_ptr(), n, d_out.data_ptr(), None)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    cld_amd.kernel_times(0)                      # reset the event accumulator
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms, launches = cld_amd.kernel_times(0)
+    stats = cld_amd.last_stats(0)
+    per = [m / max(1, launches) for m in ms]
+    doc_bytes = int(offs[-1])
+    alg_bytes = doc_bytes + ALG_BYTES_PER_DOC * n
+    kern_ms = per[cfg["kernel"]]                 # the dominant kernel's average launch
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    pmc = pmc_summary(cfg_name)
+    traffic = issue = None
+    if pmc and pmc.get("docs") == n:
+        traffic = pmc.get("hbm_bytes_per_launch")
+        c = pmc.get("counters_per_launch", {})
+        if "SQ_INSTS_VALU" in c:
+            ks = kern_ms / 1e3
+            issue = {"valu": {"achieved": c["SQ_INSTS_VALU"] / ks, "peak": VALU_PEAK,
+                              "frac": c["SQ_INSTS_VALU"] / ks / VALU_PEAK},
+                     "salu": {"achieved": c["SQ_INSTS_SALU"] / ks, "peak": SALU_PEAK,
+                              "frac": c["SQ_INSTS_SALU"] / ks / SALU_PEAK},
+                     "unit": "wave-instructions/s",
+                     "active_inst_frac": pmc.get("frac_active_inst"), "wait_frac": pmc.get("frac_wait_any"),
+                     "source": "profiles/pmc_current.json (%s)" % pmc.get("source", "")}
+    res = {
+        "n": n, "elapsed": elapsed, "steps": steps, "doc_bytes": doc_bytes,
+        "value": n * steps / elapsed,
+        "input_GBps": doc_bytes * steps / elapsed / 1e9,
+        "passes_hist": [int(x) for x in stats.passes[:3]],
+        "kernels": {"wave_ms": per[0], "long_ms": per[1], "general_ms": per[2],
+                    "last_batch": {"wave_docs": int(stats.short_docs), "long_docs": int(stats.long_docs),
+                                   "general_docs": int(stats.general_docs),
+                                   "long_requeue_reasons": [int(x) for x in stats.long_requeue]}},
+        "roofline": {"bound": "hbm", "kernel": cfg["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes, "issue": issue},
+    }
+    gpu_out = d_out.cpu().numpy().view(cld_amd.RESULT_DTYPE) if rank == 0 else None
+    del d_buf, d_offs, d_out
+    return res, buf, offs, gpu_out
+
+
+def host_path(n, steps, rank):
+    """cld_detect_batch from host memory (C2): pageable numpy buffers (staged
+    through the runtime's pinned chunk buffers) and pinned ones
+    (cld_host_alloc: DMA'd directly).  docs/s including PCIe both ways."""
+    import cld_amd
+    import corpus
+    buf, offs = corpus.c2(n, seed=corpus.SEEDS["c2"] + 7919 * rank)
+    out = {}
+    pb = cld_amd.host_array(len(buf), np.uint8)
+    pb[:] = buf
+    po = cld_amd.host_array(len(offs), np.uint64)
+    po[:] = offs
+    pout = cld_amd.host_array(n, cld_amd.RESULT_DTYPE)
+    for kind, (b, o) in (("pageable", (buf, offs)), ("pinned", (pb, po))):
+        cld_amd.detect_batch(buf=b, offsets=o)                 # warm (staging buffers grow once)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            if kind == "pinned":
+                rc = cld_amd.lib().cld_detect_batch(b.ctypes.data, o.ctypes.data, n, pout.ctypes.data, 0)
+                assert rc == 0, rc
+            else:
+                cld_amd.detect_batch(buf=b, offsets=o)
+        dt = time.perf_counter() - t0
+        out[kind] = {"value": n * steps / dt, "unit": "docs/s", "ms_per_step": dt / steps * 1e3,
+                     "input_GBps": float(offs[-1]) * steps / dt / 1e9}
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps (default: per config)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--docs", type=int, default=0, help="documents per GPU (default: config size)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="skip the C3 sub-measurement of a C2 run")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-memory path measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -88,92 +240,63 @@ def main():
     dev = torch.device("cuda", local)
 
     import cld_amd
-    import corpus
     cld_amd.init_device(local)
 
     cfg = CONFIGS[args.config]
     n = args.docs or cfg["docs"]
-    buf, offs = corpus.GENERATORS[args.config](n, seed=corpus.SEEDS[args.config] + 7919 * rank)
-    d_buf = torch.from_numpy(buf).to(dev)
-    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    d_out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    steps = args.steps or cfg["steps"]
+    head, buf, offs, gpu_out = measure(args.config, n, steps, args.warmup, rank, dist, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, buf, offs, gpu_out, args.cpu_seconds,
+                           200_000 if args.config in ("c2", "c4") else 20_000)
+    del buf, offs, gpu_out
 
-    def step():
-        cld_amd.detect_batch_device(0, d_buf.data_ptr(), d_offs.data_ptr(), n, d_out.data_ptr(), None)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    cld_amd.kernel_time(0)                      # reset the event accumulator
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    short_ms, general_ms, launches = cld_amd.kernel_time(0)
-    stats = cld_amd.last_stats(0)
-    kernel_ms = (short_ms + general_ms) / max(1, launches)
-    doc_bytes = int(offs[-1])
-    alg_bytes = doc_bytes + ALG_BYTES_PER_DOC * n
-    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            p = json.load(f)
-        if p.get("docs") == n:
-            traffic = p.get("hbm_bytes_per_launch")
+    sub = None
+    if args.config == "c2" and not args.no_sub:
+        c3n = CONFIGS["c3"]["docs"] if not args.docs else max(1000, args.docs // 10)
+        r3, b3, o3, g3 = measure("c3", c3n, CONFIGS["c3"]["steps"], 1, rank, dist, dev)
+        sub = {"metric": "docs/sec", "value": r3["value"] * world, "unit": "docs/s",
+               "workload": CONFIGS["c3"]["workload"], "docs_per_gpu": c3n, "steps": r3["steps"],
+               "ms_per_step": r3["elapsed"] / r3["steps"] * 1e3, "input_GBps": r3["input_GBps"] * world,
+               "passes_hist": r3["passes_hist"], "kernels": r3["kernels"], "roofline": r3["roofline"],
+               "cpu_baseline": (cpu_baseline("c3", b3, o3, g3, args.cpu_seconds, 4_000)
+                                if rank == 0 and world == 1 and not args.no_cpu_baseline else None)}
+        del b3, o3, g3
+    host = None
+    if args.config == "c2" and not args.no_host and rank == 0:
+        host = host_path(n, 5, rank)
+        host["kernel_only_docs_per_s"] = head["value"]
+        host["pinned_vs_kernel_only"] = host["pinned"]["value"] / head["value"]
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-
-    gpu_out = d_out.cpu().numpy().view(cld_amd.RESULT_DTYPE)
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, buf, offs, gpu_out, args.cpu_seconds)
-
-    total_docs = n * world * args.steps
     line = {
         "metric": "docs/sec",
-        "value": total_docs / elapsed,
+        "value": head["value"] * world,
         "unit": "docs/s",
         "n_gpus": world,
-        "steps": args.steps,
+        "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head["elapsed"] / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded corpus.py; vocabularies from the reference's octa tables; "
-                "quadgram table synthetic -- the real one is a missing blob)",
-        "config": {"workload": cfg["workload"], "docs_per_gpu": n, "bytes_per_gpu": doc_bytes,
-                   "mean_doc_bytes": doc_bytes / n, "parallelism": "document shards, %d rank(s)" % world},
-        "input_GBps": doc_bytes * world * args.steps / elapsed / 1e9,
-        "passes_hist": [int(x) for x in stats.passes[:3]],
-        "kernels": {"wave_ms": short_ms / max(1, launches), "long_plus_general_ms": general_ms / max(1, launches),
-                    "last_batch": {"wave_ms": stats.short_ms, "long_ms": stats.long_ms, "general_ms": stats.general_ms,
-                                   "wave_docs": int(stats.short_docs), "long_docs": int(stats.long_docs),
-                                   "general_docs": int(stats.general_docs),
-                                   "long_requeue_reasons": [int(x) for x in stats.long_requeue]}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic},
+        "data": "synthetic (seeded corpus.py; vocabularies from the reference's octa tables; quadgram table: "
+                "the synthetic Q1 (the real quadchrome table is a missing blob))",
+        "config": {"workload": cfg["workload"], "docs_per_gpu": n, "bytes_per_gpu": head["doc_bytes"],
+                   "mean_doc_bytes": head["doc_bytes"] / n, "parallelism": "document shards, %d rank(s)" % world},
+        "input_GBps": head["input_GBps"] * world,
+        "passes_hist": head["passes_hist"],
+        "kernels": head["kernels"],
+        "roofline": head["roofline"],
         "cpu_baseline": cpu,
+        "c3": sub,
+        "host_path": host,
+        "tables": cld_amd.version(),
     }
     print(json.dumps(line), flush=True)
     if dist:

@@ -79,6 +79,12 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
  * short_ms = wavefront kernel; general_ms = long-document + sequential kernels. */
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
+/* Same accounting split per kernel stage: ms[0] the wavefront kernel (k_wave),
+ * ms[1] the long-document stage (length ordering + k_long), ms[2] the
+ * sequential kernel (k_general).  Sums since the previous call of either
+ * function; resets. */
+int cld_kernel_times(int ctx, double* ms3, int* launches);
+
 /* Diagnostics: per-stage shader-clock cycle sums on context `ctx` since the
  * previous call; 16 entries.  [0..7] short-document wavefront kernel (0 load,
  * 1 span, 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level);
@@ -95,7 +101,9 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * CLD2::DetectLanguage(buffer, length, ...)).  `out` is caller-allocated
  * (n entries).  Host buffers; not retained after return.  Blocks until the
  * results are in `out`.  Documents are sharded across the initialised GPUs
- * by byte count.  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING (above).
+ * by byte count; each shard streams through the GPU in chunks of <= 64 MB /
+ * 512K documents (pinned staging, upload / kernels / download overlapped on
+ * three streams).  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING (above).
  * Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
                      cld_result* out, uint32_t flags);
@@ -119,6 +127,14 @@ int cld_detect_batch_device_ex(int device, const uint8_t* d_buf, const uint64_t*
  * CLD_FLAG_CSTRING.  Blocks until the result is on the host. */
 int cld_prepare_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, uint32_t flags,
                       uint8_t* out_buf, uint64_t* out_offsets);
+
+/* Pinned host memory for callers of cld_detect_batch.  Documents, offsets and
+ * results that live in such memory skip the runtime's staging copy: they are
+ * DMA'd straight from/to it (the batch HTTP endpoint keeps its request and
+ * response buffers here).  Any other host memory works too and is staged
+ * through the runtime's own pinned chunk buffers.  NULL on failure. */
+void* cld_host_alloc(size_t bytes);
+void cld_host_free(void* p);
 
 /* LanguageCode / LanguageName (lang_script.cc:212-217, :205-210). */
 const char* cld_language_code(int lang);
@@ -168,7 +184,11 @@ int cld_is_data_dynamic(void);
 int cld_export_tables(const char* out_cldt_path);
 int cld_convert_data_file(const char* cld2_data_file, const char* base_cldt, const char* out_cldt_path);
 
-/* Build / table identity string ("cld-mi355x <ver> tables=<date> ..."). */
+/* Build / table identity string: "cld-mi355x <ver> tables=<path> quad=<q>
+ * quad_build=<date>" where q says which quadgram table is live: "empty-Q0"
+ * (the default: the reference's placeholder pattern, no quadgram scoring),
+ * "synthetic-Q1" (the test/bench table, opted into via CLD_MI355X_TABLES) or
+ * "other" (e.g. a real table from cld_load_data_from_file). */
 const char* cld_version(void);
 
 #ifdef __cplusplus

@@ -16,7 +16,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CLD_MI355X_LIB") or os.path.join(HERE, "build", "libcld_mi355x.so")
-TABLES = os.path.join(HERE, "data", "cld2_mi355x.cldt")
+# Product default: Q0, the empty quadgram table (cld_version() says "quad=empty-Q0").
+# Tests and the benchmark opt into the synthetic Q1 table through CLD_MI355X_TABLES.
+Q0_TABLES = os.path.join(HERE, "data", "cld2_q0.cldt")
+SYNTH_TABLES = os.path.join(HERE, "data", "cld2_synth_q1.cldt")
 FLAG_STRIP_EXTRAS = 1      # include/cld_mi355x.h CLD_FLAG_STRIP_EXTRAS
 FLAG_CSTRING = 2           # include/cld_mi355x.h CLD_FLAG_CSTRING
 
@@ -30,7 +33,8 @@ EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cl
            "cld_language_name", "cld_last_batch_stats", "cld_version", "cld_stage_cycles",
            "cld_load_data_from_file", "cld_load_data_from_raw_address", "cld_unload_data",
            "cld_is_data_dynamic", "cld_export_tables", "cld_convert_data_file",
-           "cld_detect_batch_device_ex", "cld_prepare_batch")
+           "cld_detect_batch_device_ex", "cld_prepare_batch", "cld_host_alloc", "cld_host_free",
+           "cld_kernel_times")
 
 
 class BatchStats(ctypes.Structure):
@@ -72,6 +76,7 @@ def lib():
         L.cld_plan_shards.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.cld_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+        L.cld_kernel_times.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
         L.cld_prepare_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
                                         ctypes.c_void_p, ctypes.c_void_p]
         L.cld_detect_batch_device_ex.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -80,6 +85,9 @@ def lib():
         L.cld_load_data_from_raw_address.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.cld_export_tables.argtypes = [ctypes.c_char_p]
         L.cld_convert_data_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.cld_host_alloc.argtypes = [ctypes.c_size_t]
+        L.cld_host_alloc.restype = ctypes.c_void_p
+        L.cld_host_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -155,6 +163,16 @@ def kernel_time(ctx=0):
     return a.value, b.value, n.value
 
 
+def kernel_times(ctx=0):
+    """([wave_ms, long_ms, general_ms], launches) summed over batches since the last call."""
+    ms = (ctypes.c_double * 3)()
+    n = ctypes.c_int()
+    rc = lib().cld_kernel_times(ctx, ms, ctypes.byref(n))
+    if rc != 0:
+        raise CldError("cld_kernel_times failed: %d" % rc)
+    return [ms[0], ms[1], ms[2]], n.value
+
+
 def stage_cycles(ctx=0):
     """Per-stage cycle sums of the wavefront kernel (CLD_PROFILE_STAGES=1)."""
     c = np.zeros(16, dtype=np.uint64)
@@ -209,6 +227,26 @@ def detect_language(text):
     """main.go:77-81 / wrapper.cc:7-16: NUL-terminated text -> ISO code ('en' for unknown)."""
     b = text.encode("utf-8") if isinstance(text, str) else bytes(text)
     return lib().detect_language(b).decode()
+
+
+def version():
+    return lib().cld_version().decode()
+
+
+def host_array(n, dtype):
+    """numpy array of n elements in pinned host memory (cld_host_alloc): a
+    cld_detect_batch on such buffers skips the staging copy.  The memory is
+    released with the array."""
+    dtype = np.dtype(dtype)
+    nbytes = max(1, n * dtype.itemsize)
+    p = lib().cld_host_alloc(nbytes)
+    if not p:
+        raise CldError("cld_host_alloc(%d) failed" % nbytes)
+    raw = (ctypes.c_uint8 * nbytes).from_address(p)
+    arr = np.frombuffer(raw, dtype=np.uint8)[:n * dtype.itemsize].view(dtype)
+    import weakref
+    weakref.finalize(raw, lib().cld_host_free, p)
+    return arr
 
 
 def language_code(lang):

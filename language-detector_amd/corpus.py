@@ -9,7 +9,8 @@ documents (unittest_data.h kTeststr_{zh_Hans,zh_Hant,ja_Hani,ko_Hani}).
       words, 5% digit/punctuation tokens                       
   c3  n x 16384 B pages: four ~4 KB paragraphs in Latin / Cyrillic / Arabic /
       Devanagari languages in random order                      
-  c4  n x ~150 B zh-Hans/zh-Hant/ja/ko documents                
+  c4  zh-Hans/zh-Hant/ja/ko documents: 10 of every 11 ~150 B, 1 in 11 ~4 KB
+      (1.1M docs = 1M x 150 B + 100K x 4 KB)                     
   c5  lognormal lengths (median 140 B, cap 64 KB) mixing c2..c4
 
 All generators are vectorised numpy and return (buf uint8[], offsets uint64[n+1]).
@@ -159,8 +160,34 @@ def cjk_pools():
     return _cjk
 
 
-def c4(n, seed=SEEDS["c4"], lo=120, hi=180):
-    """CJK 'words' are runs of 2-6 characters from the language's pool."""
+def _interleave(mask, a, b):
+    """Packed set a (rows where mask is False) and b (rows where True), in row order."""
+    (ba, oa), (bb, ob) = a, b
+    n = len(mask)
+    lens = np.zeros(n, dtype=np.int64)
+    lens[~mask] = np.diff(oa.astype(np.int64))
+    lens[mask] = np.diff(ob.astype(np.int64))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    out = np.empty(int(offs[-1]), dtype=np.uint8)
+    for m, (buf, o) in ((~mask, a), (mask, b)):
+        rows = np.nonzero(m)[0]
+        src_start = o[:-1].astype(np.int64)
+        l = lens[rows]
+        total = int(l.sum())
+        if total == 0:
+            continue
+        seg = np.zeros(len(rows), dtype=np.int64)
+        np.cumsum(l[:-1], out=seg[1:])
+        rel = np.arange(total, dtype=np.int64) - np.repeat(seg, l)
+        out[np.repeat(offs[rows].astype(np.int64), l) + rel] = buf[np.repeat(src_start, l) + rel]
+    return out, offs
+
+
+def c4(n, seed=SEEDS["c4"], lo=120, hi=180, long_every=11, long_lo=3800, long_hi=4300):
+    """CJK 'words' are runs of 2-6 characters from the language's pool; one
+    document in `long_every` (at seeded random positions) is ~4 KB, which
+    takes the long-document kernel's CJK rounds (SURVEY 8d C4's 100K x 4 KB)."""
     rng = np.random.default_rng(seed)
     pools = cjk_pools()
     words = {}
@@ -174,7 +201,16 @@ def c4(n, seed=SEEDS["c4"], lo=120, hi=180):
     table = WordTable(words)
     lang_idx = rng.integers(0, len(table.langs), size=n)
     targets = rng.integers(lo, hi + 1, size=n)
-    return _assemble(rng, table, lang_idx, targets, kmax=40, cap_frac=0.0, punct_frac=0.03)
+    nl = n // long_every if long_every else 0
+    long_mask = np.zeros(n, dtype=bool)
+    if nl:
+        long_mask[rng.choice(n, size=nl, replace=False)] = True
+    short = _assemble(rng, table, lang_idx[~long_mask], targets[~long_mask], kmax=40, cap_frac=0.0, punct_frac=0.03)
+    if not nl:
+        return short
+    lt = rng.integers(long_lo, long_hi + 1, size=nl)
+    longs = _assemble(rng, table, lang_idx[long_mask], lt, kmax=long_hi // 7 + 8, cap_frac=0.0, punct_frac=0.03)
+    return _interleave(long_mask, short, longs)
 
 
 def c5(n, seed=SEEDS["c5"], cap=65536):

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
 // round 1j's lane-parallel chunk summaries 8 wins (C3 100K pages: 6 -> 566K,
 // 7 -> 738K, 8 -> 754K docs/s; profiles/round1j_ab_long/).  9 does not fit.
 #ifndef LNG_WPS
-#define LNG_WPS 8
+#define LNG_WPS 4
 #endif
 template <int WPB, bool DIAG>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const uint8_t* __restrict__ buf,

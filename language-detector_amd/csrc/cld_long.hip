@@ -42,6 +42,7 @@ namespace lng {
 
 using wave::excl_scan;
 using wave::lower_char;
+using wave::lower_char_sm;
 using wave::lanemask_lt;
 using wave::rdl;
 using wave::rdl64;
@@ -63,6 +64,14 @@ constexpr int kHB = 1024;                            // hits per round (referenc
 constexpr int kEB = 2048;                            // base emissions per round (<= 2 per hit)
 constexpr int kMaxCh = 64;                           // chunks per round (<= 50 + 1)
 constexpr uint32_t kInf = 0xFFFFFFFFu;
+// A lowered span of up to kLdsText - 48 bytes (pads included) is scored from
+// LDS: the chain walk, the gram hashes and the word scans then read the text
+// at LDS latency instead of through the per-wave HBM slot.  Longer spans run
+// the same code on the slot copy.
+#ifndef LNG_TEXT
+#define LNG_TEXT 5632
+#endif
+constexpr int kLdsText = LNG_TEXT;
 
 // Per-wave working set in HBM (one per resident wavefront of the persistent grid).
 struct Slot {
@@ -72,9 +81,7 @@ struct Slot {
   uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
   uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats)
   uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces
-  uint32_t cls[kDocCap + 64];            // per document byte, see cls_* below
-  uint32_t low[kDocCap + 64];            // lowered bytes of the character starting here (<= 4)
-  uint8_t lb[2][kLB];                    // lowered span text; [1] = after CheapRepWords
+  alignas(16) uint8_t lb[2][kLB];        // lowered span text; [1] = after CheapRepWords
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
   uint16_t chain[kListCap];              // quad chain of the span
@@ -92,6 +99,7 @@ struct Slot {
 
 // Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4)
 struct alignas(16) Smem {
+  uint8_t text[kLdsText];                // the current span's lowered text when it fits (see kLdsText)
   uint32_t tote[256];                    // chunk tote, one key per word (uint16 wrap applied at read)
   int32_t theta[kMaxCh];                 // chunk k takes delta/distinct emissions with offset <= theta_k
   uint32_t lo[kMaxCh];                   // first offset of chunk k
@@ -205,8 +213,7 @@ __device__ int find_first_g(const uint64_t* m, int from, int L) {
 // A character cut by the end of the document (`cut`) runs out of input
 // instead: the scan ends there, and unless it is back in state 0 it backs up
 // to the lead byte (a stop), exactly as at :538-546.
-__device__ int scan_char(const DevTables& T, const DocView& d, int p, int n, bool cut) {
-  const DevSM& sm = T.scan;
+__device__ int scan_char_sm(const DevSM& sm, const DocView& d, int p, int n, bool cut) {
   const int64_t tb0 = sm.state0;
   int64_t tb = tb0;
   for (int k = 0; k < n; ++k) {
@@ -220,6 +227,9 @@ __device__ int scan_char(const DevTables& T, const DocView& d, int p, int n, boo
   }
   if (cut) return in_state_zero(sm, tb) ? (tb == tb0 ? 0 : -1) : 1;
   return tb == tb0 ? 0 : -1;
+}
+__device__ __forceinline__ int scan_char(const DevTables& T, const DocView& d, int p, int n, bool cut) {
+  return scan_char_sm(T.scan, d, p, n, cut);
 }
 
 // Character property table: for every well-formed 1-, 2- and 3-byte UTF-8
@@ -243,77 +253,99 @@ __device__ uint64_t cpt_eval(const DevTables& T, const uint8_t* b, int n) {
          ((uint64_t)(lowok ? olen : 0) << 11) | ((lowok ? (o & 0xFFFFFFFFull) : 0ull) << 32);
 }
 
-// Per character (lead byte): script number, script of the next character,
-// scanner stop, and the lowered bytes (LowerScriptSpan is per character once
-// each one starts and ends in state 0, checked by lower_char) -- all computed
-// once per document, so the span builder and the second pass only copy.
-// The 8 bytes a lane needs are loaded up front (one round trip), then one
-// property-table lookup per character.  False if the document does not tile
-// into characters with local scanner behaviour.
+// The rare characters the property table does not cover (4-byte or cut by
+// the document end): the three machines, out of line so their state does not
+// count against the span builder's registers.  The machines go by value (see
+// lower_tail).  -> sn | (int8)st << 8 | lowok << 16 | olen << 20 | lowered << 32
+__device__ __noinline__ uint64_t char_slow(DevSM script, DevSM scan, DevSM lower, DocView dv, int p, int n,
+                                           int avail) {
+  const int sn = script_num_sm(script, dv, p);
+  const int st = scan_char_sm(scan, dv, p, avail, avail < n);
+  uint64_t o = 0;
+  int olen = 0;
+  const bool lowok = avail == n && lower_char_sm(lower, dv.p + p, n, o, olen) && olen <= 4;
+  if (!lowok) { olen = 0; o = 0; }
+  return (uint64_t)(sn & 0xFF) | ((uint64_t)(uint8_t)(int8_t)st << 8) | ((uint64_t)lowok << 16) |
+         ((uint64_t)olen << 20) | ((o & 0xFFFFFFFFull) << 32);
+}
+
+// Per byte p of the document: the class word (cls_* above) and, for a lead
+// byte, the lowered bytes of its character (LowerScriptSpan is per character
+// once each one starts and ends in state 0, checked by lower_char).  The 8
+// bytes a lane needs are loaded up front (one round trip), then one
+// property-table lookup per character; 4-byte and cut characters run the
+// machines.  bad: the character breaks the local formulation; need/conts
+// count the continuation bytes the lead bytes claim / that are present.
+// Nothing is stored: classify() and the span builder both call this, so the
+// per-wave slot holds no per-byte state.
+__device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView& dv, int p, uint32_t& lw, int& bad,
+                                               int& need, int& conts) {
+  const int L = dv.len;
+  lw = 0;
+  if (p >= L) return 0u;
+  uint32_t b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = dv.at(p + k);
+  const uint32_t c = b[0];
+  if ((c & 0xC0) == 0x80) {
+    ++conts;
+    return 0u;
+  }
+  const int n = utf8_len((uint8_t)c);
+  const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
+  bool wf = true;
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+    if (k < avail) wf &= (b[k] & 0xC0) == 0x80;
+  bad |= !wf;
+  need += avail - 1;
+  int sn, st, olen = 0;
+  bool lowok;
+  if (avail == n && n <= 3) {
+    const uint64_t e = T.cpt[cpt_index(b[0], b[1], b[2], n)];
+    sn = (int)(e & 0xFF);
+    st = (int)((e >> 8) & 3);
+    if (st == 3) st = -1;
+    lowok = (e >> 10) & 1;
+    olen = (int)((e >> 11) & 15);
+    lw = (uint32_t)(e >> 32);
+  } else {                                   // 4-byte or cut: run the machines (out of line)
+    const uint64_t e = char_slow(T.script, T.scan, T.lower, dv, p, n, avail);
+    sn = (int)(e & 0xFF);
+    st = (int)(int8_t)((e >> 8) & 0xFF);
+    lowok = (e >> 16) & 1;
+    olen = (int)((e >> 20) & 15);
+    lw = (uint32_t)(e >> 32);
+  }
+  // script of the next character (its bytes are b[n..n+3]; NULs past the end)
+  int sn2;
+  const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
+  const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
+  const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
+  const int n2 = utf8_len((uint8_t)c2);
+  if (c2 < 0x80) sn2 = (int)(T.cpt[c2] & 0xFF);
+  else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) sn2 = (int)(T.cpt[cpt_index(c2, d1, 0, 2)] & 0xFF);
+  else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80)
+    sn2 = (int)(T.cpt[cpt_index(c2, d1, d2, 3)] & 0xFF);
+  else sn2 = script_num(T, dv, p + n);
+  if (st < 0) bad = 1;
+  const bool ls = st > 0 && sn != 0;
+  return (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
+         ((uint32_t)(avail < n) << 21) | ((uint32_t)!lowok << 22) | ((uint32_t)olen << 24);
+}
+
+// Validity of the per-character formulation over the whole document, and the
+// letter-stop bitmap (one bit per byte) the span builder searches for span
+// starts.  False if the document does not tile into characters with local
+// scanner behaviour (then k_general redoes it).
 __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lane) {
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
   const int nw = (L + 63) >> 6;
   for (int w = 0; w < nw; ++w) {
-    const int p = (w << 6) + lane;
-    bool ls = false;
-    uint32_t cw = 0, lw = 0;
-    if (p < L) {
-      uint32_t b[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b[k] = dv.at(p + k);
-      const uint32_t c = b[0];
-      if ((c & 0xC0) == 0x80) {
-        ++conts;
-      } else {
-        const int n = utf8_len((uint8_t)c);
-        const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
-        bool wf = true;
-#pragma unroll
-        for (int k = 1; k < 4; ++k)
-          if (k < avail) wf &= (b[k] & 0xC0) == 0x80;
-        bad |= !wf;
-        need += avail - 1;
-        int sn, st, olen = 0;
-        bool lowok;
-        if (avail == n && n <= 3) {
-          const uint64_t e = T.cpt[cpt_index(b[0], b[1], b[2], n)];
-          sn = (int)(e & 0xFF);
-          st = (int)((e >> 8) & 3);
-          if (st == 3) st = -1;
-          lowok = (e >> 10) & 1;
-          olen = (int)((e >> 11) & 15);
-          lw = (uint32_t)(e >> 32);
-        } else {                                   // 4-byte or cut: run the machines
-          sn = script_num(T, dv, p);
-          st = scan_char(T, dv, p, avail, avail < n);
-          uint64_t o = 0;
-          lowok = avail == n && lower_char(T, dv.p + p, n, o, olen) && olen <= 4;
-          if (!lowok) olen = 0;
-          lw = (uint32_t)o;
-        }
-        // script of the next character (its bytes are b[n..n+3]; NULs past the end)
-        int sn2;
-        const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
-        const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
-        const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
-        const int n2 = utf8_len((uint8_t)c2);
-        if (c2 < 0x80) sn2 = (int)(T.cpt[c2] & 0xFF);
-        else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) sn2 = (int)(T.cpt[cpt_index(c2, d1, 0, 2)] & 0xFF);
-        else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80)
-          sn2 = (int)(T.cpt[cpt_index(c2, d1, d2, 3)] & 0xFF);
-        else sn2 = script_num(T, dv, p + n);
-        if (st < 0) bad = 1;
-        ls = st > 0 && sn != 0;
-        cw = (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
-             ((uint32_t)(avail < n) << 21) | ((uint32_t)!lowok << 22) | ((uint32_t)olen << 24);
-      }
-    }
-    if (p < L) {
-      S.cls[p] = cw;
-      S.low[p] = lw;
-    }
-    const uint64_t m = __ballot(ls);
+    uint32_t lw;
+    const uint32_t cw = char_props(T, dv, (w << 6) + lane, lw, bad, need, conts);
+    const uint64_t m = __ballot((cw >> 20) & 1);
     if (lane == 0) S.lsm[w] = m;
   }
   bad |= (wsum(conts) != wsum(need)) ? 1 : 0;
@@ -359,16 +391,18 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     status = 0;
     return 0;
   }
-  const int ss = ufl(cls_sn(S.cls[q]));
+  int ignore = 0;
+  uint32_t lq;
+  const int ss = ufl(cls_sn(char_props(T, dv, q, lq, ignore, ignore, ignore)));
   ulscript = ss;
   if (lane == 0) lb[0] = ' ';
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
-    const bool valid = x >= q && x < L;
-    const uint32_t cw = valid ? S.cls[x] : 0u;
-    const uint32_t lw = valid ? S.low[x] : 0u;
+    int ignore = 0;
+    uint32_t lw = 0;
+    const uint32_t cw = x >= q ? char_props(T, dv, x, lw, ignore, ignore, ignore) : 0u;
     const bool lead = cls_lead(cw);
     const int n = cls_n(cw);
     bool brk = false, ok = false, foreign = false;
@@ -521,7 +555,7 @@ __device__ bool predict_window(uint64_t* tbl, uint32_t epoch, uint64_t lm, uint3
 // CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) on a lowered span
 // of more than 2048 bytes: >= 25% spaces or >= 67% predicted bytes in the first
 // 256 bytes (fresh table, hash 0).
-__device__ bool squeeze_trigger(Slot& S, const uint8_t* text, int lane) {
+__device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, int lane) {
   int sp = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) sp += text[lane * 4 + k] == ' ';
@@ -547,7 +581,7 @@ __device__ bool squeeze_trigger(Slot& S, const uint8_t* text, int lane) {
 // segment runs from a space (inclusive: its byte counts for the next word) to
 // the next space; at that space the bytes after the previous space, this space
 // included, are dropped if more than half of the segment was predicted.
-__device__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
+__device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
                          int lane) {
   const int nw = (len + 63) >> 6;
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
@@ -620,7 +654,7 @@ __device__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uin
 // at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
 // else mid (+1 on a vowel).  It never jumps over a space, so it enters every
 // word at its first byte and a word's entries depend on that word alone.
-__device__ bool word_lists(const uint8_t* text, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+__device__ __forceinline__ bool word_lists(const uint8_t* text, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
   nws = 0;
   nsp = 0;
   for (int w0 = start; w0 <= tb; w0 += 64) {
@@ -662,7 +696,7 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
   return cnt;
 }
 
-__device__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int lane) {
+__device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int lane) {
   int nch = 0;
   for (int i0 = 0; i0 < nws; i0 += 64) {
     const int i = i0 + lane;
@@ -684,7 +718,7 @@ __device__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int la
 // GetQuadHits for one round from chain entry c0 (cldutil.cc:315-405): probes
 // per entry, the "not one of the last two hits" filter, the 1000-hit cut.
 // Returns the round end (the reference's `next`); c0 advances.
-__device__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int nch, int& c0, int& nb,
+__device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int nch, int& c0, int& nb,
                           int lane) {
   nb = 0;
   uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
@@ -773,7 +807,7 @@ __device__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot&
 // GetOctaHits (cldutil.cc:416-533) over [off, next]: one lane per word (words
 // end at the spaces in [start, next]); the two-word repeat filter updates the
 // pair partner even when the probes miss; caps: 1000 delta / 999 distinct.
-__device__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int nsp, int& j0, int off, int next,
+__device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int nsp, int& j0, int off, int next,
                            int& nd, int& nx, int lane) {
   const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
   const int lim = next + 1;
@@ -877,7 +911,7 @@ __device__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int
 }
 
 // GetUniHits + GetBiHits (cldutil.cc:201-310) for one round from off.
-__device__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int off, int& nb, int& nd,
+__device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int off, int& nb, int& nd,
                          int& nx, int lane) {
   const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
   nb = 0;
@@ -1269,8 +1303,8 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
 template <bool D>
-__device__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb, int ulscript,
-                           int lane, uint32_t* tr, uint32_t doc) {
+__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb,
+                                           int ulscript, int lane, uint32_t* tr, uint32_t doc) {
   const int rt = rtype_of(T, ulscript);
   if (rt == RTypeNone || rt == RTypeOne) {
     if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
@@ -1360,21 +1394,42 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
       if constexpr (D) mark(s, lane, 1, t);
       if (st == 0) break;
       if (st < 0) return -kWhySpan;
-      const uint8_t* text = S.lb[0];
       if (pass == 1) {
-        if (tb > 2048 && squeeze_trigger(S, text, lane)) return -kWhySqueeze;   // Squeeze restart: k_general
+        if (tb > 2048 && squeeze_trigger(S, S.lb[0], lane)) return -kWhySqueeze;   // Squeeze restart: k_general
         if constexpr (D) mark(s, lane, 2, t);
+      }
+      bool ok;
+      if (tb + 48 <= kLdsText) {
+        // the span (and its pads) fits in LDS: 16 bytes per lane per step
+        const int n16 = (tb + 48 + 15) >> 4;
+        for (int i = lane; i < n16; i += 64)
+          reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(S.lb[0])[i];
+        wsync();
+        if (pass == 2) {
+          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, lane);   // in place, as the reference does
+          if constexpr (D) mark(s, lane, 3, t);
+        }
+        if constexpr (D) trace(tr, lane, doc, 5, tb);
+        if constexpr (D) {
+          const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
+          dbg_words(s, lane, v, 4);
+        }
+        ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc);
       } else {
-        tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, lane);
-        text = S.lb[1];
-        if constexpr (D) mark(s, lane, 3, t);
+        const uint8_t* text = S.lb[0];
+        if (pass == 2) {
+          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, lane);
+          text = S.lb[1];
+          if constexpr (D) mark(s, lane, 3, t);
+        }
+        if constexpr (D) trace(tr, lane, doc, 5, tb);
+        if constexpr (D) {
+          const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
+          dbg_words(s, lane, v, 4);
+        }
+        ok = score_span<D>(T, S, s, text, tb, ul, lane, tr, doc);
       }
-      if constexpr (D) trace(tr, lane, doc, 5, tb);
-      if constexpr (D) {
-        const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
-        dbg_words(s, lane, v, 4);
-      }
-      if (!score_span<D>(T, S, s, text, tb, ul, lane, tr, doc)) return -kWhyCapacity;
+      if (!ok) return -kWhyCapacity;
       t = (D && s.prof) ? (long long)clock64() : 0;
       total += tb;
     }

@@ -79,8 +79,7 @@ __device__ __forceinline__ int32_t sm8(const DevSM& sm, int64_t i) {
 // GetUTF8LetterScriptNum -> UTF8GenericPropertyTwoByte
 // getonescriptspan.cc:1083-1088, utf8statetable.cc:362-411
 template <class Src>
-__device__ int script_num(const DevTables& T, const Src& s, int i) {
-  const DevSM& sm = T.script;
+__device__ int script_num_sm(const DevSM& sm, const Src& s, int i) {
   uint8_t c = s.at(i);
   int64_t b = sm.state0;
   if (c < 0x80) return (int)(uint8_t)sm16(sm, b + c);
@@ -103,6 +102,8 @@ __device__ int script_num(const DevTables& T, const Src& s, int i) {
   }
   return (int)(uint8_t)e;
 }
+template <class Src>
+__device__ __forceinline__ int script_num(const DevTables& T, const Src& s, int i) { return script_num_sm(T.script, s, i); }
 
 // UTF8GenericPropertyBigOneByte on the CJK unigram machine, srclen =
 // kAdvanceOneChar[lead] (cldutil.cc:221-226, utf8statetable.cc:271-320)

@@ -48,6 +48,8 @@ struct HostTables {
   DevTables offs{};   // pointer fields hold byte offsets into blob
 };
 
+// Section `id` of a parsed blob; parse_tables has checked that every section
+// table entry lies inside the blob before any other reader runs.
 const uint8_t* section(const std::vector<uint8_t>& b, uint32_t id, uint64_t* off, uint64_t* size) {
   const cldt_file_header* fh = (const cldt_file_header*)b.data();
   const cldt_section* s = (const cldt_section*)(b.data() + fh->section_table_offset);
@@ -66,8 +68,9 @@ P at(uint64_t off) { return reinterpret_cast<P>((uintptr_t)off); }
 bool parse_sm(const std::vector<uint8_t>& b, uint32_t id, DevSM* sm) {
   uint64_t off, size;
   const uint8_t* p = section(b, id, &off, &size);
-  if (!p) return false;
+  if (!p || size < sizeof(cldt_sm_header)) return false;
   const cldt_sm_header* h = (const cldt_sm_header*)p;
+  if (h->bytes_per_entry != 1 && h->bytes_per_entry != 2) return false;
   sm->state0 = h->state0; sm->state0_size = h->state0_size; sm->total = h->total_size;
   sm->shift = h->entry_shift; sm->n_remap = h->n_remap; sm->n_rstr = h->n_remap_string;
   uint64_t tbl = off + sizeof(cldt_sm_header);
@@ -79,31 +82,45 @@ bool parse_sm(const std::vector<uint8_t>& b, uint32_t id, DevSM* sm) {
   uint64_t r = (sizeof(cldt_sm_header) + (uint64_t)h->total_size * h->bytes_per_entry + 15) & ~15ull;
   sm->remap = at<const uint8_t*>(off + r);
   sm->rstr = at<const uint8_t*>(off + r + 4ull * h->n_remap);
-  return true;
+  // every table entry, remap entry and remap byte the machines can index lies inside the section
+  // (the device bounds each table read by `total`)
+  const uint64_t need = h->bytes_per_entry == 2 ? sizeof(cldt_sm_header) + 2ull * h->total_size
+                                                : r + 4ull * h->n_remap + h->n_remap_string;
+  return need <= size && h->state0 < h->total_size;
 }
 
 bool parse_tbl(const std::vector<uint8_t>& b, uint32_t id, DevTbl* t) {
-  uint64_t off;
-  const uint8_t* p = section(b, id, &off, nullptr);
-  if (!p) return false;
+  uint64_t off, size;
+  const uint8_t* p = section(b, id, &off, &size);
+  if (!p || size < sizeof(cldt_table_header)) return false;
   const cldt_table_header* h = (const cldt_table_header*)p;
   t->size_one = h->size_one; t->size = h->size; t->key_mask = h->key_mask;
   t->n_ind = h->n_ind; t->n_buckets = h->n_buckets_stored;
   uint64_t bo = off + sizeof(cldt_table_header);
   t->b = at<const uint32_t*>(bo);
   t->ind = at<const uint32_t*>(bo + 16ull * h->n_buckets_stored);
-  // buckets are read as one 16-byte vector: they must be 16-byte aligned
-  return (bo % 16) == 0 && (h->size == 0 || (h->size & (h->size - 1)) == 0);
+  // buckets are read as one 16-byte vector: they must be 16-byte aligned; the
+  // subscript is masked with size-1, so every such bucket must be stored; the
+  // indirect reads are bounded by n_ind on the device
+  return (bo % 16) == 0 && (h->size == 0 || (h->size & (h->size - 1)) == 0) &&
+         h->size <= h->n_buckets_stored &&
+         sizeof(cldt_table_header) + 16ull * h->n_buckets_stored + 4ull * h->n_ind <= size;
 }
 
 std::vector<std::string> strings(const std::vector<uint8_t>& b, uint32_t id) {
   std::vector<std::string> out;
-  const uint8_t* p = section(b, id, nullptr, nullptr);
-  if (!p) return out;
+  uint64_t size = 0;
+  const uint8_t* p = section(b, id, nullptr, &size);
+  if (!p || size < 4) return out;
   uint32_t n = *(const uint32_t*)p;
+  if (4ull * (n + 2) > size) return out;
   const uint32_t* o = (const uint32_t*)(p + 4);
   const char* base = (const char*)(p + 4 + 4 * (n + 1));
-  for (uint32_t i = 0; i < n; ++i) out.emplace_back(base + o[i]);
+  const uint64_t avail = size - 4ull * (n + 2);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (o[i] >= avail) return std::vector<std::string>();
+    out.emplace_back(base + o[i], strnlen(base + o[i], avail - o[i]));
+  }
   return out;
 }
 
@@ -125,11 +142,18 @@ int parse_tables(HostTables* t, const std::string& label) {
   const long n = (long)t->blob.size();
   if (n < (long)sizeof(cldt_file_header)) return CLD_EINVAL;
   const cldt_file_header* fh = (const cldt_file_header*)t->blob.data();
-  if (fh->magic != CLDT_MAGIC || fh->version != CLDT_VERSION ||
+  if (fh->magic != CLDT_MAGIC || fh->version != CLDT_VERSION || fh->n_sections > 4096 ||
       fh->section_table_offset + (uint64_t)fh->n_sections * sizeof(cldt_section) > (uint64_t)n)
     return CLD_EINVAL;
-  const uint8_t* m = section(t->blob, CLDT_META, nullptr, nullptr);
-  if (!m) return CLD_EINVAL;
+  {  // every section lies inside the blob and is 4-byte aligned (the tables are read as u16/u32/u64)
+    const cldt_section* sec = (const cldt_section*)(t->blob.data() + fh->section_table_offset);
+    for (uint32_t i = 0; i < fh->n_sections; ++i)
+      if (sec[i].offset > (uint64_t)n || sec[i].size > (uint64_t)n - sec[i].offset || sec[i].offset % 4)
+        return CLD_EINVAL;
+  }
+  uint64_t msize = 0;
+  const uint8_t* m = section(t->blob, CLDT_META, nullptr, &msize);
+  if (!m || msize < sizeof(t->meta)) return CLD_EINVAL;
   memcpy(&t->meta, m, sizeof(t->meta));
   DevTables& D = t->offs;
   bool ok = parse_sm(t->blob, CLDT_SCRIPT_PROP, &D.script) && parse_sm(t->blob, CLDT_LOWER_REPL, &D.lower) &&
@@ -156,6 +180,12 @@ int parse_tables(HostTables* t, const std::string& label) {
     *s.dst = at<const void*>(off);
     if (s.count) *s.count = (uint32_t)(size / s.elem);
   }
+  {  // fixed-size maps indexed by a byte (per-script numbers, kLgProbV2Tbl rows) or by script
+    auto sz = [&](uint32_t id) { uint64_t z = 0; section(t->blob, id, nullptr, &z); return z; };
+    if (sz(CLDT_PLANG_TO_LANG_LATN) < 512 || sz(CLDT_PLANG_TO_LANG_OTHR) < 512 || sz(CLDT_LGPROB) < 240 * 8 ||
+        sz(CLDT_ULSCRIPT_DEFAULT_LANG) < 2ull * D.n_scripts || D.n_scripts == 0 || D.n_langs == 0)
+      return CLD_EINVAL;
+  }
   {  // the wavefront kernel's packed tote relies on small score bytes (kMaxLgProbScore)
     if (!section(t->blob, CLDT_LGPROB, &off, &size) || size % 8 || off % 4) return CLD_EINVAL;
     for (uint64_t r = 0; r < size; r += 8)
@@ -174,7 +204,16 @@ int parse_tables(HostTables* t, const std::string& label) {
   t->codes = strings(t->blob, CLDT_LANG_CODES);
   t->names = strings(t->blob, CLDT_LANG_NAMES);
   const cldt_table_header* q = (const cldt_table_header*)section(t->blob, CLDT_QUAD, nullptr, nullptr);
-  t->version = "cld-mi355x 1.0 tables=" + label + " quad_build=" + std::to_string(q->build_date);
+  // which quadgram table is live: the empty placeholder (Q0, what the reference
+  // itself can run without the missing quadchrome blob), the synthetic Q1 test
+  // table, or one imported from a cld2 data file / other CLDT
+  std::string quad = "other";
+  uint64_t psize = 0;
+  const uint8_t* prov = section(t->blob, CLDT_PROVENANCE, nullptr, &psize);
+  const std::string pv = prov ? std::string((const char*)prov, psize) : std::string();
+  if (D.quad.n_buckets <= 1 && D.quad.n_ind <= 1 && D.quad2.size == 0) quad = "empty-Q0";
+  else if (pv.find("SYNTHETIC") != std::string::npos) quad = "synthetic-Q1";
+  t->version = "cld-mi355x 2.0 tables=" + label + " quad=" + quad + " quad_build=" + std::to_string(q->build_date);
   return CLD_OK;
 }
 
@@ -244,6 +283,28 @@ struct Device {
   cld_batch_stats last{};
   uint64_t last_n = 0;
   bool stats_pending = false;
+  // Every batch on this device reuses the scratch above (counters, re-queue
+  // lists, k_long slots, staging).  `done` is recorded after a batch's last
+  // launch and every enqueue makes its stream wait on it first, so batches on
+  // different caller streams (or the runtime's own) execute one after another.
+  hipEvent_t done = nullptr;
+  // Streamed host path (run_host_shard): two chunk slots, each with pinned
+  // staging and device buffers; uploads, kernels and downloads on three
+  // streams so chunk k+1's upload and chunk k-1's download overlap chunk k.
+  struct Slot {
+    uint8_t* h_in = nullptr; size_t h_in_cap = 0;        // pinned: document bytes
+    uint64_t* h_offs = nullptr; size_t h_offs_cap = 0;   // pinned: offsets (caller's, not rebased)
+    cld_result* h_out = nullptr; size_t h_out_cap = 0;   // pinned: results
+    uint8_t* d_in = nullptr; size_t d_in_cap = 0;
+    uint64_t* d_offs = nullptr; size_t d_offs_cap = 0;
+    cld_result* d_out = nullptr; size_t d_out_cap = 0;
+    hipEvent_t up = nullptr, comp = nullptr, down = nullptr;
+    size_t pending_n = 0; cld_result* pending_dst = nullptr;   // results to hand over once `down` fires
+    bool busy = false;
+  } hs[2];
+  hipStream_t up_stream = nullptr, down_stream = nullptr;
+  uint32_t* h_ctr = nullptr;        // pinned: per-chunk counter snapshots (kCtrSlots each)
+  size_t h_ctr_cap = 0;
   std::mutex mu;
 };
 
@@ -255,15 +316,19 @@ std::vector<Device*> g_devs;
 bool g_dynamic = false;       // g_tab came from a cld2 dynamic data file (cld_load_data_*)
 std::string g_base_path;      // the CLDT the static tables were read from
 
+// The product default is Q0, the empty quadgram table (the reference's own
+// placeholder pattern): out of the box no answer comes from fabricated quad
+// data.  Tests and the benchmark opt into the synthetic Q1 table explicitly
+// (CLD_MI355X_TABLES), and a real table arrives through cld_load_data_*.
 std::string default_tables_path() {
   if (const char* e = getenv("CLD_MI355X_TABLES")) return e;
   Dl_info info;
   if (dladdr((void*)&default_tables_path, &info) && info.dli_fname) {
     std::string so = info.dli_fname;
     std::string dir = so.substr(0, so.find_last_of('/'));
-    return dir + "/../data/cld2_mi355x.cldt";
+    return dir + "/../data/cld2_q0.cldt";
   }
-  return "language-detector_amd/data/cld2_mi355x.cldt";
+  return "language-detector_amd/data/cld2_q0.cldt";
 }
 
 template <class T>
@@ -277,31 +342,70 @@ int grow(T** p, size_t* cap, size_t need) {
   return CLD_OK;
 }
 
-// Table blob -> HBM (once per GPU, and again when dynamic data replaces the tables).
-// The caller holds d->mu or owns d exclusively; the stream is drained first.
-int upload_tables(Device* d, const HostTables& t) {
-  HIP_OK(hipSetDevice(d->id));
-  HIP_OK(hipDeviceSynchronize());   // batches enqueued on caller streams may still read the old blob
+// Table blob -> HBM (once per GPU, and again when dynamic data replaces the
+// tables), in two steps so a multi-GPU swap is all-or-nothing: stage_tables
+// allocates and fills a new copy (the old one stays live), then commit_tables
+// drains the device and swaps it in, or discard_tables frees it.
+struct StagedTables {
   uint8_t* blob = nullptr;
   uint64_t* cpt = nullptr;
-  HIP_OK(hipMalloc(&blob, t.blob.size()));
-  HIP_OK(hipMemcpy(blob, t.blob.data(), t.blob.size(), hipMemcpyHostToDevice));
-  DevTables T = device_tables(t.offs, blob);
+  DevTables T{};
+};
+
+int stage_tables(Device* d, const HostTables& t, StagedTables* st) {
+  HIP_OK(hipSetDevice(d->id));
+  HIP_OK(hipMalloc(&st->blob, t.blob.size()));
+  HIP_OK(hipMemcpy(st->blob, t.blob.data(), t.blob.size(), hipMemcpyHostToDevice));
+  st->T = device_tables(t.offs, st->blob);
   // per-character property table for the long-document kernel, built from the uploaded machines
-  HIP_OK(hipMalloc(&cpt, cld_cpt_entries() * sizeof(uint64_t)));
-  HIP_OK(cld_build_cpt(&T, cpt, d->stream));
+  HIP_OK(hipMalloc(&st->cpt, cld_cpt_entries() * sizeof(uint64_t)));
+  HIP_OK(cld_build_cpt(&st->T, st->cpt, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
-  T.cpt = cpt;
-  if (d->d_blob) (void)hipFree(d->d_blob);
-  if (d->T.cpt) (void)hipFree((void*)d->T.cpt);
-  d->d_blob = blob;
-  d->T = T;
+  st->T.cpt = st->cpt;
   return CLD_OK;
 }
+
+void discard_tables(Device* d, StagedTables* st) {
+  (void)hipSetDevice(d->id);
+  if (st->blob) (void)hipFree(st->blob);
+  if (st->cpt) (void)hipFree(st->cpt);
+  *st = StagedTables();
+}
+
+// The caller holds d->mu or owns d exclusively.
+int commit_tables(Device* d, StagedTables* st) {
+  HIP_OK(hipSetDevice(d->id));
+  HIP_OK(hipDeviceSynchronize());   // batches enqueued on caller streams may still read the old blob
+  if (d->d_blob) (void)hipFree(d->d_blob);
+  if (d->T.cpt) (void)hipFree((void*)d->T.cpt);
+  d->d_blob = st->blob;
+  d->T = st->T;
+  *st = StagedTables();
+  return CLD_OK;
+}
+
+int upload_tables(Device* d, const HostTables& t) {
+  StagedTables st;
+  int rc = stage_tables(d, t, &st);
+  if (rc) { discard_tables(d, &st); return rc; }
+  return commit_tables(d, &st);
+}
+
+// Replace the tables on every initialised GPU, or on none.  Caller holds g_init_mu.
+int swap_tables_all(const HostTables& nt);
 
 int init_device(Device* d) {
   HIP_OK(hipSetDevice(d->id));
   HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&d->up_stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&d->down_stream, hipStreamNonBlocking));
+  HIP_OK(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(d->done, d->stream));
+  for (auto& h : d->hs) {
+    HIP_OK(hipEventCreateWithFlags(&h.up, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&h.comp, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&h.down, hipEventDisableTiming));
+  }
   if (int rc = upload_tables(d, g_tab)) return rc;
   HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&d->d_lhist, 256 * sizeof(uint32_t)));
@@ -355,6 +459,7 @@ constexpr uint32_t kPrepFlags = CLD_FLAG_STRIP_EXTRAS | CLD_FLAG_CSTRING;
 // prepared documents in d->d_sbuf / d->d_soffs.  cap_bytes bounds offs[n].
 int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, uint64_t cap_bytes,
                     uint32_t flags, hipStream_t s) {
+  HIP_OK(hipStreamWaitEvent(s, d->done, 0));   // the previous batch may still read d_sbuf
   if (grow(&d->d_sbuf, &d->sbuf_cap, std::max<size_t>(cap_bytes + n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_soffs, &d->soffs_cap, n + 1)) return CLD_ENOMEM;
   if (grow(&d->d_sscr, &d->sscr_cap, cld_strip_scratch_bytes((int)n))) return CLD_ENOMEM;
@@ -377,6 +482,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     d->ev_pool.push_back(t);
   }
   auto& ev = d->ev_pool[d->ev_used++];
+  HIP_OK(hipStreamWaitEvent(s, d->done, 0));   // serialise with the previous batch's scratch use
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
   if (d->d_dbg) HIP_OK(hipMemsetAsync(d->d_dbg, 0, 4, s));
   HIP_OK(hipEventRecord(ev[0], s));
@@ -403,33 +509,44 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
                               d->d_counters, kCtrRequeue, kCtrDequeue, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
+  HIP_OK(hipEventRecord(d->done, s));
   for (int k = 0; k < 4; ++k) d->ev[k] = ev[k];
   d->last_n = n;
   d->stats_pending = true;
   return CLD_OK;
 }
 
+// Adds one batch's device counters to st (docs = documents of that batch).
+void add_counters(Device* d, const uint32_t* c, uint64_t docs, cld_batch_stats* st) {
+  const uint32_t to_general = d->n_slots > 0 ? c[kCtrRequeue2] : c[kCtrRequeue];
+  st->docs += docs;
+  st->general_docs += to_general;
+  st->long_docs += c[kCtrRequeue] - to_general;
+  st->short_docs += docs - c[kCtrRequeue];
+  st->passes[0] += (docs - c[kCtrRequeue]) + c[kCtrPass1];
+  st->passes[1] += c[kCtrPass2];
+  st->passes[2] += c[kCtrPass3];
+  st->passes[3] += c[kCtrError];
+  for (int k = 0; k < 8; ++k) st->long_requeue[k] += c[kCtrWhy + k];
+}
+
 int collect_stats(Device* d) {
   if (!d->stats_pending) return CLD_OK;
   uint32_t c[kCtrSlots];
+  // the batch may have run on a caller's stream: wait for its last event, then
+  // read the counters before any later batch can reset them (the runtime
+  // stream waits on `done`, which a later enqueue re-records only after this)
+  HIP_OK(hipEventSynchronize(d->ev[3]));
+  HIP_OK(hipStreamWaitEvent(d->stream, d->ev[3], 0));
   HIP_OK(hipMemcpyAsync(c, d->d_counters, sizeof(c), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   float ms1 = 0, ms2 = 0, ms3 = 0;
-  (void)hipEventElapsedTime(&ms1, d->ev[0], d->ev[1]);
-  (void)hipEventElapsedTime(&ms2, d->ev[1], d->ev[2]);
-  (void)hipEventElapsedTime(&ms3, d->ev[2], d->ev[3]);
+  HIP_OK(hipEventElapsedTime(&ms1, d->ev[0], d->ev[1]));
+  HIP_OK(hipEventElapsedTime(&ms2, d->ev[1], d->ev[2]));
+  HIP_OK(hipEventElapsedTime(&ms3, d->ev[2], d->ev[3]));
   cld_batch_stats& st = d->last;
   memset(&st, 0, sizeof(st));
-  st.docs = d->last_n;
-  const uint32_t to_general = d->n_slots > 0 ? c[kCtrRequeue2] : c[kCtrRequeue];
-  st.general_docs = to_general;
-  st.long_docs = c[kCtrRequeue] - to_general;
-  st.short_docs = d->last_n - c[kCtrRequeue];
-  st.passes[0] = st.short_docs + c[kCtrPass1];
-  st.passes[1] = c[kCtrPass2];
-  st.passes[2] = c[kCtrPass3];
-  st.passes[3] = c[kCtrError];
-  for (int k = 0; k < 8; ++k) st.long_requeue[k] = c[kCtrWhy + k];
+  add_counters(d, c, d->last_n, &st);
   st.short_ms = ms1;
   st.long_ms = ms2;
   st.general_ms = ms3;
@@ -437,73 +554,163 @@ int collect_stats(Device* d) {
   return c[kCtrError] ? CLD_EIO : CLD_OK;
 }
 
-// Host batch on one device: H2D, kernels, D2H.
+// Debug (CLD_TRACE=1): a batch that overruns dumps where every k_long wave is.
+void watch_trace(Device* d, hipStream_t s) {
+  auto t0 = std::chrono::steady_clock::now();
+  while (hipStreamQuery(s) == hipErrorNotReady) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el <= d->trace_timeout) continue;
+    fprintf(stderr, "cld_mi355x: batch still running after %.0f s; k_long waves (doc stage value count):\n", el);
+    int untouched = 0, exited = 0;
+    for (int w = 0; w < d->n_slots; ++w) {
+      volatile uint32_t* t = d->h_trace + 4 * w;
+      untouched += t[3] == 0xFFFFFFFFu;
+      exited += (t[1] & 0xFFFF) == 100;
+    }
+    fprintf(stderr, "  %d waves: %d never started, %d exited\n", d->n_slots, untouched, exited);
+    for (int w = 0; w < d->n_slots; ++w) {
+      volatile uint32_t* t = d->h_trace + 4 * w;
+      if (t[3] != 0xFFFFFFFFu && ((t[1] & 0xFFFF) != 100 || w < 2))
+        fprintf(stderr, "  wave %d: doc %u stage %u (active lanes %u, first %u) value %u count %u\n", w, t[0],
+                t[1] & 0xFFFF, (t[1] >> 16) & 0xFF, t[1] >> 24, t[2], t[3]);
+    }
+    fflush(stderr);
+    abort();
+  }
+}
+
+// Chunking of the streamed host path: a chunk is at most kChunkBytes of
+// document text and kChunkDocs documents, so two chunks in flight stay small
+// next to HBM while each is still a full-chip launch.
+constexpr uint64_t kChunkBytes = 64ull << 20;
+constexpr size_t kChunkDocs = 512 * 1024;
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();   // unregistered pageable memory reports an error: clear it
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+template <class T>
+int grow_host(T** p, size_t* cap, size_t need) {
+  if (*cap >= need) return CLD_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  size_t n = std::max(need, *cap * 3 / 2);
+  if (hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) { *cap = 0; return CLD_ENOMEM; }
+  *cap = n;
+  return CLD_OK;
+}
+
+// memcpy split over a few host threads: staging into pinned memory runs on the
+// CPU while the GPU works on the previous chunk, and one core copies ~10 GB/s.
+void par_copy(void* dst, const void* src, size_t n) {
+  const size_t kPiece = 8u << 20;
+  const int t = (int)std::min<size_t>(8, (n + kPiece - 1) / kPiece);
+  if (t <= 1) { memcpy(dst, src, n); return; }
+  std::vector<std::thread> th;
+  const size_t per = (n + t - 1) / t;
+  for (int i = 1; i < t; ++i) {
+    const size_t a = per * i, b = std::min(n, a + per);
+    if (a < b) th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
+  }
+  memcpy(dst, src, std::min(n, per));
+  for (auto& x : th) x.join();
+}
+
+// Host batch on one device, streamed: documents go in chunks through two
+// slots.  Per chunk: stage into pinned memory (skipped when the caller's
+// buffers are already pinned), upload on up_stream, the kernels on the
+// runtime stream, results back on down_stream.  Offsets are uploaded as the
+// caller wrote them and the kernels get `d_in - offs[first]` as their buffer
+// base, so no rebasing pass runs anywhere.  Chunk k's staging overlaps chunk
+// k-1's kernels; its upload overlaps them too.
 int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
-  const uint64_t base = offs[0], bytes = offs[n] - offs[0];
-  if (grow(&d->d_buf, &d->buf_cap, std::max<size_t>(bytes, 1))) return CLD_ENOMEM;
-  if (grow(&d->d_offs, &d->offs_cap, n + 1)) return CLD_ENOMEM;
-  if (grow(&d->d_out, &d->out_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
-  std::vector<uint64_t> rel(n + 1);
-  for (size_t i = 0; i <= n; ++i) rel[i] = offs[i] - base;
-  if (bytes) HIP_OK(hipMemcpyAsync(d->d_buf, buf + base, bytes, hipMemcpyHostToDevice, d->stream));
-  HIP_OK(hipMemcpyAsync(d->d_offs, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
-  int rc;
-  if (flags & kPrepFlags) {
-    if ((rc = enqueue_prepare(d, d->d_buf, d->d_offs, n, bytes, flags, d->stream))) return rc;
-    rc = enqueue(d, d->d_sbuf, d->d_soffs, n, d->d_out, d->stream);
-  } else {
-    rc = enqueue(d, d->d_buf, d->d_offs, n, d->d_out, d->stream);
-  }
-  if (rc) return rc;
-  if (d->h_trace) {           // debug: a batch that overruns dumps where every k_long wave is
-                              // (polled before the D2H copy: a pageable copy blocks the host)
-    auto t0 = std::chrono::steady_clock::now();
-    while (hipStreamQuery(d->stream) == hipErrorNotReady) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > d->trace_timeout) {
-        fprintf(stderr, "cld_mi355x: batch still running after %.0f s; k_long waves (doc stage value count):\n", el);
-        {
-          int untouched = 0, exited = 0;
-          for (int w = 0; w < d->n_slots; ++w) {
-            volatile uint32_t* t = d->h_trace + 4 * w;
-            untouched += t[3] == 0xFFFFFFFFu;
-            exited += (t[1] & 0xFFFF) == 100;
-          }
-          fprintf(stderr, "  %d waves: %d never started, %d exited; events: %d\n", d->n_slots, untouched, exited,
-                  (int)hipEventQuery(d->ev[1]) * 10 + (int)hipEventQuery(d->ev[2]));
-        }
-        for (int w = 0; w < d->n_slots; ++w) {
-          volatile uint32_t* t = d->h_trace + 4 * w;
-          if (t[3] != 0xFFFFFFFFu && ((t[1] & 0xFFFF) != 100 || w < 2))
-            fprintf(stderr, "  wave %d: doc %u stage %u (active lanes %u, first %u) value %u count %u\n", w, t[0],
-                    t[1] & 0xFFFF, (t[1] >> 16) & 0xFF, t[1] >> 24, t[2], t[3]);
-        }
-        hipStream_t s2;                       // the counters, through a second stream
-        uint32_t* hc = nullptr;
-        if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess &&
-            hipHostMalloc((void**)&hc, kCtrSlots * 4, hipHostMallocCoherent) == hipSuccess &&
-            hipMemcpyAsync(hc, d->d_counters, kCtrSlots * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) {
-          for (int k = 0; k < 200 && hipStreamQuery(s2) == hipErrorNotReady; ++k)
-            std::this_thread::sleep_for(std::chrono::milliseconds(10));
-          if (hipStreamQuery(s2) == hipSuccess) {
-            fprintf(stderr, "  counters:");
-            for (int k = 0; k < 8; ++k) fprintf(stderr, " %u", hc[k]);
-            fprintf(stderr, "\n");
-          } else {
-            fprintf(stderr, "  counters: copy did not complete\n");
-          }
-        }
-        fflush(stderr);
-        abort();
-      }
+  const bool in_pinned = host_pinned(buf + offs[0]) && host_pinned(offs);
+  const bool out_pinned = host_pinned(out);
+  // chunk plan
+  std::vector<size_t> cut{0};
+  while (cut.back() < n) {
+    const size_t a = cut.back();
+    size_t lo = a + 1, hi = std::min(n, a + kChunkDocs);     // largest b <= hi with bytes <= kChunkBytes (>= 1 doc)
+    while (lo < hi) {
+      const size_t mid = (lo + hi + 1) / 2;
+      if (offs[mid] - offs[a] <= kChunkBytes) lo = mid; else hi = mid - 1;
     }
+    cut.push_back(lo);
   }
-  HIP_OK(hipMemcpyAsync(out, d->d_out, n * sizeof(cld_result), hipMemcpyDeviceToHost, d->stream));
+  const size_t nch = cut.size() - 1;
+  if (grow_host(&d->h_ctr, &d->h_ctr_cap, nch * kCtrSlots)) return CLD_ENOMEM;
+  int rc = CLD_OK;
+  auto deliver = [&](Device::Slot& h) -> int {
+    if (!h.busy) return CLD_OK;
+    HIP_OK(hipEventSynchronize(h.down));
+    if (h.pending_dst && h.pending_dst != h.h_out) par_copy(h.pending_dst, h.h_out, h.pending_n * sizeof(cld_result));
+    h.busy = false;
+    return CLD_OK;
+  };
+  for (size_t c = 0; c < nch && rc == CLD_OK; ++c) {
+    Device::Slot& h = d->hs[c & 1];
+    if ((rc = deliver(h))) break;                      // chunk c-2: its results, and its buffers free
+    const size_t a = cut[c], m = cut[c + 1] - a;
+    const uint64_t base = offs[a], bytes = offs[a + m] - base;
+    if ((rc = grow(&h.d_in, &h.d_in_cap, std::max<size_t>(bytes, 1))) ||
+        (rc = grow(&h.d_offs, &h.d_offs_cap, m + 1)) || (rc = grow(&h.d_out, &h.d_out_cap, m)))
+      break;
+    const uint8_t* src_in = buf + base;
+    const uint64_t* src_offs = offs + a;
+    if (!in_pinned) {
+      if ((rc = grow_host(&h.h_in, &h.h_in_cap, std::max<size_t>(bytes, 1))) ||
+          (rc = grow_host(&h.h_offs, &h.h_offs_cap, m + 1)))
+        break;
+      par_copy(h.h_in, src_in, bytes);
+      memcpy(h.h_offs, src_offs, (m + 1) * sizeof(uint64_t));
+      src_in = h.h_in;
+      src_offs = h.h_offs;
+    }
+    cld_result* dst = out + a;
+    if (!out_pinned && (rc = grow_host(&h.h_out, &h.h_out_cap, m))) break;
+    // upload (after the slot's previous kernels stopped reading its device buffers)
+    HIP_OK(hipStreamWaitEvent(d->up_stream, h.comp, 0));
+    if (bytes) HIP_OK(hipMemcpyAsync(h.d_in, src_in, bytes, hipMemcpyHostToDevice, d->up_stream));
+    HIP_OK(hipMemcpyAsync(h.d_offs, src_offs, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->up_stream));
+    HIP_OK(hipEventRecord(h.up, d->up_stream));
+    // kernels: buffer base biased so that the caller's offsets index it directly
+    HIP_OK(hipStreamWaitEvent(d->stream, h.up, 0));
+    const uint8_t* kbuf = h.d_in - base;
+    if (flags & kPrepFlags) {
+      if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
+      rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream);
+    } else {
+      rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream);
+    }
+    if (rc) break;
+    HIP_OK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, d->stream));
+    HIP_OK(hipEventRecord(h.comp, d->stream));
+    // download
+    HIP_OK(hipStreamWaitEvent(d->down_stream, h.comp, 0));
+    HIP_OK(hipMemcpyAsync(out_pinned ? dst : h.h_out, h.d_out, m * sizeof(cld_result), hipMemcpyDeviceToHost,
+                          d->down_stream));
+    HIP_OK(hipEventRecord(h.down, d->down_stream));
+    h.pending_n = m;
+    h.pending_dst = out_pinned ? nullptr : dst;
+    h.busy = true;
+  }
+  if (rc == CLD_OK && d->h_trace) watch_trace(d, d->stream);
+  for (auto& h : d->hs) {                              // drain (also after an error: no DMA may outlive the call)
+    int r = deliver(h);
+    if (rc == CLD_OK) rc = r;
+  }
   HIP_OK(hipStreamSynchronize(d->stream));
+  if (rc) return rc;
   if (d->d_dbg) {             // debug: write the dumped words to $CLD_DEBUG_OUT
     uint32_t cnt = 0;
     HIP_OK(hipMemcpy(&cnt, d->d_dbg, 4, hipMemcpyDeviceToHost));
@@ -513,7 +720,23 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     const char* path = getenv("CLD_DEBUG_OUT") ? getenv("CLD_DEBUG_OUT") : "/tmp/cld_dbg.bin";
     if (FILE* f = fopen(path, "wb")) { fwrite(w.data(), 4, w.size(), f); fclose(f); }
   }
-  return collect_stats(d);
+  // statistics of the whole call: counters summed over chunks, kernel time over launches
+  cld_batch_stats& st = d->last;
+  memset(&st, 0, sizeof(st));
+  bool err = false;
+  for (size_t c = 0; c < nch; ++c) {
+    add_counters(d, d->h_ctr + c * kCtrSlots, cut[c + 1] - cut[c], &st);
+    err |= d->h_ctr[c * kCtrSlots + kCtrError] != 0;
+  }
+  for (size_t i = 0; i < d->ev_used; ++i) {
+    float x = 0, y = 0, z = 0;
+    HIP_OK(hipEventElapsedTime(&x, d->ev_pool[i][0], d->ev_pool[i][1]));
+    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][2]));
+    HIP_OK(hipEventElapsedTime(&z, d->ev_pool[i][2], d->ev_pool[i][3]));
+    st.short_ms += x; st.long_ms += y; st.general_ms += z;
+  }
+  d->stats_pending = false;
+  return err ? CLD_EIO : CLD_OK;
 }
 
 // ------------------------------------------------ detect_language batching
@@ -544,12 +767,26 @@ int load_dynamic(const uint8_t* data, size_t len, const std::string& label) {
     fprintf(stderr, "WARNING: Dynamic data loading failed. (tables rejected)\n");
     return rc;
   }
-  for (Device* d : g_devs) {
-    std::lock_guard<std::mutex> dl(d->mu);
-    if ((rc = upload_tables(d, nt)) != CLD_OK) return rc;
-  }
+  if ((rc = swap_tables_all(nt)) != CLD_OK) return rc;
   g_tab = std::move(nt);
   g_dynamic = true;
+  return CLD_OK;
+}
+
+int swap_tables_all(const HostTables& nt) {
+  std::vector<StagedTables> st(g_devs.size());
+  for (size_t i = 0; i < g_devs.size(); ++i) {
+    std::lock_guard<std::mutex> dl(g_devs[i]->mu);
+    if (int rc = stage_tables(g_devs[i], nt, &st[i])) {
+      for (size_t j = 0; j <= i; ++j) discard_tables(g_devs[j], &st[j]);
+      fprintf(stderr, "cld_mi355x: table upload failed on device %d; the tables in use are kept\n", g_devs[i]->id);
+      return rc;
+    }
+  }
+  for (size_t i = 0; i < g_devs.size(); ++i) {       // cannot fail short of a device error
+    std::lock_guard<std::mutex> dl(g_devs[i]->mu);
+    if (int rc = commit_tables(g_devs[i], &st[i])) return rc;
+  }
   return CLD_OK;
 }
 
@@ -616,23 +853,32 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16) {
   return CLD_OK;
 }
 
-int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches) {
-  if (ctx < 0 || ctx >= (int)g_devs.size()) return CLD_EINVAL;
+int cld_kernel_times(int ctx, double* ms3, int* launches) {
+  if (ctx < 0 || ctx >= (int)g_devs.size() || !ms3) return CLD_EINVAL;
   Device* d = g_devs[ctx];
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
-  double a = 0, b = 0;
+  double a = 0, b = 0, c = 0;
   for (size_t i = 0; i < d->ev_used; ++i) {
     HIP_OK(hipEventSynchronize(d->ev_pool[i][3]));
-    float x = 0, y = 0;
+    float x = 0, y = 0, z = 0;
     HIP_OK(hipEventElapsedTime(&x, d->ev_pool[i][0], d->ev_pool[i][1]));
-    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][3]));
-    a += x; b += y;
+    HIP_OK(hipEventElapsedTime(&y, d->ev_pool[i][1], d->ev_pool[i][2]));
+    HIP_OK(hipEventElapsedTime(&z, d->ev_pool[i][2], d->ev_pool[i][3]));
+    a += x; b += y; c += z;
   }
-  if (short_ms) *short_ms = a;
-  if (general_ms) *general_ms = b;
+  ms3[0] = a; ms3[1] = b; ms3[2] = c;
   if (launches) *launches = (int)d->ev_used;
   d->ev_used = 0;
+  return CLD_OK;
+}
+
+int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches) {
+  double ms[3];
+  int rc = cld_kernel_times(ctx, ms, launches);
+  if (rc) return rc;
+  if (short_ms) *short_ms = ms[0];
+  if (general_ms) *general_ms = ms[1] + ms[2];
   return CLD_OK;
 }
 
@@ -662,6 +908,15 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
+    for (auto& h : d->hs) {
+      (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);
+      (void)hipFree(h.d_in); (void)hipFree(h.d_offs); (void)hipFree(h.d_out);
+      (void)hipEventDestroy(h.up); (void)hipEventDestroy(h.comp); (void)hipEventDestroy(h.down);
+    }
+    (void)hipHostFree(d->h_ctr);
+    (void)hipEventDestroy(d->done);
+    (void)hipStreamDestroy(d->up_stream);
+    (void)hipStreamDestroy(d->down_stream);
     (void)hipStreamDestroy(d->stream);
     delete d;
   }
@@ -763,6 +1018,16 @@ int cld_last_batch_stats(int device, cld_batch_stats* st) {
   return rc;
 }
 
+void* cld_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void cld_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 const char* cld_language_code(int lang) {
   if (cld_init(nullptr, 0) != CLD_OK && g_tab.codes.empty()) return "un";
   if (lang < 0 || (size_t)lang >= g_tab.codes.size()) lang = (int)g_tab.meta.unknown_language;
@@ -800,10 +1065,7 @@ int cld_unload_data(void) {
   HostTables nt;
   int rc = load_tables(g_base_path.c_str(), &nt);
   if (rc) return rc;
-  for (Device* d : g_devs) {
-    std::lock_guard<std::mutex> dl(d->mu);
-    if ((rc = upload_tables(d, nt)) != CLD_OK) return rc;
-  }
+  if ((rc = swap_tables_all(nt)) != CLD_OK) return rc;
   g_tab = std::move(nt);
   g_dynamic = false;
   return CLD_OK;

@@ -390,8 +390,7 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
 __device__ __forceinline__ void setb(uint64_t& o, int i, uint32_t v) {
   o = (o & ~(0xFFull << (8 * i))) | ((uint64_t)(v & 0xFF) << (8 * i));
 }
-__device__ bool lower_char(const DevTables& T, const uint8_t* src, int n, uint64_t& out, int& olen) {
-  const DevSM& sm = T.lower;
+__device__ bool lower_char_sm(const DevSM& sm, const uint8_t* src, int n, uint64_t& out, int& olen) {
   const int sh = (int)sm.shift;
   const int nE = 1 << sh;
   const int64_t tb0 = sm.state0;
@@ -472,6 +471,9 @@ __device__ bool lower_char(const DevTables& T, const uint8_t* src, int n, uint64
     i += m;
   }
   return true;
+}
+__device__ __forceinline__ bool lower_char(const DevTables& T, const uint8_t* src, int n, uint64_t& out, int& olen) {
+  return lower_char_sm(T.lower, src, n, out, olen);
 }
 
 // LowerScriptSpan (getonescriptspan.cc:1033-1054): returns text_bytes, or -1.

@@ -36,6 +36,11 @@ def _dump(obj):
     return json.dumps(obj, separators=(",", ":"), ensure_ascii=False).encode("utf-8")
 
 
+def _reject_constant(name):
+    """rapidjson (kParseDefaultFlags) rejects NaN / Infinity / -Infinity; so must we."""
+    raise ValueError("non-standard JSON constant %s" % name)
+
+
 def _first_key_object(pairs):
     d = {}
     for k, v in pairs:              # rapidjson GetMember finds the first member of a name
@@ -83,7 +88,8 @@ class LanguageDetectorService:
             return self._error("Content-Type must be set to application/json", 400)
         body = bytes(body[:self.body_limit])
         try:
-            doc = json.loads(body.decode("utf-8", "surrogateescape"), object_pairs_hook=_first_key_object)
+            doc = json.loads(body.decode("utf-8", "surrogateescape"), object_pairs_hook=_first_key_object,
+                             parse_constant=_reject_constant)
         except ValueError:
             return self._error("Unable to parse request - invalid JSON detected", 400)
         if doc is None:                                       # handlers.go:112-114: nothing written
@@ -129,7 +135,8 @@ def serve(service, port=3000):
     class H(BaseHTTPRequestHandler):
         def _reply(self, method):
             n = int(self.headers.get("Content-Length") or 0)
-            body = self.rfile.read(n) if n else b""
+            # io.LimitReader (handlers.go:40): never read past the limit
+            body = self.rfile.read(min(n, service.body_limit)) if n > 0 else b""
             status, out = service.handle(method, self.path, self.headers.get("Content-Type", ""), body)
             self.send_response(status)
             if out or status != 200:

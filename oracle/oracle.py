@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libcld_oracle.so")
-DEFAULT_TABLES = os.path.join(os.path.dirname(HERE), "language-detector_amd", "data", "cld2_mi355x.cldt")
+DEFAULT_TABLES = os.path.join(os.path.dirname(HERE), "language-detector_amd", "data", "cld2_synth_q1.cldt")
 
 
 class Result(ctypes.Structure):

@@ -7,6 +7,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in ("language-detector_amd", "oracle", "tools", ""):
     sys.path.insert(0, os.path.join(ROOT, p))
 
+# The library's default tables are Q0 (empty quadgram table).  The parity
+# suite opts into the synthetic Q1 table explicitly, so the quadgram path is
+# exercised; the oracle reads the same file (oracle.DEFAULT_TABLES).
+os.environ.setdefault("CLD_MI355X_TABLES",
+                      os.path.join(ROOT, "language-detector_amd", "data", "cld2_synth_q1.cldt"))
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP path)")
@@ -49,4 +55,4 @@ def kats():
 @pytest.fixture(scope="session")
 def blob():
     import cldt
-    return cldt.Blob.load(os.path.join(ROOT, "language-detector_amd", "data", "cld2_mi355x.cldt"))
+    return cldt.Blob.load(os.path.join(ROOT, "language-detector_amd", "data", "cld2_synth_q1.cldt"))

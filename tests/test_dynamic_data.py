@@ -26,7 +26,7 @@ import corpus
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DATA = os.path.join(ROOT, "language-detector_amd", "data")
-SYNTH = os.path.join(DATA, "cld2_mi355x.cldt")     # synthetic quadgram table
+SYNTH = os.path.join(DATA, "cld2_synth_q1.cldt")     # synthetic quadgram table
 Q0 = os.path.join(DATA, "cld2_q0.cldt")             # empty quadgram table
 REPLACED = (cldt.CJK_UNI_PROP, cldt.EXPECTED_SCORE) + cld2_data_file.TABLE_SECTIONS
 

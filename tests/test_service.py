@@ -68,6 +68,49 @@ def test_handler_cases_without_detection(main_test):
         assert (st, body.decode()) == (c["status"], c["expected"]), c["test"]
 
 
+def test_handler_rejects_non_standard_constants(main_test):
+    """rapidjson's default parse rejects NaN / Infinity (handlers.go:51-58 -> 400)."""
+    svc = LanguageDetectorService(dict(main_test["known_languages"]), detect_codes=stub_codes)
+    bad = b'{"error":"Unable to parse request - invalid JSON detected"}'
+    for lit in (b"NaN", b"Infinity", b"-Infinity"):
+        assert svc.handle("POST", "/", "application/json", b'{"request": [{"text": "a", "n": ' + lit + b'}]}') == (400, bad)
+
+
+def test_serve_reads_at_most_the_body_limit(main_test):
+    """io.LimitReader semantics: a large Content-Length never makes the server
+    read (or buffer) past the limit."""
+    import http.client
+    import threading
+    from http.server import ThreadingHTTPServer
+    import service as svc_mod
+    svc = LanguageDetectorService(dict(main_test["known_languages"]), detect_codes=stub_codes, body_limit=64)
+    got = []
+    orig = svc.handle
+    svc.handle = lambda m, p, ct, body: (got.append(len(body)), orig(m, p, ct, body))[1]
+    srv = []
+    real = ThreadingHTTPServer.__init__
+
+    def capture(self, *a, **kw):
+        real(self, *a, **kw)
+        srv.append(self)
+    ThreadingHTTPServer.__init__ = capture
+    try:
+        t = threading.Thread(target=svc_mod.serve, args=(svc, 0), daemon=True)
+        t.start()
+        while not srv:
+            pass
+    finally:
+        ThreadingHTTPServer.__init__ = real
+    port = srv[0].server_address[1]
+    body = b'{"request": [{"text": "hello"}]}' + b" " * 4096
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    c.request("POST", "/", body=body, headers={"Content-Type": "application/json"})
+    r = c.getresponse()
+    r.read()
+    srv[0].shutdown()
+    assert got == [64]
+
+
 def test_handler_edge_semantics(main_test):
     svc = LanguageDetectorService(dict(main_test["known_languages"]), detect_codes=stub_codes)
     ok = b'{"request": [{"text": "hi"}]}'

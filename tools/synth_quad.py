@@ -19,7 +19,7 @@ data exists in this environment.  This tool derives a deterministic stand-in
     scoreonescriptspan.cc:938-964).
 
 Outputs (all deterministic):
-  language-detector_amd/data/cld2_mi355x.cldt   base blob + QUAD/QUAD2 + provenance
+  language-detector_amd/data/cld2_synth_q1.cldt   base blob + QUAD/QUAD2 + provenance
   language-detector_amd/data/vocab.json         {lang_code: [words...]} for synthetic text
 """
 import json
@@ -177,7 +177,7 @@ def main():
     sections.append((cldt.QUAD2, cldt.table_section_bytes(size_one, QUAD2_BUCKETS, KEYMASK, 20261015, b2, ind)))
     sections.append((cldt.PROVENANCE, prov.encode()))
     sections.sort(key=lambda s: s[0])
-    out = os.path.join(ROOT, "language-detector_amd/data/cld2_mi355x.cldt")
+    out = os.path.join(ROOT, "language-detector_amd/data/cld2_synth_q1.cldt")
     cldt.write_blob(out, sections)
 
     # Q0: the reference's own empty-table pattern (generated_distinct_bi_0.cc:22-48)
