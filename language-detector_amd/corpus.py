@@ -113,9 +113,16 @@ def c2(n, seed=SEEDS["c2"]):
     return _assemble(rng, table, lang_idx, targets, kmax=48)
 
 
-def c3(n, seed=SEEDS["c3"], page=16384):
+BOILERPLATE = b"home | news | contact | login | "
+
+
+def c3(n, seed=SEEDS["c3"], page=16384, boiler_frac=0.0):
     """Four paragraphs per page, one per script (random order, random language
-    of that script), each ~page/4 bytes; pages padded with spaces to `page`."""
+    of that script), each ~page/4 bytes; pages padded with spaces to `page`.
+    boiler_frac: in that fraction of pages (seeded) the Latin paragraph opens
+    with ~1 KB of repeated navigation boilerplate, which trips
+    CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) and makes the
+    document take the Squeeze passes."""
     rng = np.random.default_rng(seed)
     v = vocab()
     scripts = list(C3_SCRIPTS)
@@ -143,8 +150,16 @@ def c3(n, seed=SEEDS["c3"], page=16384):
             for j, r in enumerate(rows):
                 pieces[r][k] = b[ol[j]:ol[j + 1]]
     out = np.full(n * page, ord(" "), dtype=np.uint8)
+    boiler = np.zeros(n, dtype=bool)
+    if boiler_frac:
+        boiler[rng.random(n) < boiler_frac] = True
+        bp = np.frombuffer(BOILERPLATE * (1024 // len(BOILERPLATE) + 1), dtype=np.uint8)[:1024]
+    latin = np.argmax(order == 0, axis=1)              # slot of the Latin paragraph
     for r in range(n):
-        doc = np.concatenate(pieces[r])[:page]
+        ps = list(pieces[r])
+        if boiler[r]:
+            ps.insert(int(latin[r]), bp)
+        doc = np.concatenate(ps)[:page]
         out[r * page:r * page + len(doc)] = doc
     return out, np.arange(n + 1, dtype=np.uint64) * page
 

@@ -53,6 +53,10 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
   const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // nothing re-queued (every C2 / C4 batch): leave before touching the shared
+  // dequeue counter, so an empty launch costs its dispatch and nothing more
+  const uint32_t done0 = __hip_atomic_load(&counters[ctr_deq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (done0 >= total) return;
   for (;;) {
     uint32_t k = atomicAdd(&counters[ctr_deq], 1u);
     if (k >= total) break;                       // every lane reaches this exit
@@ -136,6 +140,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::Slot));
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (total == 0) return;                       // empty re-queue list: no dequeue atomics at all
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
   if (lane == 0) smem[wv].kscript = -1;
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (lane == 0) {
-      if (passes >= 1 && passes <= 2) {
+      if (passes >= 1 && passes <= 3) {
         atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
       } else {
         const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);

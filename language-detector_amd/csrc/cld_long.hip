@@ -55,7 +55,7 @@ using wave::wor64;
 using wave::wsum;
 using wave::wsync;
 
-constexpr int kDocCap = 69632;                       // longest document taken (C5 caps at 64 KB)
+constexpr int kDocCap = 1 << 20;                     // longest document taken (C5 caps at 64 KB; the slot holds 1 bit per byte)
 constexpr int kLB = kMaxScriptLowerBuffer + 256;     // lowered span + pads + hash read slack
 constexpr int kDocWords = kDocCap / 64 + 2;
 constexpr int kSpanWords = kLB / 64 + 1;
@@ -75,12 +75,15 @@ constexpr int kLdsText = LNG_TEXT;
 
 // Per-wave working set in HBM (one per resident wavefront of the persistent grid).
 struct Slot {
-  uint32_t epoch;
-  uint32_t pad_[31];
-  uint64_t pred[kPredictionTableSize];   // predictor: (epoch << 32) | last char after hash h
+  uint32_t epoch, epoch2;
+  uint32_t pad_[30];
+  uint64_t pred[kPredictionTableSize];   // Repeats predictor (doc-wide): (epoch << 32) | last char after hash h
+  uint64_t pred2[kPredictionTableSize];  // Squeeze / trigger-test predictor (per span), epoch2
   uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
-  uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats)
-  uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces
+  uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats, Squeeze)
+  uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces; Squeeze: predicted starts
+  uint64_t aux[2][kSpanWords];           // Squeeze: predicted starts of 2/4-byte, 3/4-byte characters
+  uint64_t chm[kSpanWords];              // Squeeze: chunk starts
   alignas(16) uint8_t lb[2][kLB];        // lowered span text; [1] = after CheapRepWords
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
@@ -498,15 +501,67 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   return lpos;
 }
 
+// Character starts of the sequential UTF-8 decode that CountPredictedBytes
+// and CheapRepWordsInplace run (compact_lang_det_impl.cc:541-580, 610-692):
+// a lead byte consumes the count its value claims, continuation bytes or not.
+// For well-formed text that is "every byte that is not 10xxxxxx"; a malformed
+// character (a document cut inside a character leaves one at a span end)
+// swallows the bytes it claims.  Window [base, base + 64) of text[0, len);
+// decoding restarts at every set bit of `resets` (null: only at 0); carry =
+// bytes of this window the previous window's last character still claims.
+__device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, int len, const uint64_t* resets,
+                                                int& carry, int lane) {
+  const int x = base + lane;
+  const bool valid = x < len;
+  const uint8_t b = valid ? text[x] : (uint8_t)0;
+  const bool nc = valid && (b & 0xC0) != 0x80;
+  const int n = utf8_len(b);
+  bool mal = false;
+  if (nc)
+    for (int k = 1; k < n; ++k) mal |= (text[x + k] & 0xC0) != 0x80;
+  const uint64_t ncm = __ballot(nc);
+  const int end = min(base + 64, len);
+  if (!__ballot(mal) && carry == 0) {             // well-formed window: starts = non-continuation bytes
+    if (ncm) {                                    // the last character may claim bytes of the next window
+      const int last = base + topbit(ncm);
+      const int q = last + utf8_len(ufl(text[last]));
+      carry = q > end ? q - end : 0;
+    }
+    return ncm;
+  }
+  // rare: walk the window (uniform scalar loop)
+  auto reset_after = [&](int p) -> int {          // first reset position > p, or a large value
+    if (!resets) return 0x7FFFFFFF;
+    for (int q = p + 1; q < base + 64 + 4; ++q)
+      if ((ufl64(resets[q >> 6]) >> (q & 63)) & 1) return q;
+    return 0x7FFFFFFF;
+  };
+  int p = base + carry;
+  if (carry > 0) {
+    const int r = reset_after(base - 1);
+    if (r < p) p = r;
+  }
+  uint64_t m = 0;
+  while (p < end) {
+    m |= 1ull << (p - base);
+    const int q = p + utf8_len(ufl(text[p]));
+    const int r = reset_after(p);
+    p = r < q ? r : q;
+  }
+  carry = p > end ? p - end : 0;      // in the last window: the last character runs past len
+  return m;
+}
+
 // ------------------------------------------------------ predictor (squeeze/repeats)
-__device__ uint32_t new_epoch(Slot& S, int lane) {
-  uint32_t e = uflu(S.epoch) + 1u;
+// A fresh predictor table: a new epoch makes every older entry read as 0.
+__device__ uint32_t new_epoch(uint32_t& epoch, uint64_t* tbl, int lane) {
+  uint32_t e = uflu(epoch) + 1u;
   if (e == 0) {                                     // wrapped: clear for real
-    for (int i = lane; i < kPredictionTableSize; i += 64) S.pred[i] = 0;
+    for (int i = lane; i < kPredictionTableSize; i += 64) tbl[i] = 0;
     e = 1;
   }
   gsync();
-  if (lane == 0) S.epoch = e;
+  if (lane == 0) epoch = e;
   return e;
 }
 
@@ -560,17 +615,17 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, in
 #pragma unroll
   for (int k = 0; k < 4; ++k) sp += text[lane * 4 + k] == ' ';
   if (wsum(sp) >= (256 * 25) / 100) return true;
-  const uint32_t ep = new_epoch(S, lane);
+  const uint32_t ep = new_epoch(S.epoch2, S.pred2, lane);
   uint32_t h = 0;
-  int pc = 0;
+  int pc = 0, carry = 0;
   for (int w = 0; w < 4; ++w) {
     const int x = (w << 6) + lane;
-    const uint8_t b = text[x];
-    const bool lead = (b & 0xC0) != 0x80;
+    const uint64_t st = char_starts(text, w << 6, 256, nullptr, carry, lane);
+    const bool lead = (st >> lane) & 1;
     int incr = 1;
     const uint32_t c = lead ? (uint32_t)next_char_code(text + x, &incr) : 0u;
     const uint64_t lm = __ballot(lead);
-    const bool pr = predict_window(S.pred, ep, lm, c, h, lane);
+    const bool pr = predict_window(S.pred2, ep, lm, c, h, lane);
     pc += (lead && pr) ? incr : 0;
   }
   return wsum(pc) >= (256 * 67) / 100;
@@ -582,14 +637,16 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, in
 // the next space; at that space the bytes after the previous space, this space
 // included, are dropped if more than half of the segment was predicted.
 __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
-                         int lane) {
+                         bool& ok, int lane) {
   const int nw = (len + 63) >> 6;
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
+  int carry = 0;
   for (int w = 0; w < nw; ++w) {
     const int x = (w << 6) + lane;
     const bool valid = x < len;
     const uint8_t b = valid ? src[x] : (uint8_t)0;
-    const bool lead = valid && (b & 0xC0) != 0x80;
+    const uint64_t st = char_starts(src, w << 6, len, nullptr, carry, lane);
+    const bool lead = valid && ((st >> lane) & 1);
     int incr = 1;
     const uint32_t c = lead ? (uint32_t)next_char_code(src + x, &incr) : 0u;
     const uint64_t lm = __ballot(lead);
@@ -619,6 +676,10 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     }
   }
   gsync();
+  // a last character claiming bytes past the span would make the reference
+  // copy pad bytes too: k_general takes that (malformed) document
+  ok = carry == 0;
+  if (!ok) return len;
   int dpos = 0;
   for (int w = 0; w < nw; ++w) {
     const int x = (w << 6) + lane;
@@ -647,6 +708,136 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
   }
   gsync();
   return dpos;
+}
+
+// CheapSqueezeInplace (compact_lang_det_impl.cc:785-865) on a lowered span,
+// in place.  Chunk boundaries (48 bytes, extended past continuation bytes)
+// depend on the text alone and are found first.  The chunks' CountPredictedBytes
+// calls share one fresh table and hash, so the predictor runs over the span's
+// characters in order -- block-parallel, as for Repeats -- with the decode
+// restarting at every chunk start; each chunk's predicted-byte and
+// CountSpaces4 counts are popcounts over per-byte bitmasks.  The keep / skip
+// assembly then walks the chunks: BackscanToSpace and ForwardscanToSpace
+// (:491-522) are ballots over <= 32 bytes, and a kept chunk (<= 51 bytes)
+// moves in one lane-parallel step, reads before writes, exactly as memmove.
+__device__ __forceinline__ int range_pop(const uint64_t* m, int a, int b) {   // set bits in [a, b)
+  int c = 0;
+  while (a < b) {
+    const int w = a >> 6, o = a & 63, e = min(b - (w << 6), 64);
+    const uint64_t bits = ufl64(m[w]) >> o;
+    const int n = e - o;
+    c += __popcll(n >= 64 ? bits : bits & ((1ull << n) - 1));
+    a += n;
+  }
+  return c;
+}
+
+__device__ __forceinline__ int squeeze_span(Slot& S, uint8_t* text, int len, int lane) {
+  constexpr int kChunk = 48;
+  const int nw = (len + 63) >> 6;
+  // chunk starts
+  for (int i = lane; i < nw + 1; i += 64) S.chm[i] = 0;
+  gsync();
+  {
+    int src = 0, cw = 0;
+    uint64_t cur = 0;
+    while (src < len) {
+      if ((src >> 6) != cw) {
+        if (lane == 0) S.chm[cw] = cur;
+        cur = 0;
+        cw = src >> 6;
+      }
+      cur |= 1ull << (src & 63);
+      int clen = min(kChunk, len - src);
+      while ((ufl(text[src + clen]) & 0xC0) == 0x80) ++clen;
+      src += clen;
+    }
+    if (lane == 0) S.chm[cw] = cur;
+  }
+  gsync();
+  // predictions, decode restarting at each chunk start
+  const uint32_t ep = new_epoch(S.epoch2, S.pred2, lane);
+  uint32_t h = 0;
+  int carry = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int x = (w << 6) + lane;
+    const bool valid = x < len;
+    const uint8_t b = valid ? text[x] : (uint8_t)0;
+    const uint64_t st = char_starts(text, w << 6, len, S.chm, carry, lane);
+    const bool lead = valid && ((st >> lane) & 1);
+    int incr = 1;
+    const uint32_t c = lead ? (uint32_t)next_char_code(text + x, &incr) : 0u;
+    const uint64_t lm = __ballot(lead);
+    const bool pr = predict_window(S.pred2, ep, lm, c, h, lane);
+    const bool ps = lead && pr;                  // CountPredictedBytes adds incr for it
+    const uint64_t m0 = __ballot(ps), m1 = __ballot(ps && ((incr - 1) & 1)), m2 = __ballot(ps && ((incr - 1) & 2));
+    const uint64_t sm = __ballot(valid && b == ' ');
+    if (lane == 0) {
+      S.delm[w] = m0;
+      S.aux[0][w] = m1;
+      S.aux[1][w] = m2;
+      S.spm[w] = sm;
+    }
+  }
+  gsync();
+  constexpr int kSpaceThresh = (kChunk * 25) / 100, kPredictThresh = (kChunk * 40) / 100;
+  int src = 0, dst = 0;
+  bool skipping = false;
+  while (src < len) {
+    int clen = min(kChunk, len - src);
+    while ((ufl(text[src + clen]) & 0xC0) == 0x80) ++clen;    // move past continuation bytes
+    const int space_n = range_pop(S.spm, src, src + (clen & ~3));
+    const int predb_n = range_pop(S.delm, src, src + clen) + range_pop(S.aux[0], src, src + clen) +
+                        2 * range_pop(S.aux[1], src, src + clen);
+    if (space_n >= kSpaceThresh || predb_n >= kPredictThresh) {
+      if (!skipping) {                           // keeping -> skipping: back to a word start
+        const int lim = min(dst, 32);
+        const uint64_t spc = __ballot(lane < lim && text[dst - lane - 1] == ' ');
+        int n = 0;
+        if (spc) {
+          n = __builtin_ctzll(spc);
+        } else {
+          const uint64_t cb = __ballot(lane < lim && (text[dst - lane] & 0xC0) != 0x80);
+          n = cb ? __builtin_ctzll(cb) : 0;
+        }
+        dst -= n;
+        if (dst == 0) {                          // force a leading space if the first chunk goes
+          if (lane == 0) text[0] = ' ';
+          dst = 1;
+        }
+        skipping = true;
+      }
+    } else {
+      int s2 = src, l2 = clen;
+      if (skipping) {                            // skipping -> keeping: forward to a word start
+        const int lim = min(clen, 32);
+        const uint64_t spc = __ballot(lane < lim && text[src + lane] == ' ');
+        int n = 0;
+        if (spc) {
+          n = __builtin_ctzll(spc) + 1;
+        } else {
+          const uint64_t cb = __ballot(lane < lim && (text[src + lane] & 0xC0) != 0x80);
+          n = cb ? __builtin_ctzll(cb) : 0;
+        }
+        s2 += n;
+        l2 -= n;
+        skipping = false;
+      }
+      if (l2 > 0) {                              // memmove(dst, src, l2), l2 <= 51
+        const uint8_t v = lane < l2 ? text[s2 + lane] : (uint8_t)0;
+        gsync();
+        if (lane < l2) text[dst + lane] = v;
+        dst += l2;
+      }
+    }
+    gsync();
+    src += clen;
+  }
+  // pad: "   \0", or one ' ' when fewer than 4 bytes went (:852-862)
+  if (lane < 4 && dst < len - 3) text[dst + lane] = lane < 3 ? ' ' : 0;
+  else if (lane == 0 && dst < len) text[dst] = ' ';
+  gsync();
+  return dst;
 }
 
 // ---------------------------------------------------- quad chain of a span
@@ -1379,13 +1570,21 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
   if (!classify(T, dv, S, lane)) return -kWhyClassify;
   if constexpr (D) mark(s, lane, 0, t);
   if constexpr (D) trace(tr, lane, doc, 2, 0);
-  for (int pass = 1; pass <= 2; ++pass) {
+  // Passes (compact_lang_det_impl.cc:1848-2105): 1 = flags 0; the Squeeze
+  // trigger restarts the document as pass 2 = Squeeze; otherwise pass 2 =
+  // Repeats|Finish.  After a Squeeze pass that is not good enough, pass 3 =
+  // Squeeze|Repeats|Finish.  The Repeats predictor is document-wide (pred),
+  // the Squeeze one is fresh per span (pred2).
+  bool sq = false;
+  for (int pass = 1; pass <= 3; ++pass) {
+    const bool rep = pass == 3 || (pass == 2 && !sq);    // Repeats always comes with Finish
     if (lane == 0) s.dt.init();
     if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
     uint32_t hcarry = 0, ep = 0;
-    if (pass == 2) ep = new_epoch(S, lane);
+    if (rep) ep = new_epoch(S.epoch, S.pred, lane);
     wsync();
     int next = 0, total = 0;
+    bool restart = false;
     for (;;) {
       int ul = 0, st = 0;
       if constexpr (D) trace(tr, lane, doc, 3, next);
@@ -1395,7 +1594,10 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
       if (st == 0) break;
       if (st < 0) return -kWhySpan;
       if (pass == 1) {
-        if (tb > 2048 && squeeze_trigger(S, S.lb[0], lane)) return -kWhySqueeze;   // Squeeze restart: k_general
+        if (tb > 2048 && squeeze_trigger(S, S.lb[0], lane)) {   // recursion with Squeeze (:1867-1900)
+          restart = true;
+          break;
+        }
         if constexpr (D) mark(s, lane, 2, t);
       }
       bool ok;
@@ -1405,8 +1607,11 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         for (int i = lane; i < n16; i += 64)
           reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(S.lb[0])[i];
         wsync();
-        if (pass == 2) {
-          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, lane);   // in place, as the reference does
+        if (sq) tb = squeeze_span(S, s.text, tb, lane);             // in place, as the reference does
+        if (rep) {
+          bool okr;
+          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, okr, lane);   // in place, as the reference does
+          if (!okr) return -kWhySpan;
           if constexpr (D) mark(s, lane, 3, t);
         }
         if constexpr (D) trace(tr, lane, doc, 5, tb);
@@ -1417,8 +1622,11 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc);
       } else {
         const uint8_t* text = S.lb[0];
-        if (pass == 2) {
-          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, lane);
+        if (sq) tb = squeeze_span(S, S.lb[0], tb, lane);
+        if (rep) {
+          bool okr;
+          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, okr, lane);
+          if (!okr) return -kWhySpan;
           text = S.lb[1];
           if constexpr (D) mark(s, lane, 3, t);
         }
@@ -1433,8 +1641,11 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
       t = (D && s.prof) ? (long long)clock64() : 0;
       total += tb;
     }
-    const int res = wave::finish_document(T, s.dt, total, pass == 2, out, lane) ? 1 : 2;
-    if (res == 1) return pass;
+    if (restart) {
+      sq = true;
+      continue;
+    }
+    if (wave::finish_document(T, s.dt, total, rep, out, lane)) return pass;
   }
   return 0;
 }

@@ -826,6 +826,7 @@ struct cldo_ctx {
   int sqz_tbl[kPredictionTableSize];
   uint8_t* docbuf; int docbuf_cap;
   cldo_trace_fn trace; void* trace_arg;
+  int trace_text;                              /* also trace each lowered span's bytes (hex) */
 };
 
 static void tracef(struct cldo_ctx* c, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -1518,6 +1519,22 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
     span_t span;
     while (get_one_script_span(ss, &span)) {
       lower_script_span(ss, &span);
+      if (c->trace && c->trace_text) {
+        static const char hx[] = "0123456789abcdef";
+        char* h = (char*)malloc(2 * (size_t)span.text_bytes + 1);
+        for (int i = 0; i < span.text_bytes; ++i) {
+          h[2 * i] = hx[span.text[i] >> 4];
+          h[2 * i + 1] = hx[span.text[i] & 15];
+        }
+        h[2 * span.text_bytes] = 0;
+        if (c->trace) {                        /* direct: longer than tracef's line buffer */
+          char* line = (char*)malloc(2 * (size_t)span.text_bytes + 32);
+          sprintf(line, "lowered %d %s", flags, h);
+          c->trace(c->trace_arg, line);
+          free(line);
+        }
+        free(h);
+      }
       if (flags & kCLDFlagSqueeze) {
         span.text_bytes = cheap_squeeze_inplace(span.text, span.text_bytes, 0, c->sqz_tbl);
       } else if ((kCheapSqueezeTestThresh >> 1) < span.text_bytes && !(flags & kCLDFlagFinish)) {
@@ -1583,6 +1600,7 @@ void cldo_ctx_free(cldo_ctx* c) {
   free(c->ss.sbuf); free(c->ss.lbuf); free(c->docbuf); free(c);
 }
 void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg) { c->trace = fn; c->trace_arg = arg; }
+void cldo_set_trace_text(cldo_ctx* c, int on) { c->trace_text = on; }
 
 /* The document is copied into a buffer followed by 16 NUL bytes, matching
  * the NUL-terminated C string the reference wrapper receives. */

@@ -31,6 +31,7 @@ int cldo_load(const char* cldt_path);
 cldo_ctx* cldo_ctx_new(void);
 void cldo_ctx_free(cldo_ctx* c);
 void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg);
+void cldo_set_trace_text(cldo_ctx* c, int on);   /* trace lines "lowered <flags> <hex>" per span */
 int cldo_detect(cldo_ctx* c, const char* text, int len, cldo_result* r);
 const char* cldo_detect_language(cldo_ctx* c, const char* text);
 int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_result* out, int threads);

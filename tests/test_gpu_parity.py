@@ -61,7 +61,9 @@ def test_bucket_boundaries_and_requeue(gpu, oracle):
         i = int(rng.integers(0, 3000))
         d = bytes(b2[o2[i]:o2[i + 40]])[:L]
         docs.append(d)
-    docs.append(("aaaa bbbb cccc " * 400).encode())                 # squeeze trigger (repetitive)
+    docs.append(("aaaa bbbb cccc " * 400).encode())                 # repetitive, below the trigger
+    docs.append(corpus.BOILERPLATE * 40 + bytes(b2[o2[0]:o2[30]]))  # squeeze trigger: predicted bytes
+    docs.append(("a b c d e f g h " * 300).encode())                # squeeze trigger: spaces
     docs.append((" ".join(["w%d" % i for i in range(2000)])).encode())
     docs.append(bytes(b2[o2[0]:o2[300]]))                           # ~40 KB mixed-language: pass 3
     buf, offs = gpu.pack(docs)
@@ -83,6 +85,48 @@ def test_long_documents(gpu, oracle):
     docs.append(bytes(b2[o2[0]:o2[-1]]).replace(b" ", b" "))          # ~800 KB single document
     buf, offs = gpu.pack(docs)
     check(gpu, oracle, buf, offs, "long")
+    st = gpu.last_stats(0)
+    assert st.general_docs == 0, list(st.long_requeue)           # up to 1 MB: the wavefront path
+
+
+def test_squeeze_documents_stay_on_the_wavefront_path(gpu, oracle):
+    """CheapSqueezeTriggerTest restarts (compact_lang_det_impl.cc:1867-1900) and
+    the Squeeze / Squeeze+Repeats passes run in k_long: bit-exact, and no
+    document falls through to the sequential kernel."""
+    b3, o3 = corpus.c3(2000, seed=21, boiler_frac=0.05)
+    b2, o2 = corpus.c2(3000, seed=22)
+    docs = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(2000)]
+    docs += [corpus.BOILERPLATE * k + bytes(b2[o2[10 * k]:o2[10 * k + 25 + k]]) for k in range(8, 80, 3)]
+    docs += [("a b c d e f g h " * (150 + 7 * k)).encode() + bytes(b2[o2[k]:o2[k + 5]]) for k in range(20)]
+    buf, offs = gpu.pack(docs)
+    got = check(gpu, oracle, buf, offs, "squeeze")
+    st = gpu.last_stats(0)
+    ref = oracle.detect_batch(buf, offs, threads=16)
+    assert int((ref["passes"] == 3).sum()) >= 60          # the Squeeze restarts taken
+    assert st.general_docs == 0, list(st.long_requeue)
+    assert st.passes[2] == int((ref["passes"] == 3).sum())
+    assert len(got) == len(docs)
+
+
+def test_full_size_c3_c4_properties(gpu, oracle):
+    """BASELINE sizes of C3 (100K x 16 KB pages) and C4 (1M x 150 B + 100K x
+    4 KB CJK): an oracle-checked random sample and re-batching invariance."""
+    rng = np.random.default_rng(7)
+    for cfg, n, k in (("c3", 100_000, 1500), ("c4", 1_100_000, 20000)):
+        buf, offs = corpus.GENERATORS[cfg](n)
+        got = gpu.detect_batch(buf=buf, offsets=offs)
+        st = gpu.last_stats(0)
+        assert st.general_docs == 0, (cfg, list(st.long_requeue))
+        idx = np.sort(rng.choice(n, size=k, replace=False))
+        docs = [bytes(buf[offs[i]:offs[i + 1]]) for i in idx]
+        sb, so = gpu.pack(docs)
+        assert_same(got[idx], oracle.detect_batch(sb, so, threads=16), cfg + " sample")
+        perm = rng.permutation(len(docs))
+        pb, po = gpu.pack([docs[i] for i in perm])
+        again = gpu.detect_batch(buf=pb, offsets=po)
+        inv = np.empty_like(perm); inv[perm] = np.arange(len(perm))
+        assert_same(again[inv], got[idx], cfg + " permuted")
+        del buf, offs, got
 
 
 def test_full_size_c2_properties(gpu, oracle):

@@ -41,4 +41,18 @@ def summarise(d):
 
 
 if __name__ == "__main__":
-    print(json.dumps(summarise(sys.argv[1]), indent=1))
+    # pmc_summary.py DIR [CONFIG DOCS]: with CONFIG, also record the summary as
+    # profiles/pmc_current.json[CONFIG] (what bench.py reads for traffic / issue)
+    s = summarise(sys.argv[1])
+    print(json.dumps(s, indent=1))
+    if len(sys.argv) > 3:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        path = os.path.join(root, "profiles", "pmc_current.json")
+        cur = json.load(open(path)) if os.path.exists(path) else {}
+        s["docs"] = int(sys.argv[3])
+        s["source"] = os.path.relpath(sys.argv[1], root)
+        if "hbm_fetch_bytes" in s and "hbm_write_bytes" in s:
+            s["hbm_bytes_per_launch"] = s["hbm_fetch_bytes"] + s["hbm_write_bytes"]
+        cur[sys.argv[2]] = s
+        with open(path, "w") as f:
+            json.dump(cur, f, indent=1, sort_keys=True)
