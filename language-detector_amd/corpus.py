@@ -253,4 +253,72 @@ def c5(n, seed=SEEDS["c5"], cap=65536):
     return np.concatenate(docs) if n else np.zeros(0, np.uint8), offs
 
 
+HTML_TAGS = [b"p", b"div", b"span", b"b", b"i", b"em", b"td", b"tr", b"li", b"h1", b"h2", b"a", b"font", b"br"]
+HTML_ENTITIES = [b"&amp;", b"&lt;", b"&gt;", b"&quot;", b"&nbsp;", b"&eacute;", b"&Eacute;", b"&uuml;", b"&ntilde;",
+                 b"&copy;", b"&#233;", b"&#xE9;", b"&#1044;", b"&#x4e2d;", b"&#20013;", b"&mdash;", b"&hellip;",
+                 b"&rsquo;", b"&bogus;", b"&", b"&#;", b"&#x;", b"&#65;", b"&#0000000065;", b"&#123456789;",
+                 b"&lang", b"&lang;", b"&amp", b"&auml", b"&#150;", b"&#xFFFE;", b"&#55296;"]
+
+
+def html(n, seed=0xC1D20006, lo=200, hi=6000):
+    """HTML pages for the is_plain_text=false path (no BASELINE config names
+    it): words of one c2/c3 language wrapped in tags, with
+    <script>/<style>/<!-- --> blocks, quoted attributes (some with CR/LF),
+    lang= / meta content-language attributes, named and numeric entities, and
+    stray '<' / '>' -- every construct the reference's tag parser and entity
+    reader distinguish (getonescriptspan.cc:150-541)."""
+    rng = np.random.default_rng(seed)
+    v = vocab()
+    langs = [l for l in C2_LANGS + sum(C3_SCRIPTS.values(), []) if l in v]
+    docs = []
+    for _ in range(n):
+        lang = langs[int(rng.integers(0, len(langs)))]
+        words = v[lang]
+        target = int(rng.integers(lo, hi))
+        out = [b"<html lang=\"" + lang.encode() + b"\"><head><title>"]
+        if rng.random() < 0.3:
+            out.append(b'<meta http-equiv="content-language" content="' + lang.encode() + b'">')
+        while sum(map(len, out)) < target:
+            r = rng.random()
+            if r < 0.55:
+                k = int(rng.integers(1, 9))
+                ws = [words[int(i)] for i in rng.integers(0, len(words), size=k)]
+                if rng.random() < 0.2:
+                    ws[0] = ws[0][:1].upper() + ws[0][1:]
+                out.append(b" ".join(ws) + b" ")
+            elif r < 0.70:
+                t = HTML_TAGS[int(rng.integers(0, len(HTML_TAGS)))]
+                if rng.random() < 0.3:
+                    t = t.upper()
+                attr = b""
+                if rng.random() < 0.3:
+                    q = b'"' if rng.random() < 0.7 else b"'"
+                    val = b"x > y" if rng.random() < 0.3 else (b"a\nb" if rng.random() < 0.2 else b"cls")
+                    attr = b" class=" + q + val + q
+                out.append(b"<" + t + attr + b">" if rng.random() < 0.6 else b"</" + t + b">")
+            elif r < 0.80:
+                out.append(HTML_ENTITIES[int(rng.integers(0, len(HTML_ENTITIES)))])
+            elif r < 0.85:
+                body = b" ".join(words[int(i)] for i in rng.integers(0, len(words), size=3))
+                kind = int(rng.integers(0, 4))
+                if kind == 0:
+                    out.append(b"<script type=\"text/javascript\">var s = '<b>" + body + b"</b>';</script>")
+                elif kind == 1:
+                    out.append(b"<STYLE>p { color: red } " + body + b"</STYLE >")
+                elif kind == 2:
+                    out.append(b"<!-- " + body + b" <b> -- -->")
+                else:
+                    out.append(b"<script>" + body + b"</scrip t>" + body + b"</script>")
+            elif r < 0.90:
+                out.append([b" < ", b" > ", b"<<", b"a<b", b"<!", b"<!-", b"<x '", b"\r\n", b"1 < 2 > 0", b"<>"][int(rng.integers(0, 10))])
+            else:
+                out.append(b"<span lang='" + lang.encode() + b"'>")
+        if rng.random() < 0.8:
+            out.append(b"</body></html>")
+        docs.append(b"".join(out))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(d) for d in docs], out=offs[1:])
+    return (np.frombuffer(b"".join(docs), dtype=np.uint8).copy() if n else np.zeros(0, np.uint8)), offs
+
+
 GENERATORS = {"c2": c2, "c3": c3, "c4": c4, "c5": c5}

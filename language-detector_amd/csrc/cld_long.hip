@@ -58,6 +58,10 @@ using wave::wsync;
 constexpr int kDocCap = 1 << 20;                     // longest document taken (C5 caps at 64 KB; the slot holds 1 bit per byte)
 constexpr int kLB = kMaxScriptLowerBuffer + 256;     // lowered span + pads + hash read slack
 constexpr int kDocWords = kDocCap / 64 + 2;
+// Documents up to this size keep their per-byte classes in the slot (classify
+// writes them once, both passes' span builders stream them back, prefetching
+// a window ahead); longer ones recompute them in the span builder.
+constexpr int kClsCap = 65536 + 128;
 constexpr int kSpanWords = kLB / 64 + 1;
 constexpr int kListCap = kLB / 2;                    // words / spaces / chain entries per span
 constexpr int kHB = 1024;                            // hits per round (reference: <= 1000)
@@ -80,6 +84,8 @@ struct Slot {
   uint64_t pred[kPredictionTableSize];   // Repeats predictor (doc-wide): (epoch << 32) | last char after hash h
   uint64_t pred2[kPredictionTableSize];  // Squeeze / trigger-test predictor (per span), epoch2
   uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
+  uint32_t cls[kClsCap];                 // documents <= kClsCap - 64 bytes: class word per byte (cls_* below)
+  uint32_t low[kClsCap];                 //   and the lowered bytes of the character starting there
   uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats, Squeeze)
   uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces; Squeeze: predicted starts
   uint64_t aux[2][kSpanWords];           // Squeeze: predicted starts of 2/4-byte, 3/4-byte characters
@@ -281,6 +287,7 @@ __device__ __noinline__ uint64_t char_slow(DevSM script, DevSM scan, DevSM lower
 // count the continuation bytes the lead bytes claim / that are present.
 // Nothing is stored: classify() and the span builder both call this, so the
 // per-wave slot holds no per-byte state.
+template <bool SN2 = true>
 __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView& dv, int p, uint32_t& lw, int& bad,
                                                int& need, int& conts) {
   const int L = dv.len;
@@ -321,7 +328,8 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
     lw = (uint32_t)(e >> 32);
   }
   // script of the next character (its bytes are b[n..n+3]; NULs past the end)
-  int sn2;
+  int sn2 = 0;
+  if constexpr (SN2) {
   const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
   const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
   const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
@@ -331,6 +339,7 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
   else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80)
     sn2 = (int)(T.cpt[cpt_index(c2, d1, d2, 3)] & 0xFF);
   else sn2 = script_num(T, dv, p + n);
+  }
   if (st < 0) bad = 1;
   const bool ls = st > 0 && sn != 0;
   return (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
@@ -341,15 +350,25 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // letter-stop bitmap (one bit per byte) the span builder searches for span
 // starts.  False if the document does not tile into characters with local
 // scanner behaviour (then k_general redoes it).
-__device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, int lane) {
+template <bool ST>
+__device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
+  cut = false;
   const int nw = (L + 63) >> 6;
   for (int w = 0; w < nw; ++w) {
+    const int p = (w << 6) + lane;
     uint32_t lw;
-    const uint32_t cw = char_props(T, dv, (w << 6) + lane, lw, bad, need, conts);
+    const uint32_t cw = char_props<ST>(T, dv, p, lw, bad, need, conts);
+    if constexpr (ST) {
+      if (p < L) {
+        S.cls[p] = cw;
+        S.low[p] = lw;
+      }
+    }
     const uint64_t m = __ballot((cw >> 20) & 1);
     if (lane == 0) S.lsm[w] = m;
+    cut |= __ballot(cls_cut(cw)) != 0;
   }
   bad |= (wsum(conts) != wsum(need)) ? 1 : 0;
   gsync();
@@ -380,6 +399,7 @@ __device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, ui
 // with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
+template <bool ST>
 __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane) {
   const int L = dv.len;
@@ -396,16 +416,37 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   }
   int ignore = 0;
   uint32_t lq;
-  const int ss = ufl(cls_sn(char_props(T, dv, q, lq, ignore, ignore, ignore)));
+  const int ss = ufl(cls_sn(ST ? S.cls[q] : char_props<false>(T, dv, q, lq, ignore, ignore, ignore)));
   ulscript = ss;
   if (lane == 0) lb[0] = ' ';
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
+  // stored classes: window w+1's words are loaded while window w is processed
+  uint32_t ncw = 0, nlw = 0;
+  if constexpr (ST) {
+    const int x0 = ((q >> 6) << 6) + lane;
+    if (x0 >= q && x0 < L) {
+      ncw = S.cls[x0];
+      nlw = S.low[x0];
+    }
+  }
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
-    int ignore = 0;
-    uint32_t lw = 0;
-    const uint32_t cw = x >= q ? char_props(T, dv, x, lw, ignore, ignore, ignore) : 0u;
+    uint32_t lw = 0, cw = 0;
+    if constexpr (ST) {
+      cw = ncw;
+      lw = nlw;
+      const int xn = x + 64;
+      ncw = 0;
+      nlw = 0;
+      if (xn < L) {
+        ncw = S.cls[xn];
+        nlw = S.low[xn];
+      }
+    } else {
+      int ignore2 = 0;
+      if (x >= q) cw = char_props(T, dv, x, lw, ignore2, ignore2, ignore2);
+    }
     const bool lead = cls_lead(cw);
     const int n = cls_n(cw);
     bool brk = false, ok = false, foreign = false;
@@ -501,41 +542,18 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   return lpos;
 }
 
-// Character starts of the sequential UTF-8 decode that CountPredictedBytes
-// and CheapRepWordsInplace run (compact_lang_det_impl.cc:541-580, 610-692):
-// a lead byte consumes the count its value claims, continuation bytes or not.
-// For well-formed text that is "every byte that is not 10xxxxxx"; a malformed
-// character (a document cut inside a character leaves one at a span end)
-// swallows the bytes it claims.  Window [base, base + 64) of text[0, len);
-// decoding restarts at every set bit of `resets` (null: only at 0); carry =
-// bytes of this window the previous window's last character still claims.
-__device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, int len, const uint64_t* resets,
-                                                int& carry, int lane) {
-  const int x = base + lane;
-  const bool valid = x < len;
-  const uint8_t b = valid ? text[x] : (uint8_t)0;
-  const bool nc = valid && (b & 0xC0) != 0x80;
-  const int n = utf8_len(b);
-  bool mal = false;
-  if (nc)
-    for (int k = 1; k < n; ++k) mal |= (text[x + k] & 0xC0) != 0x80;
-  const uint64_t ncm = __ballot(nc);
-  const int end = min(base + 64, len);
-  if (!__ballot(mal) && carry == 0) {             // well-formed window: starts = non-continuation bytes
-    if (ncm) {                                    // the last character may claim bytes of the next window
-      const int last = base + topbit(ncm);
-      const int q = last + utf8_len(ufl(text[last]));
-      carry = q > end ? q - end : 0;
-    }
-    return ncm;
-  }
-  // rare: walk the window (uniform scalar loop)
+// The sequential walk of char_starts for a window holding a malformed
+// character (or the tail of one), out of line: it is rare, and its loop would
+// otherwise add to the span builders' registers.
+__device__ __noinline__ uint64_t char_starts_walk(const uint8_t* text, int base, int len, const uint64_t* resets,
+                                                  int& carry) {
   auto reset_after = [&](int p) -> int {          // first reset position > p, or a large value
     if (!resets) return 0x7FFFFFFF;
     for (int q = p + 1; q < base + 64 + 4; ++q)
       if ((ufl64(resets[q >> 6]) >> (q & 63)) & 1) return q;
     return 0x7FFFFFFF;
   };
+  const int end = min(base + 64, len);
   int p = base + carry;
   if (carry > 0) {
     const int r = reset_after(base - 1);
@@ -550,6 +568,43 @@ __device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, i
   }
   carry = p > end ? p - end : 0;      // in the last window: the last character runs past len
   return m;
+}
+
+// Character starts of the sequential UTF-8 decode that CountPredictedBytes
+// and CheapRepWordsInplace run (compact_lang_det_impl.cc:541-580, 610-692):
+// a lead byte consumes the count its value claims, continuation bytes or not.
+// For well-formed text that is "every byte that is not 10xxxxxx"; a malformed
+// character (a document cut inside a character leaves one at a span end)
+// swallows the bytes it claims.  Window [base, base + 64) of text[0, len);
+// decoding restarts at every set bit of `resets` (null: only at 0); carry =
+// bytes of this window the previous window's last character still claims.
+__device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, int len, const uint64_t* resets,
+                                                int& carry, bool careful, int lane) {
+  const int x = base + lane;
+  if (!careful)                                  // no cut character in the document: well-formed span text
+    return __ballot(x < len && (text[x] & 0xC0) != 0x80);
+  const bool valid = x < len;
+  const uint8_t b = valid ? text[x] : (uint8_t)0;
+  const bool nc = valid && (b & 0xC0) != 0x80;
+  const int n = utf8_len(b);
+  bool mal = false;
+  if (nc)
+    for (int k = 1; k < n; ++k) mal |= (text[x + k] & 0xC0) != 0x80;
+  const uint64_t ncm = __ballot(nc);
+  const int end = min(base + 64, len);
+  // well-formed window whose carried bytes (the tail of a character begun in
+  // the previous window) are continuation bytes: starts = non-continuation bytes
+  const bool carry_ok = carry == 0 || (carry < 64 && (ncm & ((1ull << carry) - 1)) == 0);
+  if (!__ballot(mal) && carry_ok) {
+    if (ncm) {                                    // the last character may claim bytes of the next window
+      const int last = base + topbit(ncm);
+      const int q = last + utf8_len(ufl(text[last]));
+      carry = q > end ? q - end : 0;
+    }
+    return ncm;
+  }
+  // rare: walk the window (uniform scalar loop, out of line)
+  return char_starts_walk(text, base, len, resets, carry);
 }
 
 // ------------------------------------------------------ predictor (squeeze/repeats)
@@ -610,7 +665,7 @@ __device__ bool predict_window(uint64_t* tbl, uint32_t epoch, uint64_t lm, uint3
 // CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) on a lowered span
 // of more than 2048 bytes: >= 25% spaces or >= 67% predicted bytes in the first
 // 256 bytes (fresh table, hash 0).
-__device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, int lane) {
+__device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, bool careful, int lane) {
   int sp = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) sp += text[lane * 4 + k] == ' ';
@@ -620,7 +675,7 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, in
   int pc = 0, carry = 0;
   for (int w = 0; w < 4; ++w) {
     const int x = (w << 6) + lane;
-    const uint64_t st = char_starts(text, w << 6, 256, nullptr, carry, lane);
+    const uint64_t st = char_starts(text, w << 6, 256, nullptr, carry, careful, lane);
     const bool lead = (st >> lane) & 1;
     int incr = 1;
     const uint32_t c = lead ? (uint32_t)next_char_code(text + x, &incr) : 0u;
@@ -637,7 +692,7 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, in
 // the next space; at that space the bytes after the previous space, this space
 // included, are dropped if more than half of the segment was predicted.
 __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
-                         bool& ok, int lane) {
+                         bool careful, bool& ok, int lane) {
   const int nw = (len + 63) >> 6;
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
   int carry = 0;
@@ -645,7 +700,7 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     const int x = (w << 6) + lane;
     const bool valid = x < len;
     const uint8_t b = valid ? src[x] : (uint8_t)0;
-    const uint64_t st = char_starts(src, w << 6, len, nullptr, carry, lane);
+    const uint64_t st = char_starts(src, w << 6, len, nullptr, carry, careful, lane);
     const bool lead = valid && ((st >> lane) & 1);
     int incr = 1;
     const uint32_t c = lead ? (uint32_t)next_char_code(src + x, &incr) : 0u;
@@ -732,7 +787,9 @@ __device__ __forceinline__ int range_pop(const uint64_t* m, int a, int b) {   //
   return c;
 }
 
-__device__ __forceinline__ int squeeze_span(Slot& S, uint8_t* text, int len, int lane) {
+// Out of line: Squeeze is rare, and inlined its state would count against the
+// registers of every pass.
+__device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool careful, int lane) {
   constexpr int kChunk = 48;
   const int nw = (len + 63) >> 6;
   // chunk starts
@@ -763,7 +820,7 @@ __device__ __forceinline__ int squeeze_span(Slot& S, uint8_t* text, int len, int
     const int x = (w << 6) + lane;
     const bool valid = x < len;
     const uint8_t b = valid ? text[x] : (uint8_t)0;
-    const uint64_t st = char_starts(text, w << 6, len, S.chm, carry, lane);
+    const uint64_t st = char_starts(text, w << 6, len, S.chm, carry, careful, lane);
     const bool lead = valid && ((st >> lane) & 1);
     int incr = 1;
     const uint32_t c = lead ? (uint32_t)next_char_code(text + x, &incr) : 0u;
@@ -1567,7 +1624,10 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
   const DocView dv{g, L};
   if constexpr (D) trace(tr, lane, doc, 1, L);
   long long t = (D && s.prof) ? (long long)clock64() : 0;
-  if (!classify(T, dv, S, lane)) return -kWhyClassify;
+  const bool stored = L <= kClsCap - 64;
+  bool careful;                                  // a cut last character: span text may be malformed
+  if (!(stored ? classify<true>(T, dv, S, careful, lane) : classify<false>(T, dv, S, careful, lane)))
+    return -kWhyClassify;
   if constexpr (D) mark(s, lane, 0, t);
   if constexpr (D) trace(tr, lane, doc, 2, 0);
   // Passes (compact_lang_det_impl.cc:1848-2105): 1 = flags 0; the Squeeze
@@ -1588,13 +1648,14 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
     for (;;) {
       int ul = 0, st = 0;
       if constexpr (D) trace(tr, lane, doc, 3, next);
-      int tb = next_span(T, dv, S, S.lb[0], next, ul, st, lane);
+      int tb = stored ? next_span<true>(T, dv, S, S.lb[0], next, ul, st, lane)
+                      : next_span<false>(T, dv, S, S.lb[0], next, ul, st, lane);
       if constexpr (D) trace(tr, lane, doc, 4, tb);
       if constexpr (D) mark(s, lane, 1, t);
       if (st == 0) break;
       if (st < 0) return -kWhySpan;
       if (pass == 1) {
-        if (tb > 2048 && squeeze_trigger(S, S.lb[0], lane)) {   // recursion with Squeeze (:1867-1900)
+        if (tb > 2048 && squeeze_trigger(S, S.lb[0], careful, lane)) {   // recursion with Squeeze (:1867-1900)
           restart = true;
           break;
         }
@@ -1607,10 +1668,10 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         for (int i = lane; i < n16; i += 64)
           reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(S.lb[0])[i];
         wsync();
-        if (sq) tb = squeeze_span(S, s.text, tb, lane);             // in place, as the reference does
+        if (sq) tb = squeeze_span(S, s.text, tb, careful, lane);             // in place, as the reference does
         if (rep) {
           bool okr;
-          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, okr, lane);   // in place, as the reference does
+          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, careful, okr, lane);   // in place, as the reference does
           if (!okr) return -kWhySpan;
           if constexpr (D) mark(s, lane, 3, t);
         }
@@ -1622,10 +1683,10 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc);
       } else {
         const uint8_t* text = S.lb[0];
-        if (sq) tb = squeeze_span(S, S.lb[0], tb, lane);
+        if (sq) tb = squeeze_span(S, S.lb[0], tb, careful, lane);
         if (rep) {
           bool okr;
-          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, okr, lane);
+          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, careful, okr, lane);
           if (!okr) return -kWhySpan;
           text = S.lb[1];
           if constexpr (D) mark(s, lane, 3, t);

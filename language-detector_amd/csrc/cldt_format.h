@@ -39,6 +39,17 @@ enum cldt_section_id {
   CLDT_LANG_CODES = 29,          /* string table                                */
   CLDT_LANG_NAMES = 30,
   CLDT_ULSCRIPT_CODES = 31,
+  /* HTML mode (getonescriptspan.cc:150-541) and hints (compact_lang_det_hint_code.cc);
+   * optional: a blob without them supports plain text without hints only */
+  CLDT_ENTITY_NAMES = 32,        /* string table, sorted (generated_entities.cc) */
+  CLDT_ENTITY_VALUES = 33,       /* int32[n] code points                        */
+  CLDT_CP1252_FIX = 34,          /* uint32[256] FixUnicodeValue below U+0100    */
+  CLDT_HINT_LANGTAG1 = 35,       /* cldt_hint_entry[n] + string pool, sorted    */
+  CLDT_HINT_LANGTAG2 = 36,
+  CLDT_HINT_TLD = 37,
+  CLDT_HINT_CODE_ACTION = 38,    /* uint8[256] language-attribute scanner       */
+  CLDT_HINT_CODE_REMAP = 39,     /* uint8[256]                                  */
+  CLDT_HINT_ENCODING = 41,       /* int16[n_encodings] prior per Encoding (0: none) */
   CLDT_PROVENANCE = 40           /* free text: how each section was produced    */
 };
 
@@ -79,5 +90,14 @@ typedef struct {
   uint32_t size_one, size, key_mask, build_date;
   uint32_t n_ind, n_buckets_stored, reserved[2];
 } cldt_table_header;
+
+/* Hint lookup tables (LangTagLookup / TLDLookup, compact_lang_det_hint_code.cc):
+ * u32 n, then n entries, then the string pool; offsets are into the pool,
+ * code_off = 0xFFFFFFFF when the table has no language-code column.  A prior
+ * is OneCLDLangPrior: (weight << 10) + Language, int16. */
+typedef struct {
+  uint32_t key_off, code_off;
+  int16_t prior1, prior2;
+} cldt_hint_entry;
 
 #endif  /* CLDT_FORMAT_H_ */

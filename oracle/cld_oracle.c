@@ -117,6 +117,9 @@ static struct {
   const uint8_t* codes; /* string section */
   const uint8_t* names;
   const uint8_t* script_codes;
+  /* HTML mode (optional sections) */
+  const uint8_t* ent_names; const int32_t* ent_values; uint32_t n_ent;
+  const uint32_t* cp1252;
 } T;
 
 static const uint8_t* find_section(uint32_t id, uint64_t* size) {
@@ -188,6 +191,9 @@ int cldo_load(const char* path) {
   T.codes = find_section(CLDT_LANG_CODES, NULL);
   T.names = find_section(CLDT_LANG_NAMES, NULL);
   T.script_codes = find_section(CLDT_ULSCRIPT_CODES, NULL);
+  T.ent_names = find_section(CLDT_ENTITY_NAMES, NULL);
+  T.ent_values = (const int32_t*)find_section(CLDT_ENTITY_VALUES, &sz); T.n_ent = (uint32_t)(sz / 4);
+  T.cp1252 = (const uint32_t*)find_section(CLDT_CP1252_FIX, NULL);
   if (!T.expected || !T.lgprob || !T.l2p || !T.p2l_latn || !T.p2l_othr || !T.rtype ||
       !T.deflang || !T.closest || !T.close_set || !T.codes) return -7;
   T.loaded = 1;
@@ -362,7 +368,7 @@ static int scan_to_letter_or_special(const uint8_t* isrc, int len) {
 /* UTF8GenericReplace(utf8repl_lettermarklower, plain text), offset map
  * omitted (it only feeds ResultChunkVector).  utf8statetable.cc:608-867 and
  * the kExitDoAgain driver loop :1138-1169.  Returns bytes filled. */
-static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen) {
+static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen, int plain) {
   const sm_t* sm = &T.lower;
   int total_filled = 0;
   const uint8_t* in = isrc; int inlen = ilen;
@@ -425,7 +431,11 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen)
             const uint8_t* re = sm->remap + 4 * (size_t)offset;
             int del_len = re[0] & ~0x80;
             int add_len = re[1] & ~0x80;
-            /* kHtmlPlaintextFlag pair: plain text uses this entry (:755-762) */
+            /* kHtmlPlaintextFlag pair: plain text uses this entry, HTML the next (:755-762) */
+            if ((re[1] & 0x80) && !plain && (uint32_t)offset + 1 < sm->n_remap) {
+              re += 4;
+              add_len = re[1] & ~0x80;
+            }
             int string_offset = re[2] | (re[3] << 8);
             uint8_t* newdst = dst - del_len + add_len;
             if ((dstlimit - newdst) < (srclimit - src)) { e = kExitDstSpaceFull; break; }
@@ -465,12 +475,197 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen)
   return total_filled;
 }
 
+/* ------------------------------------------------------------ HTML mode */
+/* IsSpecial (getonescriptspan.cc:470-477): < > & */
+static int is_special(uint8_t c) { return c == '<' || c == '>' || c == '&'; }
+
+/* ScanToPossibleLetter (getonescriptspan.cc:150-203, 503-541): the cheap tag
+ * parser, restated as a transition function over the reference's byte
+ * classes.  It advances over <tag>, <!-- ... -->, <script ...> ... </script>
+ * and <style ...> ... </style> (quotes inside tags respected, CR/LF ends a
+ * quoted string); state 0 / 1 exit (1 = '<' seen inside a tag).  Pinned
+ * against the reference's own function by tests/test_html_hints.py. */
+enum { TC_LT, TC_GT, TC_EX, TC_HY, TC_QU, TC_AP, TC_SL, TC_S, TC_C, TC_R, TC_I, TC_P, TC_T, TC_Y, TC_L, TC_E,
+       TC_CR, TC_NL, TC_PL };
+static int tag_class(uint8_t c) {
+  switch (c) {
+    case '<': return TC_LT; case '>': return TC_GT; case '!': return TC_EX; case '-': return TC_HY;
+    case '"': return TC_QU; case '\'': return TC_AP; case '/': return TC_SL; case '\n': case '\r': return TC_CR;
+    case '&': case '@': case '`': return TC_PL;
+    default: break;
+  }
+  if ((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z')) {
+    switch (c | 0x20) {
+      case 's': return TC_S; case 'c': return TC_C; case 'r': return TC_R; case 'i': return TC_I;
+      case 'p': return TC_P; case 't': return TC_T; case 'y': return TC_Y; case 'l': return TC_L;
+      case 'e': return TC_E; default: return TC_PL;
+    }
+  }
+  return c >= 0xC0 ? TC_PL : TC_NL;
+}
+/* inside "<...": '<' is an error exit, '>' ends the tag, quotes open strings */
+static int tag_common(int k, int other) {
+  return k == TC_LT ? 1 : k == TC_GT ? 2 : k == TC_QU ? 10 : k == TC_AP ? 11 : other;
+}
+static int tag_next(int s, int k) {
+#define TAG_COMMON(other) return tag_common(k, other)
+  switch (s) {
+    case 0: case 2: return k == TC_LT ? 3 : (k >= TC_S && k <= TC_E) || k == TC_PL ? 0 : 2;
+    case 3: if (k == TC_EX) return 4; if (k == TC_S) return 13; if (k == TC_HY || k == TC_SL) return 9; TAG_COMMON(9);
+    case 4: if (k == TC_HY) return 5; TAG_COMMON(9);
+    case 5: if (k == TC_HY) return 6; TAG_COMMON(9);
+    case 6: return k == TC_HY ? 7 : 6;
+    case 7: return k == TC_HY ? 8 : 6;
+    case 8: return k == TC_GT ? 2 : k == TC_HY ? 8 : 6;
+    case 9: TAG_COMMON(9);
+    case 10: return k == TC_QU ? 9 : k == TC_CR ? 12 : 10;
+    case 11: return k == TC_AP ? 9 : k == TC_CR ? 12 : 11;
+    case 12: return k == TC_LT ? 1 : k == TC_GT ? 2 : 12;
+    case 13: if (k == TC_C) return 14; if (k == TC_T) return 28; TAG_COMMON(9);
+    case 14: if (k == TC_R) return 15; TAG_COMMON(9);
+    case 15: if (k == TC_I) return 16; TAG_COMMON(9);
+    case 16: if (k == TC_P) return 17; TAG_COMMON(9);
+    case 17: if (k == TC_T) return 18; TAG_COMMON(9);
+    case 18: if (k == TC_GT || k == TC_CR || k == TC_NL) return 19; TAG_COMMON(9);
+    case 19: return k == TC_LT ? 20 : 19;
+    case 20: return k == TC_SL ? 21 : 19;
+    case 21: return k == TC_S ? 22 : (k == TC_CR || k == TC_NL) ? 21 : 19;
+    case 22: return k == TC_C ? 23 : 19;
+    case 23: return k == TC_R ? 24 : 19;
+    case 24: return k == TC_I ? 25 : 19;
+    case 25: return k == TC_P ? 26 : 19;
+    case 26: return k == TC_T ? 27 : 19;
+    case 27: return k == TC_GT ? 2 : 19;
+    case 28: if (k == TC_Y) return 29; TAG_COMMON(9);
+    case 29: if (k == TC_L) return 30; TAG_COMMON(9);
+    case 30: if (k == TC_E) return 31; TAG_COMMON(9);
+    case 31: if (k == TC_GT || k == TC_CR || k == TC_NL) return 32; TAG_COMMON(9);
+    case 32: return k == TC_LT ? 33 : 32;
+    case 33: return k == TC_SL ? 34 : 32;
+    case 34: return k == TC_S ? 35 : (k == TC_CR || k == TC_NL) ? 34 : 32;
+    case 35: return k == TC_T ? 36 : 32;
+    case 36: return k == TC_Y ? 37 : 32;
+    case 37: return k == TC_L ? 38 : 32;
+    case 38: return k == TC_E ? 39 : 32;
+    case 39: return k == TC_GT ? 2 : 32;
+    default: return 1;
+  }
+#undef TAG_COMMON
+}
+static int scan_to_possible_letter(const uint8_t* isrc, int len) {
+  const uint8_t* src = isrc;
+  const uint8_t* lim = isrc + len;
+  int s = 0, e = 0;
+  while (src < lim) {
+    e = tag_next(s, tag_class(*src++));
+    if (e <= 1) { --src; break; }      /* kMaxExitStateLettersMarksOnly: overshot by one byte */
+    s = e;
+  }
+  if (src >= lim) return len;           /* fell off the end: pretend the last byte was '>' */
+  if (e != 0 && e != 2) {               /* '<' inside a tag: just past the first, unmatched '<' */
+    int off = (int)(src - isrc) - 1;
+    while (0 < off && isrc[off] != '<') --off;
+    return off + 1;
+  }
+  return (int)(src - isrc);
+}
+
+/* FixUnicodeValue (fixunicodevalue.cc) */
+static int32_t fix_unicode_value(int32_t uv) {
+  uint32_t u = (uint32_t)uv;
+  if (u < 0x100) return T.cp1252 ? (int32_t)T.cp1252[u] : uv;
+  if (u < 0xD800) return uv;
+  if ((u & ~0x0Fu) == 0xFDD0 || (u & ~0x0Fu) == 0xFDE0 || (u & 0xFFFEu) == 0xFFFE) return 0xFFFD;
+  if (0xE000 <= u && u <= 0x10FFFF) return uv;
+  return 0xFFFD;
+}
+static int is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+static int is_xdigit(uint8_t c) { return is_digit(c) || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+static int is_alnum(uint8_t c) { return is_digit(c) || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'); }
+static int xdigit_val(uint8_t c) { return is_digit(c) ? c - '0' : (c | 0x20) - 'a' + 10; }
+/* strto32_base10 / _base16 (getonescriptspan.cc:325-391), quirks kept: a
+ * 9-digit decimal or an 8-digit hex >= 0x80000000 is U+FFFD */
+static int32_t entity_number(const uint8_t* p, const uint8_t* lim, int hex, const uint8_t** endp) {
+  *endp = p;
+  while (p < lim && *p == '0') ++p;
+  if (p == lim || !(hex ? is_xdigit(*p) : is_digit(*p))) return -1;
+  const uint8_t* e = p;
+  while (e < lim && (hex ? is_xdigit(*e) : is_digit(*e))) ++e;
+  *endp = e;
+  const int n = (int)(e - p);
+  int fits = hex ? (n < 8 || (n == 8 && p[0] < '8')) : (n < 9 || (n == 10 && memcmp(p, "2147483647", 10) <= 0));
+  if (!fits) return 0xFFFD;
+  int32_t v = 0;
+  for (; p < e; ++p) v = hex ? (int32_t)(((uint32_t)v << 4) + (uint32_t)xdigit_val(*p)) : v * 10 + (*p - '0');
+  return fix_unicode_value(v);
+}
+/* LookupEntity (:292-300): binary search over the sorted entity names */
+static int32_t lookup_entity(const uint8_t* name, int n) {
+  if (n >= 16 || !T.ent_names) return -1;
+  char key[16];
+  memcpy(key, name, (size_t)n); key[n] = 0;
+  int lo = 0, hi = (int)T.n_ent;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    int c = strcmp(str_at(T.ent_names, (uint32_t)mid), key);
+    if (c < 0) lo = mid + 1; else if (c > 0) hi = mid; else return T.ent_values[mid];
+  }
+  return -1;
+}
+/* ReadEntity (:393-451): value, or -1 with *consumed = 1 */
+static int32_t read_entity(const uint8_t* src, int srcn, int* consumed) {
+  const uint8_t* end = src + srcn;
+  if (srcn == 0 || *src != '&') { *consumed = 0; return -1; }
+  *consumed = 1;
+  const uint8_t* st = src + 1;
+  const uint8_t* en;
+  int32_t v;
+  if (st < end && *st == '#') {
+    if (st + 2 >= end) return -1;
+    if (st[1] == 'x' || st[1] == 'X') v = entity_number(st + 2, end, 1, &en);
+    else v = entity_number(st + 1, end, 0, &en);
+    if (v == -1 || en > end) return -1;
+  } else {
+    for (en = st; en < end && is_alnum(*en); ++en) {}
+    v = lookup_entity(st, (int)(en - st));
+    if (v < 0) return -1;
+    if (v >= 256 && !(en < end && *en == ';')) return -1;
+  }
+  if (en < end && *en == ';') ++en;
+  *consumed = (int)(en - src);
+  return v;
+}
+/* runetochar (:249-286) */
+static int rune_to_utf8(uint8_t* s, uint32_t c) {
+  if (c <= 0x7F) { s[0] = (uint8_t)c; return 1; }
+  if (c <= 0x7FF) { s[0] = (uint8_t)(0xC0 | (c >> 6)); s[1] = (uint8_t)(0x80 | (c & 0x3F)); return 2; }
+  if (c > 0x10FFFF) c = 0xFFFD;
+  if (c <= 0xFFFF) {
+    s[0] = (uint8_t)(0xE0 | (c >> 12)); s[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); s[2] = (uint8_t)(0x80 | (c & 0x3F));
+    return 3;
+  }
+  s[0] = (uint8_t)(0xF0 | (c >> 18)); s[1] = (uint8_t)(0x80 | ((c >> 12) & 0x3F));
+  s[2] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); s[3] = (uint8_t)(0x80 | (c & 0x3F));
+  return 4;
+}
+/* EntityToBuffer (:454-468): take / put byte counts */
+static void entity_to_buffer(const uint8_t* src, int len, uint8_t* dst, int* tlen, int* plen) {
+  int32_t v = read_entity(src, len, tlen);
+  if (v > 0) {
+    *plen = rune_to_utf8(dst, (uint32_t)v);
+  } else {
+    *tlen = 1;
+    *plen = 0;
+  }
+}
+
 /* ------------------------------------------------------------- scanner */
 typedef struct {
   const uint8_t* buf;       /* document, followed by >= 8 NUL bytes */
   int next, remaining;      /* next_byte_ - start_byte_, byte_length_ */
   uint8_t* sbuf;            /* script_buffer_       kMaxScriptBuffer + pad */
   uint8_t* lbuf;            /* script_buffer_lower_ kMaxScriptLowerBuffer + pad */
+  int plain;                /* is_plain_text_ */
 } scanner_t;
 
 typedef struct {
@@ -478,14 +673,28 @@ typedef struct {
   int text_bytes, offset, ulscript;
 } span_t;
 
-/* ScriptScanner::SkipToFrontOfSpan, plain-text branch, getonescriptspan.cc:592-642 */
-static int skip_to_front_of_span(const uint8_t* src, int len, int* script) {
-  int sc = 0, skip = 0, tlen;
+/* ScriptScanner::SkipToFrontOfSpan, getonescriptspan.cc:592-642 */
+static int skip_to_front_of_span(const uint8_t* src, int len, int* script, int plain) {
+  int sc = 0, skip = 0, tlen = 0, plen = 0;
   while (skip < len) {
     skip += scan_to_letter_or_special(src + skip, len - skip);
     if (skip >= len) { *script = sc; return len; }
-    tlen = utf8_len(src[skip]);
-    sc = script_num(src + skip);
+    if (!plain && is_special(src[skip])) {
+      if (src[skip] == '<') {
+        tlen = scan_to_possible_letter(src + skip, len - skip);
+        sc = 0;
+      } else if (src[skip] == '>') {
+        tlen = 1;
+        sc = 0;
+      } else {                                  /* '&': expand, no advance */
+        uint8_t tmp[8] = {0};
+        entity_to_buffer(src + skip, len - skip, tmp, &tlen, &plen);
+        if (plen > 0) sc = script_num(tmp);
+      }
+    } else {
+      tlen = utf8_len(src[skip]);
+      sc = script_num(src + skip);
+    }
     if (sc != 0) break;
     skip += tlen;
   }
@@ -493,9 +702,11 @@ static int skip_to_front_of_span(const uint8_t* src, int len, int* script) {
   return skip;
 }
 
-/* ScriptScanner::GetOneScriptSpan, plain text, getonescriptspan.cc:799-1027 */
+/* ScriptScanner::GetOneScriptSpan, getonescriptspan.cc:799-1027; HTML mode
+ * (plain == 0) skips tags and decodes entities into the span. */
 static int get_one_script_span(scanner_t* ss, span_t* span) {
   const int common = (int)T.meta.ulscript_common, inherited = (int)T.meta.ulscript_inherited;
+  const int plain = ss->plain;
   span->text = ss->sbuf; span->text_bytes = 0; span->offset = ss->next; span->ulscript = 0;
   int put_soft_limit = kMaxScriptBytes - kWithinScriptTail;
   if (kMaxScriptBytes <= ss->remaining && ss->remaining < 2 * kMaxScriptBytes)
@@ -504,7 +715,7 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
   uint8_t* sb = ss->sbuf;
   sb[0] = ' '; sb[1] = 0;
   int take = 0, put = 1;
-  int skip = skip_to_front_of_span(ss->buf + ss->next, ss->remaining, &spanscript);
+  int skip = skip_to_front_of_span(ss->buf + ss->next, ss->remaining, &spanscript, plain);
   ss->next += skip; ss->remaining -= skip;
   if (ss->remaining <= 0) return 0;
   span->ulscript = spanscript;
@@ -513,10 +724,16 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
   while (take < bl) {
     int need_break = 0;
     while (take < bl) {
-      tlen = plen = utf8_len(nb[take]);
-      if (take < bl - 3) memcpy(sb + put, nb + take, 4);
-      else memcpy(sb + put, nb + take, (size_t)plen);
-      sc = script_num(nb + take);
+      if (!plain && is_special(nb[take])) {
+        if (nb[take] == '<' || nb[take] == '>') { sc = 0; break; }
+        entity_to_buffer(nb + take, bl - take, sb + put, &tlen, &plen);   /* '&': copy entity, no advance */
+        if (plen > 0) sc = script_num(sb + put);
+      } else {
+        tlen = plen = utf8_len(nb[take]);
+        if (take < bl - 3) memcpy(sb + put, nb + take, 4);
+        else memcpy(sb + put, nb + take, (size_t)plen);
+        sc = script_num(nb + take);
+      }
       if (sc != spanscript && sc != inherited) {
         if (sc == common) {
           need_break = 1;
@@ -533,8 +750,21 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
       tlen = scan_to_letter_or_special(nb + take, bl - take);
       take += tlen;
       if (take >= bl) break;
-      tlen = utf8_len(nb[take]);
-      sc = script_num(nb + take);
+      if (!plain && is_special(nb[take])) {
+        if (nb[take] == '<') {
+          tlen = scan_to_possible_letter(nb + take, bl - take);
+          sc = 0;
+        } else if (nb[take] == '>') {
+          tlen = 1;
+          sc = 0;
+        } else {                                /* '&': expand, no advance */
+          entity_to_buffer(nb + take, bl - take, sb + put, &tlen, &plen);
+          if (plen > 0) sc = script_num(sb + put);
+        }
+      } else {
+        tlen = utf8_len(nb[take]);
+        sc = script_num(nb + take);
+      }
       if (sc != 0) break;
       take += tlen;
     }
@@ -551,7 +781,7 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
 
 /* ScriptScanner::LowerScriptSpan getonescriptspan.cc:1033-1054 */
 static void lower_script_span(scanner_t* ss, span_t* span) {
-  int filled = lower_replace(span->text, span->text_bytes + 3, ss->lbuf, kMaxScriptLowerBuffer);
+  int filled = lower_replace(span->text, span->text_bytes + 3, ss->lbuf, kMaxScriptLowerBuffer, ss->plain);
   ss->lbuf[filled] = 0;
   /* bytes past `filled` are never semantically read (masked hash loads,
    * NUL-stopped advances); keep them NUL so invalid input is deterministic */
@@ -802,6 +1032,8 @@ typedef struct { int n; uint32_t lp[kMaxBoosts]; } boosts_t;
 typedef struct {
   int ulscript;
   boosts_t distinct_latn, distinct_othr;   /* ScoringContext::distinct_boost */
+  uint32_t prior_boost[2][kMaxBoosts];     /* ScoringContext::langprior_boost latn / othr (ApplyHints) */
+  uint32_t prior_whack[2][kMaxBoosts];     /* ScoringContext::langprior_whack latn / othr */
 } ctx_t;
 
 typedef struct { int offset, indirect; } hit_t;
@@ -827,6 +1059,8 @@ struct cldo_ctx {
   uint8_t* docbuf; int docbuf_cap;
   cldo_trace_fn trace; void* trace_arg;
   int trace_text;                              /* also trace each lowered span's bytes (hex) */
+  int plain;                                   /* is_plain_text (HTML mode when 0) */
+  uint32_t priors[16];                         /* ApplyHints result: boost latn[4] othr[4], whack latn[4] othr[4] */
 };
 
 static void tracef(struct cldo_ctx* c, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -1236,7 +1470,12 @@ static void score_one_chunk(ctx_t* cx, const hitbuf_t* hb, int ci, int ulscript,
     if (hb->linear[i].type <= QUADHIT) t.score_count++;
     if (hb->linear[i].type == DISTINCTHIT) { db->lp[db->n] = lp; db->n = (db->n + 1) & (kMaxBoosts - 1); }
   }
+  /* ScoreBoosts (scoreonescriptspan.cc:125-152): prior boosts, distinct boosts, then whacks */
+  const int so = ((uint32_t)cx->ulscript == T.meta.ulscript_latin) ? 0 : 1;
+  for (int k = 0; k < kMaxBoosts; ++k) if (cx->prior_boost[so][k] > 0) add_lang_prob(cx->prior_boost[so][k], &t);
   for (int k = 0; k < kMaxBoosts; ++k) if (db->lp[k] > 0) add_lang_prob(db->lp[k], &t);
+  for (int k = 0; k < kMaxBoosts; ++k)
+    if (cx->prior_whack[so][k] > 0) t.score[(cx->prior_whack[so][k] >> 8) & 0xFF] = 0;   /* ZeroPSLang :39-42 */
   int lo = hb->linear[f].offset, hi = hb->linear[fn].offset;
   set_chunk_summary(ulscript, f, lo, hi - lo, &t, cs);
 }
@@ -1511,8 +1750,10 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
     if (len == 0) return unk;
     doctote_t dt; doctote_init(&dt);
     ctx_t cx; memset(&cx, 0, sizeof(cx));
+    memcpy(cx.prior_boost, c->priors, 8 * sizeof(uint32_t));
+    memcpy(cx.prior_whack, c->priors + 8, 8 * sizeof(uint32_t));
     scanner_t* ss = &c->ss;
-    ss->buf = buf; ss->next = 0; ss->remaining = len;
+    ss->buf = buf; ss->next = 0; ss->remaining = len; ss->plain = c->plain;
     int hash = 0;
     if (flags & kCLDFlagRepeats) memset(c->predict, 0, sizeof(c->predict));
     int total = 0, restart = 0;
@@ -1591,6 +1832,7 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
 /* ---------------------------------------------------------------- API */
 cldo_ctx* cldo_ctx_new(void) {
   cldo_ctx* c = (cldo_ctx*)calloc(1, sizeof(cldo_ctx));
+  c->plain = 1;
   c->ss.sbuf = (uint8_t*)calloc(kMaxScriptBuffer + 64, 1);
   c->ss.lbuf = (uint8_t*)calloc(kMaxScriptLowerBuffer + 64, 1);
   return c;
@@ -1638,23 +1880,46 @@ int cldo_meta(int which) {
 
 /* Batch: n documents, threads > 1 splits them over pthreads (CPU baseline). */
 #include <pthread.h>
-typedef struct { const char* buf; const uint64_t* offs; int lo, hi; cldo_result* out; } job_t;
+typedef struct {
+  const char* buf; const uint64_t* offs; int lo, hi; cldo_result* out;
+  const uint8_t* plain; const uint32_t* priors;
+} job_t;
+int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
+                         const uint32_t* priors, cldo_result* out, int threads);
+/* DetectLanguageSummaryV2 with is_plain_text and the ApplyHints result
+ * (compact_lang_det_impl.cc:1587-1684) given: priors = 16 langprobs, boost
+ * latn[4] othr[4], whack latn[4] othr[4] (NULL: none). */
+int cldo_detect_ex(cldo_ctx* c, const char* text, int len, int is_plain_text, const uint32_t* priors,
+                   cldo_result* r) {
+  c->plain = is_plain_text ? 1 : 0;
+  if (priors) memcpy(c->priors, priors, sizeof(c->priors));
+  else memset(c->priors, 0, sizeof(c->priors));
+  int lang = cldo_detect(c, text, len, r);
+  c->plain = 1;
+  memset(c->priors, 0, sizeof(c->priors));
+  return lang;
+}
 static void* run_job(void* a) {
   job_t* j = (job_t*)a;
   cldo_ctx* c = cldo_ctx_new();
   for (int i = j->lo; i < j->hi; ++i)
-    cldo_detect(c, j->buf + j->offs[i], (int)(j->offs[i + 1] - j->offs[i]), &j->out[i]);
+    cldo_detect_ex(c, j->buf + j->offs[i], (int)(j->offs[i + 1] - j->offs[i]),
+                   j->plain ? j->plain[i] : 1, j->priors ? j->priors + 16 * (size_t)i : NULL, &j->out[i]);
   cldo_ctx_free(c);
   return NULL;
 }
 int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_result* out, int threads) {
+  return cldo_detect_batch_ex(buf, offsets, n, NULL, NULL, out, threads);
+}
+int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
+                         const uint32_t* priors, cldo_result* out, int threads) {
   if (!T.loaded) return -1;
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   pthread_t th[256];
   job_t jobs[256];
   for (int t = 0; t < threads; ++t) {
-    jobs[t].buf = buf; jobs[t].offs = offsets; jobs[t].out = out;
+    jobs[t].buf = buf; jobs[t].offs = offsets; jobs[t].out = out; jobs[t].plain = plain; jobs[t].priors = priors;
     jobs[t].lo = (int)((int64_t)n * t / threads); jobs[t].hi = (int)((int64_t)n * (t + 1) / threads);
     pthread_create(&th[t], NULL, run_job, &jobs[t]);
   }
@@ -1753,8 +2018,38 @@ uint32_t cldo_probe(int section, uint64_t h) {
   }
 }
 
+/* Test hooks for the HTML-mode pins (tests/test_html_hints.py): the span
+ * scanner + lowercaser alone (one callback line "<ulscript> <hex>" per span),
+ * the tag parser and the entity reader. */
+int cldo_scan_spans(const char* text, int len, int is_plain_text, cldo_trace_fn fn, void* arg) {
+  if (!T.loaded) return -1;
+  cldo_ctx* c = cldo_ctx_new();
+  uint8_t* doc = (uint8_t*)calloc((size_t)len + 16, 1);
+  memcpy(doc, text, (size_t)len);
+  scanner_t* ss = &c->ss;
+  ss->buf = doc; ss->next = 0; ss->remaining = len; ss->plain = is_plain_text ? 1 : 0;
+  span_t span;
+  int n = 0;
+  while (get_one_script_span(ss, &span)) {
+    lower_script_span(ss, &span);
+    char* line = (char*)malloc(2 * (size_t)span.text_bytes + 32);
+    int o = sprintf(line, "%d ", span.ulscript);
+    for (int i = 0; i < span.text_bytes; ++i) o += sprintf(line + o, "%02x", span.text[i]);
+    fn(arg, line);
+    free(line);
+    ++n;
+  }
+  free(doc);
+  cldo_ctx_free(c);
+  return n;
+}
+int cldo_scan_tag(const char* text, int len) { return scan_to_possible_letter((const uint8_t*)text, len); }
+int cldo_read_entity(const char* text, int len, int* consumed) {
+  return read_entity((const uint8_t*)text, len, consumed);
+}
+
 int cldo_lower(const char* in, int len, char* out, int olen) {
-  return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen);
+  return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen, 1);
 }
 int cldo_script_num(const char* s) { return script_num((const uint8_t*)s); }
 

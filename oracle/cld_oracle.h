@@ -35,6 +35,13 @@ void cldo_set_trace_text(cldo_ctx* c, int on);   /* trace lines "lowered <flags>
 int cldo_detect(cldo_ctx* c, const char* text, int len, cldo_result* r);
 const char* cldo_detect_language(cldo_ctx* c, const char* text);
 int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_result* out, int threads);
+/* is_plain_text = 0: HTML mode (tags skipped, entities decoded).  priors: the
+ * ApplyHints result as 16 langprobs (boost latn[4], othr[4], whack latn[4],
+ * othr[4]), NULL for none; batch forms take one flag / 16 priors per document. */
+int cldo_detect_ex(cldo_ctx* c, const char* text, int len, int is_plain_text, const uint32_t* priors,
+                   cldo_result* r);
+int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
+                         const uint32_t* priors, cldo_result* out, int threads);
 /* handlers.go:150-151 text preparation: flags 1 = StripExtras, 2 = C-string cut.
  * out capacity: offsets[n]-offsets[0] + n bytes. */
 int cldo_prepare_batch(const char* buf, const uint64_t* offsets, int n, int flags, char* out,
@@ -52,6 +59,9 @@ int cldo_score_chunks(int ulscript, const uint16_t* offsets, const uint8_t* type
 
 int cldo_lower(const char* in, int len, char* out, int olen);
 uint64_t cldo_gram_hash(int kind, const char* w, int n);   /* 0 quad, 1 bi, 2 octa */
+int cldo_scan_spans(const char* text, int len, int is_plain_text, cldo_trace_fn fn, void* arg);
+int cldo_scan_tag(const char* text, int len);
+int cldo_read_entity(const char* text, int len, int* consumed);
 uint64_t cldo_pair_hash(uint64_t a, uint64_t b);
 uint32_t cldo_probe(int cldt_section, uint64_t hash);
 int cldo_script_num(const char* s);

@@ -166,7 +166,8 @@ def main():
             "QUAD/QUAD2 = SYNTHETIC Q1 built by tools/synth_quad.py from the octa-table "
             "training tokens (%d langs, %d words, %d quads: %d single, %d double; "
             "table1 %d buckets, table2 %d buckets, %d spilled, %d dropped). "
-            "Real quadchrome_2 is a missing blob." % (
+            "Real quadchrome_2 is a missing blob. HTML entities, cp1252 fix and hint tables: "
+            "oracle/tablegen/extract_html_hint_tables.cc." % (
                 len(vocab), sum(len(v) for v in vocab.values()), len(entries),
                 len(singles), len(doubles), QUAD1_BUCKETS, QUAD2_BUCKETS, len(spill), len(dropped)))
 
