@@ -52,6 +52,20 @@ typedef struct cld_result {
  * request item of POST / (handlers.go:150-151). */
 #define CLD_FLAG_STRIP_EXTRAS 1u
 #define CLD_FLAG_CSTRING 2u
+/* is_plain_text = false: the documents are HTML -- tags, comments, <script>
+ * and <style> bodies are skipped and entities decoded by the span scanner
+ * (getonescriptspan.cc:150-541, 592-1027), lang= attributes in the first 8 KB
+ * become hints (compact_lang_det_impl.cc:1596-1611). */
+#define CLD_FLAG_HTML 4u
+
+/* CLDHints (compact_lang_det.h:134-139): per-document priors. */
+typedef struct cld_hints {
+  const char* content_language_hint;  /* "mi,en" boosts Maori and English; NULL / "" for none */
+  const char* tld_hint;               /* "id" boosts Indonesian; NULL / "" for none */
+  int32_t encoding_hint;              /* Encoding enum (encodings.h); CLD_UNKNOWN_ENCODING for none */
+  int32_t language_hint;              /* Language enum; 26 (UNKNOWN_LANGUAGE) for none */
+} cld_hints;
+#define CLD_UNKNOWN_ENCODING 23
 
 /* wrapper.h:8 -- returns a static ISO code; never NULL; UNKNOWN -> "en"
  * (compact_lang_det.cc:91-93).  Input is NUL-terminated, length = strlen
@@ -107,6 +121,22 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
                      cld_result* out, uint32_t flags);
+
+/* ExtDetectLanguageSummary (compact_lang_det.h:261-294 / impl.cc:1707) over a
+ * batch: `hints` is NULL or one cld_hints per document; flags may add
+ * CLD_FLAG_HTML (all documents are HTML) to the preparation flags.  Documents
+ * that are HTML or carry a hint run the exact sequential kernel; results
+ * are the same fields as cld_detect_batch.  Host buffers; blocks. */
+int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
+                        uint32_t flags, cld_result* out);
+
+/* Host-only (no GPU): the ApplyHints result for one document.  priors: the
+ * CLDLangPriors (OneCLDLangPrior = (weight << 10) + Language, at most 14)
+ * after TrimCLDLangPriors(4); boosts16: prior boosts latn[4], othr[4] and
+ * close-language whacks latn[4], othr[4] as langprobs.  Returns the prior
+ * count, or a negative error.  doc may be NULL unless is_plain_text = 0. */
+int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld_hints* hints,
+                    int16_t* priors14, uint32_t* boosts16);
 
 /* Same, with every pointer in device memory of GPU `device` and work
  * enqueued on `stream` (a hipStream_t, NULL = the runtime's stream for that

@@ -22,6 +22,9 @@ Q0_TABLES = os.path.join(HERE, "data", "cld2_q0.cldt")
 SYNTH_TABLES = os.path.join(HERE, "data", "cld2_synth_q1.cldt")
 FLAG_STRIP_EXTRAS = 1      # include/cld_mi355x.h CLD_FLAG_STRIP_EXTRAS
 FLAG_CSTRING = 2           # include/cld_mi355x.h CLD_FLAG_CSTRING
+FLAG_HTML = 4              # include/cld_mi355x.h CLD_FLAG_HTML (cld_detect_batch_ex)
+UNKNOWN_ENCODING = 23      # encodings.h UNKNOWN_ENCODING
+UNKNOWN_LANGUAGE = 26      # generated_language.h UNKNOWN_LANGUAGE
 
 RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "i1", 3),
                          ("is_reliable", "u1"), ("text_bytes", "<i4"), ("normalized3", "<f8", 3)])
@@ -34,7 +37,18 @@ EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cl
            "cld_load_data_from_file", "cld_load_data_from_raw_address", "cld_unload_data",
            "cld_is_data_dynamic", "cld_export_tables", "cld_convert_data_file",
            "cld_detect_batch_device_ex", "cld_prepare_batch", "cld_host_alloc", "cld_host_free",
-           "cld_kernel_times")
+           "cld_kernel_times", "cld_detect_batch_ex", "cld_hint_priors")
+
+
+class Hints(ctypes.Structure):
+    """CLDHints (compact_lang_det.h:134-139) = include/cld_mi355x.h cld_hints."""
+    _fields_ = [("content_language_hint", ctypes.c_char_p), ("tld_hint", ctypes.c_char_p),
+                ("encoding_hint", ctypes.c_int32), ("language_hint", ctypes.c_int32)]
+
+    @classmethod
+    def make(cls, content_language=None, tld=None, encoding=UNKNOWN_ENCODING, language=UNKNOWN_LANGUAGE):
+        enc = lambda v: v.encode() if isinstance(v, str) else v
+        return cls(enc(content_language), enc(tld), encoding, language)
 
 
 class BatchStats(ctypes.Structure):
@@ -88,6 +102,10 @@ def lib():
         L.cld_host_alloc.argtypes = [ctypes.c_size_t]
         L.cld_host_alloc.restype = ctypes.c_void_p
         L.cld_host_free.argtypes = [ctypes.c_void_p]
+        L.cld_detect_batch_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_void_p]
+        L.cld_hint_priors.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(Hints),
+                                      ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -207,6 +225,46 @@ def detect_batch(docs=None, buf=None, offsets=None, flags=0):
     if rc != 0:
         raise CldError("cld_detect_batch failed: %d" % rc)
     return out
+
+
+def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False):
+    """ExtDetectLanguageSummary per document (compact_lang_det.h:261-294):
+    html=True scores every document as HTML (is_plain_text = false); hints is
+    None or one Hints per document."""
+    if docs is not None:
+        buf, offsets = pack(docs)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    if n == 0:
+        return out
+    harr = None
+    if hints is not None:
+        if len(hints) != n:
+            raise ValueError("need one Hints per document")
+        harr = (Hints * n)(*hints)
+    bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+    rc = lib().cld_detect_batch_ex(bptr, offsets.ctypes.data, n, ctypes.cast(harr, ctypes.c_void_p) if harr else None,
+                                   FLAG_HTML if html else 0, out.ctypes.data)
+    if rc != 0:
+        raise CldError("cld_detect_batch_ex failed: %d" % rc)
+    return out
+
+
+def hint_priors(doc=b"", html=False, hints=None):
+    """Host-only ApplyHints (compact_lang_det_impl.cc:1587-1684): (priors, boosts16).
+    priors: the trimmed CLDLangPriors as int16 (weight << 10) + language;
+    boosts16: prior boosts latn[4] othr[4], whacks latn[4] othr[4] as langprobs."""
+    b = doc.encode() if isinstance(doc, str) else bytes(doc)
+    p = np.zeros(14, dtype=np.int16)
+    q = np.zeros(16, dtype=np.uint32)
+    cb = ctypes.create_string_buffer(b, len(b) + 1)
+    rc = lib().cld_hint_priors(cb, len(b), 0 if html else 1, ctypes.byref(hints) if hints is not None else None,
+                               p.ctypes.data, q.ctypes.data)
+    if rc < 0:
+        raise CldError("cld_hint_priors failed: %d" % rc)
+    return p[:rc].copy(), q
 
 
 def detect_batch_device(device, d_buf_ptr, d_offsets_ptr, n, d_out_ptr, stream_ptr=None):

@@ -36,6 +36,10 @@ struct DevTables {
   const uint16_t* closest;
   const uint64_t* cpt;        // per-character properties of 1-3 byte sequences (cld_long.hip, built on device)
   const uint8_t* close_set;
+  const uint8_t* ent_names;   // HTML mode: entity name string section (CLDT_ENTITY_NAMES), or null
+  const int32_t* ent_values;  //   and their code points
+  const uint32_t* cp1252;     //   FixUnicodeValue below U+0100
+  uint32_t n_ent;
   uint32_t n_expected, l2p_size, n_scripts, n_langs, n_closest;
   uint32_t latin, cyrillic, arabic, common, inherited;
   uint32_t unknown_lang, english, tg_unknown, french, italian, german, spanish, hawaiian;

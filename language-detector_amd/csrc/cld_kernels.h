@@ -21,28 +21,34 @@ constexpr int kShortSB = 2 * kShortCap + 64;
 constexpr int kShortLB = kShortSB * 3 / 2 + 64;
 constexpr int kShortHB = kShortCap + 32;
 
-// Device counter slots (one 64-byte line, zeroed per batch)
-// kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general.
+// Device counter slots (two 64-byte lines, zeroed per batch)
+// kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general;
+// kCtrSpecial: HTML / hinted documents the wave kernel sent straight to k_general.
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
        kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
-       kCtrSlots = 16 };
+       kCtrSpecial = 16, kCtrSlots = 32 };
+// Per-document routing bits of cld_detect_batch_ex (special[i])
+enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2 };
 // k_long: waves per workgroup
 constexpr int kLongWPB = 4;
 
 extern "C" {
 size_t cld_general_work_bytes();
 size_t cld_short_work_bytes();
+// special (nullable): per-document kSpecial* bits; such documents are appended
+// to special_list under counters[special_ctr] instead of being scored
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                           unsigned long long* prof, hipStream_t s);
+                           unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
+                           int special_ctr, hipStream_t s);
 size_t cld_wave_smem_bytes();
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                            hipStream_t s);
+                            const uint8_t* special, uint32_t* special_list, int special_ctr, hipStream_t s);
 hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              hipStream_t s);
+                              const uint8_t* special, const uint32_t* priors, hipStream_t s);
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
                                  uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s);
 size_t cld_long_slot_bytes();

@@ -25,9 +25,16 @@ __global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __res
                                               const uint64_t* __restrict__ offs, int n,
                                               cld_result* __restrict__ out,
                                               uint32_t* __restrict__ requeue_list,
-                                              uint32_t* __restrict__ counters) {
+                                              uint32_t* __restrict__ counters,
+                                              const uint8_t* __restrict__ special,
+                                              uint32_t* __restrict__ special_list, int special_ctr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (special && special[i]) {
+    special_list[atomicAdd(&counters[special_ctr], 1u)] = (uint32_t)i;
+    atomicAdd(&counters[kCtrSpecial], 1u);
+    return;
+  }
   const uint64_t a = offs[i], b = offs[i + 1];
   const int64_t len = (int64_t)(b - a);
   bool rq = len > kShortCap;
@@ -49,7 +56,9 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
                                                const uint32_t* __restrict__ list,
                                                cld_result* __restrict__ out,
                                                uint8_t* __restrict__ arena, uint64_t stride,
-                                               uint32_t* __restrict__ counters, int ctr_count, int ctr_deq) {
+                                               uint32_t* __restrict__ counters, int ctr_count, int ctr_deq,
+                                               const uint8_t* __restrict__ special,
+                                               const uint32_t* __restrict__ priors) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
   const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -64,7 +73,11 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
     const uint64_t a = offs[i], b = offs[i + 1];
     Status st{false};
     DocView d{buf + a, (int)(b - a)};
-    int passes = detect_doc(T, d, w, &out[i], st);
+    // cld_detect_batch_ex: HTML documents (special bit 0) and per-document
+    // ApplyHints priors (16 langprobs each, bit 1)
+    const uint8_t sp = special ? special[i] : 0;
+    int passes = detect_doc(T, d, w, &out[i], st, !(sp & kSpecialHtml),
+                            (sp & kSpecialPriors) ? priors + 16ull * i : nullptr);
     if (passes >= 1 && passes <= 3) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
     else atomicAdd(&counters[kCtrError], 1u);
   }
@@ -87,7 +100,9 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
                                                    cld_result* __restrict__ out,
                                                    uint32_t* __restrict__ requeue_list,
                                                    uint32_t* __restrict__ counters,
-                                                   unsigned long long* __restrict__ prof) {
+                                                   unsigned long long* __restrict__ prof,
+                                                   const uint8_t* __restrict__ special,
+                                                   uint32_t* __restrict__ special_list, int special_ctr) {
   __shared__ wave::Smem<CAP> smem[WPB];
   // wave index through readfirstlane: the document pointer, its length, the
   // result pointer and the LDS base are then scalars, not VGPRs live across
@@ -99,6 +114,14 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   const int per = ((n + WPB - 1) / WPB + 7) >> 3;          // blocks per XCD slice
   const int i = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * WPB + wv;
   if (i >= n) return;
+  // HTML / hinted documents go straight to k_general's list (cld_detect_batch_ex)
+  if (special && special[i]) {
+    if (lane == 0) {
+      special_list[atomicAdd(&counters[special_ctr], 1u)] = (uint32_t)i;
+      atomicAdd(&counters[kCtrSpecial], 1u);
+    }
+    return;
+  }
   const uint64_t a = offs[i], b = offs[i + 1];
   const int64_t len = (int64_t)(b - a);
   bool rq = len > CAP;
@@ -293,31 +316,33 @@ size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                           unsigned long long* prof, hipStream_t s) {
+                           unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
+                           int special_ctr, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
-                     requeue_list, counters, prof);
+                     requeue_list, counters, prof, special, special_list, special_ctr);
   return hipGetLastError();
 }
 
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                            hipStream_t s) {
+                            const uint8_t* special, uint32_t* special_list, int special_ctr, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   dim3 grid((n + 255) / 256), block(256);
-  hipLaunchKernelGGL(cld::k_short, grid, block, 0, s, *T, buf, offs, n, out, requeue_list, counters);
+  hipLaunchKernelGGL(cld::k_short, grid, block, 0, s, *T, buf, offs, n, out, requeue_list, counters, special,
+                     special_list, special_ctr);
   return hipGetLastError();
 }
 
 hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              hipStream_t s) {
+                              const uint8_t* special, const uint32_t* priors, hipStream_t s) {
   dim3 grid(lanes / 64), block(64);
   hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, *T, buf, offs, list, out, arena, stride,
-                     counters, ctr_count, ctr_deq);
+                     counters, ctr_count, ctr_deq, special, priors);
   return hipGetLastError();
 }
 }

@@ -182,7 +182,8 @@ __device__ int scan_to_letter_or_special(const DevTables& T, const DocView& d, i
 // `olen` is the reference's logical output capacity (kMaxScriptLowerBuffer);
 // the physical buffer only needs 1.5x the input (max per-char expansion of
 // this table, verified by tests/test_tables.py) plus padding.
-__device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, uint8_t* out0, int olen) {
+__device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
+                                bool plain = true) {
   const int sh = (int)sm.shift;
   const int nEntries = 1 << sh;
   int total_filled = 0;
@@ -246,6 +247,10 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
             const uint8_t* re = sm.remap + 4 * offset;
             int del_len = re[0] & 0x7F;
             int add_len = re[1] & 0x7F;
+            if ((re[1] & 0x80) && !plain && (uint32_t)offset + 1 < sm.n_remap) {   // HTML half of the pair (:755-762)
+              re += 4;
+              add_len = re[1] & 0x7F;
+            }
             int soff = re[2] | (re[3] << 8);
             uint8_t* newdst = dst - del_len + add_len;
             if ((dstlimit - newdst) < (srclimit - src)) { e = 239; again = false; break; }
@@ -286,8 +291,9 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
   return total_filled;
 }
 
-__device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen) {
-  return lower_replace_sm(T.lower, in0, ilen, out0, olen);
+__device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
+                                             bool plain = true) {
+  return lower_replace_sm(T.lower, in0, ilen, out0, olen, plain);
 }
 
 // ------------------------------------------------------------ lang/script
@@ -557,15 +563,236 @@ struct Span { uint8_t* text; int text_bytes; int ulscript; };
 // passes are needed: the document is re-queued for the general kernel.
 struct Status { bool requeue; };
 
+// ------------------------------------------------------------ HTML mode
+// IsSpecial (getonescriptspan.cc:470-477)
+__device__ __forceinline__ bool is_special(uint8_t c) { return c == '<' || c == '>' || c == '&'; }
+
+// ScanToPossibleLetter (getonescriptspan.cc:150-203, 503-541): the cheap tag
+// parser as a transition function over the reference's byte classes (the
+// same restatement the oracle pins against the reference, tests/test_html_hints.py).
+enum { TC_LT, TC_GT, TC_EX, TC_HY, TC_QU, TC_AP, TC_SL, TC_S, TC_C, TC_R, TC_I, TC_P, TC_T, TC_Y, TC_L, TC_E,
+       TC_CR, TC_NL, TC_PL };
+__device__ int tag_class(uint8_t c) {
+  switch (c) {
+    case '<': return TC_LT; case '>': return TC_GT; case '!': return TC_EX; case '-': return TC_HY;
+    case '"': return TC_QU; case '\'': return TC_AP; case '/': return TC_SL; case '\n': case '\r': return TC_CR;
+    case '&': case '@': case '`': return TC_PL;
+    default: break;
+  }
+  if ((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z')) {
+    switch (c | 0x20) {
+      case 's': return TC_S; case 'c': return TC_C; case 'r': return TC_R; case 'i': return TC_I;
+      case 'p': return TC_P; case 't': return TC_T; case 'y': return TC_Y; case 'l': return TC_L;
+      case 'e': return TC_E; default: return TC_PL;
+    }
+  }
+  return c >= 0xC0 ? TC_PL : TC_NL;
+}
+__device__ __forceinline__ int tag_common(int k, int other) {
+  return k == TC_LT ? 1 : k == TC_GT ? 2 : k == TC_QU ? 10 : k == TC_AP ? 11 : other;
+}
+__device__ int tag_next(int s, int k) {
+  switch (s) {
+    case 0: case 2: return k == TC_LT ? 3 : ((k >= TC_S && k <= TC_E) || k == TC_PL) ? 0 : 2;
+    case 3: return k == TC_EX ? 4 : k == TC_S ? 13 : (k == TC_HY || k == TC_SL) ? 9 : tag_common(k, 9);
+    case 4: return k == TC_HY ? 5 : tag_common(k, 9);
+    case 5: return k == TC_HY ? 6 : tag_common(k, 9);
+    case 6: return k == TC_HY ? 7 : 6;
+    case 7: return k == TC_HY ? 8 : 6;
+    case 8: return k == TC_GT ? 2 : k == TC_HY ? 8 : 6;
+    case 9: return tag_common(k, 9);
+    case 10: return k == TC_QU ? 9 : k == TC_CR ? 12 : 10;
+    case 11: return k == TC_AP ? 9 : k == TC_CR ? 12 : 11;
+    case 12: return k == TC_LT ? 1 : k == TC_GT ? 2 : 12;
+    case 13: return k == TC_C ? 14 : k == TC_T ? 28 : tag_common(k, 9);
+    case 14: return k == TC_R ? 15 : tag_common(k, 9);
+    case 15: return k == TC_I ? 16 : tag_common(k, 9);
+    case 16: return k == TC_P ? 17 : tag_common(k, 9);
+    case 17: return k == TC_T ? 18 : tag_common(k, 9);
+    case 18: return (k == TC_GT || k == TC_CR || k == TC_NL) ? 19 : tag_common(k, 9);
+    case 19: return k == TC_LT ? 20 : 19;
+    case 20: return k == TC_SL ? 21 : 19;
+    case 21: return k == TC_S ? 22 : (k == TC_CR || k == TC_NL) ? 21 : 19;
+    case 22: return k == TC_C ? 23 : 19;
+    case 23: return k == TC_R ? 24 : 19;
+    case 24: return k == TC_I ? 25 : 19;
+    case 25: return k == TC_P ? 26 : 19;
+    case 26: return k == TC_T ? 27 : 19;
+    case 27: return k == TC_GT ? 2 : 19;
+    case 28: return k == TC_Y ? 29 : tag_common(k, 9);
+    case 29: return k == TC_L ? 30 : tag_common(k, 9);
+    case 30: return k == TC_E ? 31 : tag_common(k, 9);
+    case 31: return (k == TC_GT || k == TC_CR || k == TC_NL) ? 32 : tag_common(k, 9);
+    case 32: return k == TC_LT ? 33 : 32;
+    case 33: return k == TC_SL ? 34 : 32;
+    case 34: return k == TC_S ? 35 : (k == TC_CR || k == TC_NL) ? 34 : 32;
+    case 35: return k == TC_T ? 36 : 32;
+    case 36: return k == TC_Y ? 37 : 32;
+    case 37: return k == TC_L ? 38 : 32;
+    case 38: return k == TC_E ? 39 : 32;
+    case 39: return k == TC_GT ? 2 : 32;
+    default: return 1;
+  }
+}
+__device__ int scan_to_possible_letter(const DocView& d, int start, int len) {
+  int src = start, e = 0, st = 0;
+  const int lim = start + len;
+  while (src < lim) {
+    e = tag_next(st, tag_class(d.at(src++)));
+    if (e <= 1) { --src; break; }
+    st = e;
+  }
+  if (src >= lim) return len;
+  if (e != 0 && e != 2) {
+    int off = src - start - 1;
+    while (0 < off && d.at(start + off) != '<') --off;
+    return off + 1;
+  }
+  return src - start;
+}
+// FixUnicodeValue (fixunicodevalue.cc)
+__device__ int32_t fix_unicode_value(const DevTables& T, int32_t uv) {
+  const uint32_t u = (uint32_t)uv;
+  if (u < 0x100) return T.cp1252 ? (int32_t)T.cp1252[u] : uv;
+  if (u < 0xD800) return uv;
+  if ((u & ~0x0Fu) == 0xFDD0 || (u & ~0x0Fu) == 0xFDE0 || (u & 0xFFFEu) == 0xFFFE) return 0xFFFD;
+  if (0xE000 <= u && u <= 0x10FFFF) return uv;
+  return 0xFFFD;
+}
+__device__ __forceinline__ bool is_digit_c(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool is_xdigit_c(uint8_t c) {
+  return is_digit_c(c) || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+}
+__device__ __forceinline__ bool is_alnum_c(uint8_t c) { return is_digit_c(c) || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'); }
+// strto32_base10 / _base16 (getonescriptspan.cc:325-391), quirks kept
+__device__ int32_t entity_number(const DevTables& T, const DocView& d, int p, int lim, bool hex, int* endp) {
+  *endp = p;
+  while (p < lim && d.at(p) == '0') ++p;
+  if (p == lim || !(hex ? is_xdigit_c(d.at(p)) : is_digit_c(d.at(p)))) return -1;
+  int e = p;
+  while (e < lim && (hex ? is_xdigit_c(d.at(e)) : is_digit_c(d.at(e)))) ++e;
+  *endp = e;
+  const int n = e - p;
+  bool fits;
+  if (hex) {
+    fits = n < 8 || (n == 8 && d.at(p) < '8');
+  } else {
+    fits = n < 9;
+    if (n == 10) {                                 // memcmp(p, "2147483647", 10) <= 0
+      const char* mx = "2147483647";
+      int c = 0;
+      for (int i = 0; i < 10 && c == 0; ++i) c = (int)d.at(p + i) - (int)(uint8_t)mx[i];
+      fits = c <= 0;
+    }
+  }
+  if (!fits) return 0xFFFD;
+  int32_t v = 0;
+  for (; p < e; ++p) {
+    const uint8_t c = d.at(p);
+    v = hex ? (int32_t)(((uint32_t)v << 4) + (uint32_t)(is_digit_c(c) ? c - '0' : (c | 0x20) - 'a' + 10))
+            : v * 10 + (c - '0');
+  }
+  return fix_unicode_value(T, v);
+}
+// LookupEntity (:292-300): binary search of the sorted entity names
+__device__ int32_t lookup_entity(const DevTables& T, const DocView& d, int p, int n) {
+  if (n >= 16 || !T.ent_names) return -1;
+  const uint32_t cnt = *reinterpret_cast<const uint32_t*>(T.ent_names);
+  const uint32_t* off = reinterpret_cast<const uint32_t*>(T.ent_names + 4);
+  const char* base = reinterpret_cast<const char*>(T.ent_names + 4 + 4 * (cnt + 1));
+  uint32_t lo = 0, hi = cnt;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const char* s = base + off[mid];
+    int c = 0, i = 0;
+    for (;; ++i) {                                 // strcmp(name, key)
+      const int a = (uint8_t)s[i], b = i < n ? d.at(p + i) : 0;
+      if (a != b || a == 0) { c = a - b; break; }
+    }
+    if (c < 0) lo = mid + 1;
+    else if (c > 0) hi = mid;
+    else return T.ent_values[mid];
+  }
+  return -1;
+}
+// ReadEntity (:393-451) at document position p, srcn bytes available
+__device__ int32_t read_entity(const DevTables& T, const DocView& d, int p, int srcn, int* consumed) {
+  const int end = p + srcn;
+  if (srcn == 0 || d.at(p) != '&') { *consumed = 0; return -1; }
+  *consumed = 1;
+  const int st = p + 1;
+  int en;
+  int32_t v;
+  if (st < end && d.at(st) == '#') {
+    if (st + 2 >= end) return -1;
+    const uint8_t x = d.at(st + 1);
+    v = (x == 'x' || x == 'X') ? entity_number(T, d, st + 2, end, true, &en) : entity_number(T, d, st + 1, end, false, &en);
+    if (v == -1 || en > end) return -1;
+  } else {
+    for (en = st; en < end && is_alnum_c(d.at(en)); ++en) {}
+    v = lookup_entity(T, d, st, en - st);
+    if (v < 0) return -1;
+    if (v >= 256 && !(en < end && d.at(en) == ';')) return -1;
+  }
+  if (en < end && d.at(en) == ';') ++en;
+  *consumed = en - p;
+  return v;
+}
+// runetochar (:249-286)
+__device__ int rune_to_utf8(uint8_t* s, uint32_t c) {
+  if (c <= 0x7F) { s[0] = (uint8_t)c; return 1; }
+  if (c <= 0x7FF) { s[0] = (uint8_t)(0xC0 | (c >> 6)); s[1] = (uint8_t)(0x80 | (c & 0x3F)); return 2; }
+  if (c > 0x10FFFF) c = 0xFFFD;
+  if (c <= 0xFFFF) {
+    s[0] = (uint8_t)(0xE0 | (c >> 12)); s[1] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); s[2] = (uint8_t)(0x80 | (c & 0x3F));
+    return 3;
+  }
+  s[0] = (uint8_t)(0xF0 | (c >> 18)); s[1] = (uint8_t)(0x80 | ((c >> 12) & 0x3F));
+  s[2] = (uint8_t)(0x80 | ((c >> 6) & 0x3F)); s[3] = (uint8_t)(0x80 | (c & 0x3F));
+  return 4;
+}
+// EntityToBuffer (:454-468)
+__device__ void entity_to_buffer(const DevTables& T, const DocView& d, int p, int len, uint8_t* dst, int* tlen,
+                                 int* plen) {
+  const int32_t v = read_entity(T, d, p, len, tlen);
+  if (v > 0) {
+    *plen = rune_to_utf8(dst, (uint32_t)v);
+  } else {
+    *tlen = 1;
+    *plen = 0;
+  }
+}
+// GetUTF8LetterScriptNum over a small local buffer (a decoded entity)
+struct BufView {
+  const uint8_t* p;
+  __device__ __forceinline__ uint8_t at(int i) const { return p[i]; }
+};
+
 // ------------------------------------------------------------- scanner
-// ScriptScanner::SkipToFrontOfSpan, plain text: getonescriptspan.cc:592-642
-__device__ int skip_to_front_of_span(const DevTables& T, const DocView& d, int start, int len, int* script) {
-  int sc = 0, skip = 0;
+// ScriptScanner::SkipToFrontOfSpan: getonescriptspan.cc:592-642
+__device__ int skip_to_front_of_span(const DevTables& T, const DocView& d, int start, int len, int* script,
+                                     bool plain) {
+  int sc = 0, skip = 0, tlen = 0, plen = 0;
   while (skip < len) {
     skip += scan_to_letter_or_special(T, d, start + skip, len - skip);
     if (skip >= len) { *script = sc; return len; }
-    int tlen = utf8_len(d.at(start + skip));
-    sc = script_num(T, d, start + skip);
+    const uint8_t c = d.at(start + skip);
+    if (!plain && is_special(c)) {
+      if (c == '<') {
+        tlen = scan_to_possible_letter(d, start + skip, len - skip);
+        sc = 0;
+      } else if (c == '>') {
+        tlen = 1;
+        sc = 0;
+      } else {                                   // '&': expand, no advance
+        uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        entity_to_buffer(T, d, start + skip, len - skip, tmp, &tlen, &plen);
+        if (plen > 0) sc = script_num(T, BufView{tmp}, 0);
+      }
+    } else {
+      tlen = utf8_len(c);
+      sc = script_num(T, d, start + skip);
+    }
     if (sc != 0) break;
     skip += tlen;
   }
@@ -573,20 +800,21 @@ __device__ int skip_to_front_of_span(const DevTables& T, const DocView& d, int s
   return skip;
 }
 
-// ScriptScanner::GetOneScriptSpan, plain text: getonescriptspan.cc:799-1027.
+// ScriptScanner::GetOneScriptSpan: getonescriptspan.cc:799-1027 (HTML mode
+// when !plain: tags skipped, entities decoded into the span).
 // `next`/`remaining` are next_byte_ - start_byte_ and byte_length_.
 template <class W>
 __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& next, int& remaining,
-                                    W& w, Span& span, Status& st) {
+                                    W& w, Span& span, Status& st, bool plain = true) {
   const int common = (int)T.common, inherited = (int)T.inherited;
   span.text = w.sbuf; span.text_bytes = 0; span.ulscript = 0;
   int put_soft_limit = kMaxScriptBytes - kWithinScriptTail;
   if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) put_soft_limit = remaining / 2;
-  int spanscript, sc = 0, tlen, plen;
+  int spanscript, sc = 0, tlen = 0, plen = 0;
   uint8_t* sb = w.sbuf;
   sb[0] = ' '; sb[1] = 0;
   int take = 0, put = 1;
-  int skip = skip_to_front_of_span(T, d, next, remaining, &spanscript);
+  int skip = skip_to_front_of_span(T, d, next, remaining, &spanscript, plain);
   next += skip; remaining -= skip;
   if (remaining <= 0) return false;
   span.ulscript = spanscript;
@@ -595,15 +823,21 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
     bool need_break = false;
     while (take < bl) {
       uint8_t c0 = d.at(base + take);
-      tlen = plen = utf8_len(c0);
       if (put + 4 > W::SB) { st.requeue = true; return false; }
-      if (take < bl - 3) {
-        sb[put] = c0; sb[put + 1] = d.at(base + take + 1);
-        sb[put + 2] = d.at(base + take + 2); sb[put + 3] = d.at(base + take + 3);
+      if (!plain && is_special(c0)) {
+        if (c0 == '<' || c0 == '>') { sc = 0; break; }
+        entity_to_buffer(T, d, base + take, bl - take, sb + put, &tlen, &plen);   // '&': copy entity, no advance
+        if (plen > 0) sc = script_num(T, BufView{sb + put}, 0);
       } else {
-        for (int k = 0; k < plen; ++k) sb[put + k] = d.at(base + take + k);
+        tlen = plen = utf8_len(c0);
+        if (take < bl - 3) {
+          sb[put] = c0; sb[put + 1] = d.at(base + take + 1);
+          sb[put + 2] = d.at(base + take + 2); sb[put + 3] = d.at(base + take + 3);
+        } else {
+          for (int k = 0; k < plen; ++k) sb[put + k] = d.at(base + take + k);
+        }
+        sc = script_num(T, d, base + take);
       }
-      sc = script_num(T, d, base + take);
       if (sc != spanscript && sc != inherited) {
         if (sc == common) {
           need_break = true;
@@ -620,8 +854,23 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
       tlen = scan_to_letter_or_special(T, d, base + take, bl - take);
       take += tlen;
       if (take >= bl) break;
-      tlen = utf8_len(d.at(base + take));
-      sc = script_num(T, d, base + take);
+      const uint8_t c1 = d.at(base + take);
+      if (!plain && is_special(c1)) {
+        if (c1 == '<') {
+          tlen = scan_to_possible_letter(d, base + take, bl - take);
+          sc = 0;
+        } else if (c1 == '>') {
+          tlen = 1;
+          sc = 0;
+        } else {                                 // '&': expand, no advance
+          if (put + 4 > W::SB) { st.requeue = true; return false; }
+          entity_to_buffer(T, d, base + take, bl - take, sb + put, &tlen, &plen);
+          if (plen > 0) sc = script_num(T, BufView{sb + put}, 0);
+        }
+      } else {
+        tlen = utf8_len(c1);
+        sc = script_num(T, d, base + take);
+      }
       if (sc != 0) break;
       take += tlen;
     }
@@ -640,10 +889,12 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
 
 // ScriptScanner::LowerScriptSpan getonescriptspan.cc:1033-1054
 template <class W>
-__device__ void lower_script_span(const DevTables& T, W& w, Span& span, Status& st) {
+__device__ void lower_script_span(const DevTables& T, W& w, Span& span, Status& st, bool plain = true) {
   int ilen = span.text_bytes + 3;
-  if ((ilen * 3) / 2 + 4 > W::LB) { st.requeue = true; return; }
-  int filled = lower_replace(T, span.text, ilen, w.lbuf, kMaxScriptLowerBuffer);
+  // HTML mode may map a character to more bytes (the &amp;-style half of a
+  // remap pair): then only the reference's own capacity bounds it
+  if ((plain ? (ilen * 3) / 2 + 4 : kMaxScriptLowerBuffer) > W::LB) { st.requeue = true; return; }
+  int filled = lower_replace(T, span.text, ilen, w.lbuf, kMaxScriptLowerBuffer, plain);
   w.lbuf[filled] = 0; w.lbuf[filled + 1] = 0; w.lbuf[filled + 2] = 0; w.lbuf[filled + 3] = 0;
   span.text = w.lbuf;
   span.text_bytes = filled - 3;
@@ -1003,6 +1254,9 @@ struct Linearizer {
 struct Ctx {
   int ulscript;
   Boosts latn, othr;        // ScoringContext::distinct_boost (scoreonescriptspan.h:139)
+  // ApplyHints result (compact_lang_det_impl.cc:1645-1684): langprior_boost
+  // latn[4] othr[4], then langprior_whack latn[4] othr[4]; null for none
+  const uint32_t* priors;
 };
 
 // SetChunkSummary scoreonescriptspan.cc:60-96 + SummaryBufferToDocTote :305-315
@@ -1067,7 +1321,15 @@ __device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb,
       if (cur.type == base_hit) ++cnt;
       have = lin.next(cur);
     }
+    // ScoreBoosts (scoreonescriptspan.cc:125-152): prior boosts, distinct
+    // boosts, then the prior whacks zero their languages (ZeroPSLang :39-42)
+    const int so = ((uint32_t)cx.ulscript == T.latin) ? 0 : 4;
+    if (cx.priors)
+      for (int k = 0; k < kMaxBoosts; ++k) if (cx.priors[so + k] > 0) add_lang_prob(T, cx.priors[so + k], t);
     for (int k = 0; k < kMaxBoosts; ++k) if (db.lp[k] > 0) add_lang_prob(T, db.lp[k], t);
+    if (cx.priors)
+      for (int k = 0; k < kMaxBoosts; ++k)
+        if (cx.priors[8 + so + k] > 0) t.score[(cx.priors[8 + so + k] >> 8) & 0xFF] = 0;
     int hi = have ? cur.offset : dummy_off;
     finish_chunk(T, ulscript, lo, hi, t, dt, nchunks < kMaxSummaries);
     ++nchunks;
@@ -1259,11 +1521,13 @@ __device__ void write_result(cld_result* r, const Extract& x, int summary, bool 
   *r = o;
 }
 
-// DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (plain text, no
-// hints, flags 0, no ResultChunkVector); recursion unrolled into passes.
-// Returns the number of passes, or 0 with st.requeue set.
+// DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (flags 0, no
+// ResultChunkVector; HTML mode when !plain, the ApplyHints priors when given);
+// recursion unrolled into passes.  Returns the number of passes, or 0 with
+// st.requeue set.
 template <class W>
-__device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result* out, Status& st) {
+__device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result* out, Status& st,
+                          bool plain = true, const uint32_t* priors = nullptr) {
   const int unk = (int)T.unknown_lang;
   int flags = 0;
   int passes = 0;
@@ -1281,6 +1545,7 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     Ctx cx;
     cx.ulscript = 0;
     cx.latn.n = 0; cx.othr.n = 0;
+    cx.priors = priors;
     for (int k = 0; k < kMaxBoosts; ++k) { cx.latn.lp[k] = 0; cx.othr.lp[k] = 0; }
     int next = 0, remaining = d.len;
     int hash = 0;
@@ -1290,8 +1555,8 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     int total = 0;
     bool restart = false;
     Span span;
-    while (get_one_script_span(T, d, next, remaining, w, span, st)) {
-      lower_script_span(T, w, span, st);
+    while (get_one_script_span(T, d, next, remaining, w, span, st, plain)) {
+      lower_script_span(T, w, span, st, plain);
       if (st.requeue) return 0;
       if (flags & kCLDFlagSqueeze) {
         if constexpr (W::MULTIPASS) span.text_bytes = cheap_squeeze_inplace(span.text, span.text_bytes, w.sqz);

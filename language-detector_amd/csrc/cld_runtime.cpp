@@ -24,6 +24,7 @@
 
 #include "cld_device.h"
 #include "cld_dynamic_data.h"
+#include "cld_hints.h"
 #include "cld_kernels.h"
 #include "cldt_format.h"
 
@@ -46,6 +47,7 @@ struct HostTables {
   std::vector<std::string> codes, names;
   std::string version;
   DevTables offs{};   // pointer fields hold byte offsets into blob
+  cld::HintView hints;   // host views for cld_hint_priors (null fields: the blob has no hint sections)
 };
 
 // Section `id` of a parsed blob; parse_tables has checked that every section
@@ -203,6 +205,68 @@ int parse_tables(HostTables* t, const std::string& label) {
   D.hawaiian = M.hawaiian;
   t->codes = strings(t->blob, CLDT_LANG_CODES);
   t->names = strings(t->blob, CLDT_LANG_NAMES);
+  {  // optional HTML-mode sections: entity names (a sorted string table), their
+     // code points, the cp1252 fix-up; all three or none
+    uint64_t no = 0, ns = 0, vo = 0, vs = 0, co = 0, cs = 0;
+    const uint8_t* np = section(t->blob, CLDT_ENTITY_NAMES, &no, &ns);
+    const uint8_t* vp = section(t->blob, CLDT_ENTITY_VALUES, &vo, &vs);
+    const uint8_t* cp = section(t->blob, CLDT_CP1252_FIX, &co, &cs);
+    D.ent_names = nullptr; D.ent_values = nullptr; D.cp1252 = nullptr; D.n_ent = 0;
+    if (np && vp && cp) {
+      const std::vector<std::string> ent = strings(t->blob, CLDT_ENTITY_NAMES);
+      if (ent.empty() || ent.size() * 4 != vs || cs < 256 * 4 || ns < 4ull * (ent.size() + 2)) return CLD_EINVAL;
+      for (const std::string& e : ent)            // the device compares names NUL-terminated
+        if (e.size() >= 16) return CLD_EINVAL;
+      D.ent_names = at<const uint8_t*>(no);
+      D.ent_values = at<const int32_t*>(vo);
+      D.cp1252 = at<const uint32_t*>(co);
+      D.n_ent = (uint32_t)ent.size();
+    }
+  }
+  {  // optional hint sections (host only)
+    cld::HintView& h = t->hints;
+    h = cld::HintView();
+    auto tbl = [&](uint32_t id) -> const uint8_t* {   // cldt_hint_entry table + pool, checked
+      uint64_t z = 0;
+      const uint8_t* p = section(t->blob, id, nullptr, &z);
+      if (!p || z < 4) return nullptr;
+      const uint32_t n = *(const uint32_t*)p;
+      if (4ull + (uint64_t)n * sizeof(cldt_hint_entry) > z) return nullptr;
+      const cldt_hint_entry* e = (const cldt_hint_entry*)(p + 4);
+      const uint64_t pool = z - 4 - (uint64_t)n * sizeof(cldt_hint_entry);
+      const char* ps = (const char*)(e + n);
+      for (uint32_t i = 0; i < n; ++i) {
+        if (e[i].key_off >= pool || !memchr(ps + e[i].key_off, 0, pool - e[i].key_off)) return nullptr;
+        if (e[i].code_off != 0xFFFFFFFFu &&
+            (e[i].code_off >= pool || !memchr(ps + e[i].code_off, 0, pool - e[i].code_off)))
+          return nullptr;
+      }
+      return p;
+    };
+    uint64_t az = 0, rz = 0, ez = 0;
+    const uint8_t* act = section(t->blob, CLDT_HINT_CODE_ACTION, nullptr, &az);
+    const uint8_t* rem = section(t->blob, CLDT_HINT_CODE_REMAP, nullptr, &rz);
+    const uint8_t* enc = section(t->blob, CLDT_HINT_ENCODING, nullptr, &ez);
+    if (act && rem && enc && az >= 256 && rz >= 256) {
+      h.langtag1 = tbl(CLDT_HINT_LANGTAG1);
+      h.langtag2 = tbl(CLDT_HINT_LANGTAG2);
+      h.tld = tbl(CLDT_HINT_TLD);
+      h.action = act; h.remap = rem;
+      h.enc = (const int16_t*)enc; h.n_enc = (uint32_t)(ez / 2);
+      const uint8_t* b = t->blob.data();
+      h.l2p = b + (uintptr_t)D.l2p; h.l2p_size = D.l2p_size;
+      h.p2l_latn = (const uint16_t*)(b + (uintptr_t)D.p2l_latn);
+      h.p2l_othr = (const uint16_t*)(b + (uintptr_t)D.p2l_othr);
+      h.close_set = b + (uintptr_t)D.close_set; h.n_langs = D.n_langs;
+      h.unknown_language = t->meta.unknown_language;
+      h.chinese = h.chinese_t = 0xFFFFFFFFu;
+      for (size_t i = 0; i < t->codes.size(); ++i) {
+        if (t->codes[i] == "zh") h.chinese = (uint32_t)i;
+        if (t->codes[i] == "zh-Hant") h.chinese_t = (uint32_t)i;
+      }
+      if (!h.ok()) h = cld::HintView();
+    }
+  }
   const cldt_table_header* q = (const cldt_table_header*)section(t->blob, CLDT_QUAD, nullptr, nullptr);
   // which quadgram table is live: the empty placeholder (Q0, what the reference
   // itself can run without the missing quadchrome blob), the synthetic Q1 test
@@ -242,6 +306,9 @@ DevTables device_tables(const DevTables& o, const uint8_t* d) {
   T.expected = rebase(T.expected, d); T.lgprob = rebase(T.lgprob, d); T.l2p = rebase(T.l2p, d);
   T.p2l_latn = rebase(T.p2l_latn, d); T.p2l_othr = rebase(T.p2l_othr, d); T.rtype = rebase(T.rtype, d);
   T.deflang = rebase(T.deflang, d); T.closest = rebase(T.closest, d); T.close_set = rebase(T.close_set, d);
+  if (T.ent_names) {
+    T.ent_names = rebase(T.ent_names, d); T.ent_values = rebase(T.ent_values, d); T.cp1252 = rebase(T.cp1252, d);
+  }
   return T;
 }
 
@@ -298,6 +365,10 @@ struct Device {
     uint8_t* d_in = nullptr; size_t d_in_cap = 0;
     uint64_t* d_offs = nullptr; size_t d_offs_cap = 0;
     cld_result* d_out = nullptr; size_t d_out_cap = 0;
+    uint8_t* h_sp = nullptr; size_t h_sp_cap = 0;        // cld_detect_batch_ex: routing bits + priors
+    uint32_t* h_pri = nullptr; size_t h_pri_cap = 0;
+    uint8_t* d_sp = nullptr; size_t d_sp_cap = 0;
+    uint32_t* d_pri = nullptr; size_t d_pri_cap = 0;
     hipEvent_t up = nullptr, comp = nullptr, down = nullptr;
     size_t pending_n = 0; cld_result* pending_dst = nullptr;   // results to hand over once `down` fires
     bool busy = false;
@@ -468,8 +539,12 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
   return CLD_OK;
 }
 
-// Enqueue the whole pipeline for n documents already on device d.
-int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s) {
+// Enqueue the whole pipeline for n documents already on device d.  special /
+// priors (device, nullable): cld_detect_batch_ex's per-document routing bits
+// and ApplyHints langprobs (16 per document); such documents skip the wave and
+// long kernels and run whole in k_general.
+int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
+            const uint8_t* special = nullptr, const uint32_t* priors = nullptr) {
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (d->n_slots > 0 && d->long_order) {
@@ -486,10 +561,14 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
   if (d->d_dbg) HIP_OK(hipMemsetAsync(d->d_dbg, 0, 4, s));
   HIP_OK(hipEventRecord(ev[0], s));
+  // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
+  uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
+  const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
   if (d->front == 1)
-    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, s));
+    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, special, sp_list, sp_ctr, s));
   else
-    HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, s));
+    HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
+                           sp_ctr, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
@@ -502,11 +581,11 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
                            d->d_prof ? d->d_prof + 8 : nullptr, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue2, kCtrDequeue2, s));
+                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, s));
   } else {
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue, kCtrDequeue, s));
+                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -519,11 +598,15 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
 // Adds one batch's device counters to st (docs = documents of that batch).
 void add_counters(Device* d, const uint32_t* c, uint64_t docs, cld_batch_stats* st) {
   const uint32_t to_general = d->n_slots > 0 ? c[kCtrRequeue2] : c[kCtrRequeue];
+  // special (HTML / hinted) documents sit in the k_general list directly: in
+  // d_requeue2 with k_long, in d_requeue without it
+  const uint32_t sp2 = d->n_slots > 0 ? c[kCtrSpecial] : 0;
+  const uint64_t shorts = docs - c[kCtrRequeue] - sp2;
   st->docs += docs;
   st->general_docs += to_general;
-  st->long_docs += c[kCtrRequeue] - to_general;
-  st->short_docs += docs - c[kCtrRequeue];
-  st->passes[0] += (docs - c[kCtrRequeue]) + c[kCtrPass1];
+  st->long_docs += c[kCtrRequeue] - (to_general - sp2);
+  st->short_docs += shorts;
+  st->passes[0] += shorts + c[kCtrPass1];
   st->passes[1] += c[kCtrPass2];
   st->passes[2] += c[kCtrPass3];
   st->passes[3] += c[kCtrError];
@@ -629,7 +712,8 @@ void par_copy(void* dst, const void* src, size_t n) {
 // caller wrote them and the kernels get `d_in - offs[first]` as their buffer
 // base, so no rebasing pass runs anywhere.  Chunk k's staging overlaps chunk
 // k-1's kernels; its upload overlaps them too.
-int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
+int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
+                   const uint8_t* special = nullptr, const uint32_t* priors = nullptr) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
@@ -677,10 +761,23 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     }
     cld_result* dst = out + a;
     if (!out_pinned && (rc = grow_host(&h.h_out, &h.h_out_cap, m))) break;
+    if (special) {           // per-document routing bits (and priors) for this chunk, staged pinned
+      if ((rc = grow(&h.d_sp, &h.d_sp_cap, m)) || (rc = grow_host(&h.h_sp, &h.h_sp_cap, m))) break;
+      memcpy(h.h_sp, special + a, m);
+      if (priors) {
+        if ((rc = grow(&h.d_pri, &h.d_pri_cap, 16 * m)) || (rc = grow_host(&h.h_pri, &h.h_pri_cap, 16 * m))) break;
+        memcpy(h.h_pri, priors + 16 * a, 16 * m * sizeof(uint32_t));
+      }
+    }
     // upload (after the slot's previous kernels stopped reading its device buffers)
     HIP_OK(hipStreamWaitEvent(d->up_stream, h.comp, 0));
     if (bytes) HIP_OK(hipMemcpyAsync(h.d_in, src_in, bytes, hipMemcpyHostToDevice, d->up_stream));
     HIP_OK(hipMemcpyAsync(h.d_offs, src_offs, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->up_stream));
+    if (special) {
+      HIP_OK(hipMemcpyAsync(h.d_sp, h.h_sp, m, hipMemcpyHostToDevice, d->up_stream));
+      if (priors)
+        HIP_OK(hipMemcpyAsync(h.d_pri, h.h_pri, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, d->up_stream));
+    }
     HIP_OK(hipEventRecord(h.up, d->up_stream));
     // kernels: buffer base biased so that the caller's offsets index it directly
     HIP_OK(hipStreamWaitEvent(d->stream, h.up, 0));
@@ -689,7 +786,8 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
       rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream);
     } else {
-      rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream);
+      rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream, special ? h.d_sp : nullptr,
+                   (special && priors) ? h.d_pri : nullptr);
     }
     if (rc) break;
     HIP_OK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
@@ -911,6 +1009,7 @@ void cld_shutdown(void) {
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);
       (void)hipFree(h.d_in); (void)hipFree(h.d_offs); (void)hipFree(h.d_out);
+      (void)hipHostFree(h.h_sp); (void)hipHostFree(h.h_pri); (void)hipFree(h.d_sp); (void)hipFree(h.d_pri);
       (void)hipEventDestroy(h.up); (void)hipEventDestroy(h.comp); (void)hipEventDestroy(h.down);
     }
     (void)hipHostFree(d->h_ctr);
@@ -945,6 +1044,85 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
     th.emplace_back([&, k] { rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], flags); });
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs) if (r) return r;
+  return CLD_OK;
+}
+
+int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld_hints* hints, int16_t* priors14,
+                    uint32_t* boosts16) {
+  if ((!is_plain_text && len > 0 && !doc)) return CLD_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (int rc = host_tables(nullptr)) return rc;
+  }
+  const cld::HintView& v = g_tab.hints;
+  if (!v.ok()) return CLD_EINVAL;               // tables without the hint sections
+  int16_t p[cld::kMaxPriors] = {};
+  const int n = cld::hint_priors(v, doc, len, is_plain_text != 0, hints, p);
+  if (priors14) memcpy(priors14, p, sizeof(p));
+  if (boosts16) cld::hint_boosts(v, p, n, boosts16);
+  return n;
+}
+
+int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
+                        uint32_t flags, cld_result* out) {
+  if ((flags & ~CLD_FLAG_HTML) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
+  if (n == 0) return CLD_OK;
+  if (n > 0x7FFFFFFFu) return CLD_EINVAL;
+  for (size_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return CLD_EINVAL;
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  const bool html = (flags & CLD_FLAG_HTML) != 0;
+  if (html && !g_tab.offs.ent_names) return CLD_EINVAL;     // tables without the HTML sections
+  if ((html || hints) && !g_tab.hints.ok()) return CLD_EINVAL;
+  // ApplyHints per document on the host (a few table lookups, and for HTML a
+  // scan of the first 8 KB), split over host threads
+  std::vector<uint8_t> special(n, html ? kSpecialHtml : 0);
+  std::vector<uint32_t> priors;
+  if (html || hints) {
+    priors.assign(16 * n, 0);
+    std::atomic<bool> any(false);
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()),
+                                                             (n + 4095) / 4096));
+    auto work = [&](size_t lo, size_t hi) {
+      bool a = false;
+      for (size_t i = lo; i < hi; ++i) {
+        int16_t p[cld::kMaxPriors];
+        const int k = cld::hint_priors(g_tab.hints, buf + offsets[i], offsets[i + 1] - offsets[i], !html,
+                                       hints ? hints + i : nullptr, p);
+        if (k <= 0) continue;
+        uint32_t* o = priors.data() + 16 * i;
+        cld::hint_boosts(g_tab.hints, p, k, o);
+        bool nz = false;
+        for (int j = 0; j < 16; ++j) nz |= o[j] != 0;
+        if (nz) { special[i] |= kSpecialPriors; a = true; }
+      }
+      if (a) any = true;
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    work(0, n / nt);
+    for (auto& x : th) x.join();
+    if (!any) priors.clear();
+  }
+  bool any_special = html || !priors.empty();
+  const uint8_t* sp = any_special ? special.data() : nullptr;
+  const uint32_t* pr = priors.empty() ? nullptr : priors.data();
+  const size_t ndev = g_devs.size();
+  std::vector<size_t> cut(ndev + 1, 0);
+  cld_plan_shards(offsets, n, (int)ndev, cut.data());
+  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, 0, sp, pr);
+  std::vector<int> rcs(ndev, CLD_OK);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < ndev; ++k) {
+    if (cut[k + 1] == cut[k]) continue;
+    th.emplace_back([&, k] {
+      rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], 0,
+                              sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr);
+    });
   }
   for (auto& t : th) t.join();
   for (int r : rcs) if (r) return r;

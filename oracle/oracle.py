@@ -104,6 +104,24 @@ class Oracle:
             raise RuntimeError("cldo_detect_batch rc=%d" % rc)
         return out
 
+    def detect_batch_ex(self, buf, offsets, plain=None, priors=None, threads=1):
+        """is_plain_text per document (uint8, None = all plain) and the ApplyHints
+        langprobs (uint32 [n, 16], None = no hints)."""
+        buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        pl = None if plain is None else np.ascontiguousarray(plain, dtype=np.uint8)
+        pr = None if priors is None else np.ascontiguousarray(priors, dtype=np.uint32).reshape(n, 16)
+        self.lib.cldo_detect_batch_ex.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] + [ctypes.c_void_p] * 3 + \
+            [ctypes.c_int]
+        rc = self.lib.cldo_detect_batch_ex(buf.ctypes.data, offsets.ctypes.data, n,
+                                           None if pl is None else pl.ctypes.data,
+                                           None if pr is None else pr.ctypes.data, out.ctypes.data, threads)
+        if rc != 0:
+            raise RuntimeError("cldo_detect_batch_ex rc=%d" % rc)
+        return out
+
     def prepare_batch(self, buf, offsets, flags):
         """handlers.go:150-151 (StripExtras = 1, C-string cut = 2) -> (buf, offsets)."""
         buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)

@@ -1,0 +1,100 @@
+"""cld_detect_batch_ex (HTML mode + CLDHints) on the GPU vs the oracle, bit-exact.
+
+The per-document priors come from the product's host hint code
+(cld_hint_priors, pinned to the reference's hint code by
+tests/test_html_hints.py::test_hint_priors_match_reference); the oracle then
+scores each document with the same priors and is_plain_text flag.  HTML
+documents and hinted documents run in k_general (the exact sequential
+kernel), every other document of the same batch keeps the wave / long path.
+"""
+import numpy as np
+import pytest
+
+import corpus
+from test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def priors_for(gpu, buf, offs, html, hints):
+    n = len(offs) - 1
+    pr = np.zeros((n, 16), dtype=np.uint32)
+    for i in range(n):
+        doc = bytes(buf[offs[i]:offs[i + 1]])
+        _, pr[i] = gpu.hint_priors(doc, html=html, hints=hints[i] if hints is not None else None)
+    return pr
+
+
+def random_hints(gpu, n, seed):
+    rng = np.random.default_rng(seed)
+    tags = ["en", "fr", "de", "es", "it", "pt", "nl", "ru", "uk", "id", "ms", "hr", "sr", "bs", "zh", "zh-tw",
+            "ja", "mi,en", "da,nb", "cs", "sk", "xx"]
+    tlds = ["id", "fr", "de", "ru", "ua", "cn", "tw", "com", "br", "my", "hr", "es"]
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.25:
+            out.append(gpu.Hints.make())                                   # no hint at all
+            continue
+        cl = tags[int(rng.integers(0, len(tags)))] if rng.random() < 0.5 else None
+        tld = tlds[int(rng.integers(0, len(tlds)))] if rng.random() < 0.4 else None
+        enc = int(rng.integers(0, 75)) if rng.random() < 0.3 else gpu.UNKNOWN_ENCODING
+        lang = int(rng.integers(0, 100)) if rng.random() < 0.3 else gpu.UNKNOWN_LANGUAGE
+        out.append(gpu.Hints.make(cl, tld, enc, lang))
+    return out
+
+
+def test_html_documents(gpu, oracle):
+    buf, offs = corpus.html(1500, seed=21)
+    n = len(offs) - 1
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+    st = gpu.last_stats()
+    assert st.general_docs == n                      # every HTML document runs the exact kernel
+    pr = priors_for(gpu, buf, offs, True, None)
+    assert (pr != 0).any(axis=1).sum() > n // 2      # lang= attributes became priors
+    ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=16)
+    assert_same(got, ref, "html")
+    # HTML mode matters: the plain-text answer differs on some pages
+    plain = oracle.detect_batch(buf, offs, threads=16)
+    assert (plain["text_bytes"] != ref["text_bytes"]).sum() > n // 2
+
+
+def test_html_edge_documents(gpu, oracle):
+    docs = [b"", b"<", b">", b"&", b"&amp;", b"<html lang='fr'>", b"<!-- unterminated", b"<script>x",
+            b"<p>caf&eacute; cr&egrave;me br&ucirc;l&eacute;e</p>" * 20, b"&#x4e2d;&#25991;" * 40,
+            b"<style>a{}</style >texto en espa&ntilde;ol " * 30, b"a < b > c & d" * 100,
+            b"<meta http-equiv=content-language content=\"de\">Guten Tag " * 30,
+            ("<b>" + "русский текст " * 300 + "</b>").encode(),
+            b"<html lang=\"mi,en\">" + b"kia ora " * 400]
+    buf, offs = gpu.pack(docs)
+    n = len(docs)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+    pr = priors_for(gpu, buf, offs, True, None)
+    ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr)
+    assert_same(got, ref, "html edge")
+
+
+@pytest.mark.parametrize("cfg,n,seed", [("c2", 20000, 31), ("c3", 300, 32)])
+def test_plain_documents_with_hints(gpu, oracle, cfg, n, seed):
+    buf, offs = corpus.GENERATORS[cfg](n)
+    hints = random_hints(gpu, n, seed=seed)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, hints=hints)
+    st = gpu.last_stats()
+    pr = priors_for(gpu, buf, offs, False, hints)
+    hinted = int((pr != 0).any(axis=1).sum())
+    assert hinted > n // 3
+    assert st.general_docs >= hinted                 # hinted documents ran in k_general
+    ref = oracle.detect_batch_ex(buf, offs, priors=pr, threads=16)
+    assert_same(got, ref, cfg + " hints")
+    # hints change answers (boosts / whacks reach the chunk totes)
+    base = oracle.detect_batch(buf, offs, threads=16)
+    assert (base["lang3"] != ref["lang3"]).any()
+
+
+def test_ex_without_hints_is_detect_batch(gpu):
+    buf, offs = corpus.c4(5000)
+    a = gpu.detect_batch(buf=buf, offsets=offs)
+    ga = gpu.last_stats().general_docs
+    b = gpu.detect_batch_ex(buf=buf, offsets=offs)
+    assert_same(b, a, "ex == batch")
+    assert gpu.last_stats().general_docs == ga

@@ -114,3 +114,84 @@ def test_entity_reader_matches_reference(oracle):
         got.append((v, c.value))
     assert got == [tuple(x) for x in out.tolist()]
     assert sum(1 for v, _ in got if v > 0) > 500
+
+
+LANG_TAGS = ["en", "en-us", "EN-GB", "fr", "fr-ca", "de", "de-ch", "zh", "zh-tw", "zh-hant", "zh-cn", "pt-br",
+             "es-419", "sr-latn", "nb", "no", "mi", "ja", "ko", "ru", "uk", "be", "id", "ms", "hr", "bs", "sr",
+             "xx", "x-klingon", "tl", "fil", "iw", "he", "ar", "fa", "hi"]
+TLDS = ["id", "fr", "de", "ru", "cn", "tw", "com", "uk", "xx", "jp", "br", "ch", "be", "ua", "by", "my", "hr",
+        "ba", "rs", "org", "ID", "Fr"]
+
+
+def hint_cases(seed, n):
+    """(html body or b'', content-language, tld, encoding, language) tuples."""
+    rng = np.random.default_rng(seed)
+    pick = lambda xs: xs[int(rng.integers(0, len(xs)))]
+    cases = []
+    for _ in range(n):
+        html = b""
+        if rng.random() < 0.5:
+            parts = [b"<html"]
+            if rng.random() < 0.7:
+                parts.append(b' lang="%s"' % pick(LANG_TAGS).encode())
+            parts.append(b"><head>")
+            if rng.random() < 0.4:
+                parts.append(b'<meta http-equiv="Content-Language" content="%s">' % pick(LANG_TAGS).encode())
+            if rng.random() < 0.3:
+                parts.append(b"<meta name=language content='%s'>" % pick(LANG_TAGS).encode())
+            if rng.random() < 0.3:
+                parts.append(b"<p xml:lang='%s,%s'>x</p>" % (pick(LANG_TAGS).encode(), pick(LANG_TAGS).encode()))
+            if rng.random() < 0.2:
+                parts.append(b'<a lang="%s" href=x>' % pick(LANG_TAGS).encode())   # skipped tag kind
+            parts.append(b"</head><body>texte du document</body></html>")
+            html = b"".join(parts)
+        cl = b""
+        if rng.random() < 0.4:
+            k = int(rng.integers(1, 4))
+            cl = ",".join(pick(LANG_TAGS) for _ in range(k)).encode()
+        tld = pick(TLDS).encode() if rng.random() < 0.4 else b""
+        enc = int(rng.integers(0, 75)) if rng.random() < 0.4 else 23
+        lang = int(rng.integers(0, 165)) if rng.random() < 0.3 else 26
+        cases.append((html, cl, tld, enc, lang))
+    return cases
+
+
+@needs_ref
+def test_hint_priors_match_reference():
+    """cld_hint_priors (the product's host hint code) builds the same
+    CLDLangPriors as the reference's compact_lang_det_hint_code.cc."""
+    import cld_amd
+    cases = hint_cases(8, 3000)
+    recs = []
+    for html, cl, tld, enc, lang in cases:
+        recs += [html, cl, tld, str(enc).encode(), str(lang).encode()]
+    out = refscan("hints", recs)
+    p, nonzero = 0, 0
+    for html, cl, tld, enc, lang in cases:
+        (k,) = struct.unpack_from("<I", out, p); p += 4
+        want = list(struct.unpack_from("<%dh" % k, out, p)); p += 2 * k
+        h = cld_amd.Hints.make(cl or None, tld or None, enc, lang)
+        got, boosts = cld_amd.hint_priors(html, html=bool(html), hints=h)
+        assert got.tolist() == want, (html, cl, tld, enc, lang)
+        nonzero += bool(want)
+        if not want:
+            assert not boosts.any()
+    assert nonzero > 1500
+
+
+def test_hint_boosts_shape():
+    """ApplyHints' boost/whack split: a language hint boosts its language in the
+    Latin ring with weight 8 (kLgProbV2TblBackmap[8] = 28); a close-set member
+    (Indonesian / Malay) whacks the others of its set."""
+    import cld_amd
+    en = 0                                           # ENGLISH
+    pri, b = cld_amd.hint_priors(hints=cld_amd.Hints.make(language=en))
+    assert pri.tolist() == [(8 << 10) + en]
+    assert (b[0] & 0xFF) == 28 and b[1:].sum() == 0
+    # .id boosts Indonesian and carries a negative Malay prior: two members of
+    # one close set, so no whack (close_set_count == 2)
+    pri, b = cld_amd.hint_priors(hints=cld_amd.Hints.make(tld="id"))
+    assert len(pri) == 2 and not b[8:].any()
+    indonesian = [i for i in range(200) if cld_amd.language_code(i) == "id"][0]
+    pri, b = cld_amd.hint_priors(hints=cld_amd.Hints.make(language=indonesian))
+    assert b[8:12].any() and not b[12:].any()        # Malay whacked in the Latin ring
