@@ -5,8 +5,11 @@ cld2_dynamic_data_loader.cc:41-146; writer cld2_dynamic_data_extractor.cc:45-290
 No data file produced by the reference's own tool exists here (the tool links
 the missing quadchrome blob), so the files are written by
 tools/cld2_data_file.py -- a restatement of the reference's writer -- from the
-CLDT tables: format parity is against the published layout ("parity
-unpinned" for byte-identity with a reference-written file).  Detection parity
+CLDT tables.  Format parity is pinned by the reference's own LOADER
+(oracle/dynload, compiled from cld2_dynamic_data_loader.cc where it lies):
+it accepts those files and reconstructs exactly the tables they were written
+from (test_reference_loader_reads_written_files); byte-identity with a file
+the reference's writer would produce stays unpinned.  Detection parity
 is pinned the usual way: the tables the library imports must score every
 document exactly like the oracle on the same tables.
 
@@ -158,3 +161,59 @@ def test_gpu_swaps_tables_from_data_file(gpu, q0_file, synth_file, tmp_path):
         cld_amd.unload_data()
     assert not cld_amd.is_data_dynamic()
     assert _same(cld_amd.detect_batch(buf=buf, offsets=offs), ref_syn)
+
+
+def _fnv(b):
+    h = 1469598103934665603
+    for x in bytes(b):
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return "%016x" % h
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/cld2/internal"), reason="reference sources absent")
+@pytest.mark.parametrize("which", ["synth", "q0"])
+def test_reference_loader_reads_written_files(which, synth_file, q0_file):
+    """The reference's own loader (cld2_dynamic_data_loader.cc:164-258, built by
+    oracle/dynload from the sources where they lie) accepts the files
+    tools/cld2_data_file.py writes and reconstructs exactly the tables they
+    were written from: header checks, offsets, sizes and every table byte."""
+    import json
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle", "dynload")], check=True)
+    path, src = (synth_file, SYNTH) if which == "synth" else (q0_file, Q0)
+    blob = cldt.Blob.load(src)
+    tabs = [blob.table(s) for s in cld2_data_file.TABLE_SECTIONS]
+    expected = blob.raw(cldt.EXPECTED_SCORE)
+    args = [os.path.join(ROOT, "oracle", "_ref", "dynload"), path, str(len(expected) // 2)]
+    args += [str(len(t["ind"])) for t in tabs]
+    got = json.loads(subprocess.run(args, capture_output=True, check=True, text=True).stdout)
+    assert got["loaded"] and got["length"] == os.path.getsize(path)
+    u = cld2_data_file.unigram_from_blob(blob)
+    for f in cld2_data_file.UTF8_FIELDS:
+        assert got["unigram"][f] == u[f], f
+    assert got["unigram"]["state_table"] == _fnv(u["state_table"])
+    assert got["unigram"]["remap_string"] == _fnv(b"\0") and got["unigram"]["fast_state"] is False
+    assert got["expected"] == _fnv(expected)
+    for t, g in zip(tabs, got["tables"]):
+        for f in ("size_one", "size", "key_mask", "build_date"):
+            assert g[f] == t[f], f
+        assert g["buckets"] == _fnv(t["buckets"][:t["size"]].tobytes())
+        assert g["ind"] == _fnv(t["ind"].tobytes())
+        assert g["recognized"] == ""
+
+
+def test_reference_loader_rejects_truncated_file(synth_file, tmp_path):
+    """The reference loader's size check (loader :124-138) refuses a truncated
+    file; the product's converter refuses it too."""
+    if not os.path.isdir("/root/reference/cld2/internal"):
+        pytest.skip("reference sources absent")
+    import json
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle", "dynload")], check=True)
+    bad = tmp_path / "trunc.cld2_data_file00"
+    bad.write_bytes(open(synth_file, "rb").read()[:-16])
+    args = [os.path.join(ROOT, "oracle", "_ref", "dynload"), str(bad), "0"] + ["0"] * 7
+    got = json.loads(subprocess.run(args, capture_output=True, check=True, text=True).stdout)
+    assert got == {"loaded": False}
+    with pytest.raises(cld_amd.CldError):
+        cld_amd.convert_data_file(str(bad), str(tmp_path / "x.cldt"), SYNTH)
