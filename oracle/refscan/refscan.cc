@@ -56,8 +56,10 @@ int main(int argc, char** argv) {
       std::vector<std::string> out;
       std::vector<int> scripts;
       while (ss.GetOneScriptSpanLower(&span)) {
-        out.emplace_back(span.text, span.text_bytes);
-        scripts.push_back(span.ulscript);
+        // invalid UTF-8 can leave the lowercaser short of its 3 pad bytes:
+        // text_bytes < 0 is reported as an empty span with the raw value
+        out.emplace_back(span.text, span.text_bytes > 0 ? span.text_bytes : 0);
+        scripts.push_back(span.ulscript | (span.text_bytes < 0 ? (uint32_t)(-span.text_bytes) << 16 : 0u));
       }
       put32((uint32_t)out.size());
       for (size_t i = 0; i < out.size(); ++i) {
