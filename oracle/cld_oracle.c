@@ -73,6 +73,7 @@ enum {
 #define kIgnoreMaxPercent 20
 #define kKeepMinPercent 2
 #define kMinReliableKeepPercent 41   /* :981 */
+#define kUnreliablePercentThreshold 75   /* scoreonescriptspan.cc:33 */
 #define kGoodSecondT1T2MinBytes 15   /* :1405 */
 /* compact_lang_det_impl.h:31-38 */
 #define kCLDFlagFinish 1
@@ -259,6 +260,104 @@ static int lscript4(int ulscript) {
   return 3;
 }
 
+/* ------------------------------------------------------------ offset map */
+/* OffsetMap (offsetmap.cc:43-453): a list of copy / insert / delete ranges
+ * from A (the original text) to A' (the text built from it), coded one byte
+ * per range as the reference codes it (2-bit op, 6-bit length, prefix bytes
+ * for longer lengths; adjacent copies merged by Flush).  Only built in
+ * ResultChunkVector mode, where MapBack takes chunk offsets in the lowered
+ * span text back to document offsets. */
+enum { OM_PREFIX = 0, OM_COPY = 1, OM_INSERT = 2, OM_DELETE = 3 };
+typedef struct {
+  uint8_t* d; int n, cap;             /* diffs_ */
+  int pend_op, pend_len;              /* pending_op_, pending_length_ */
+  int max_a, max_ap;                  /* max_aoffset_, max_aprimeoffset_ */
+} offmap_t;
+static void om_push(offmap_t* m, int op, int len) {          /* Emit :203-206 */
+  if (m->n == m->cap) { m->cap = m->cap ? 2 * m->cap : 256; m->d = (uint8_t*)realloc(m->d, (size_t)m->cap); }
+  m->d[m->n++] = (uint8_t)((op << 6) | (len & 0x3F));
+}
+static void om_clear(offmap_t* m) {                          /* Clear :43-55 */
+  m->n = 0; m->pend_op = OM_COPY; m->pend_len = 0; m->max_a = 0; m->max_ap = 0;
+}
+static void om_flush(offmap_t* m) {                          /* Flush :158-187 */
+  if (m->pend_len == 0) return;
+  if (m->pend_op == OM_COPY && m->n > 0) {
+    uint8_t c = m->d[m->n - 1];
+    if ((c >> 6) == OM_COPY && (c & 0x3F) + m->pend_len <= 0x3F) {
+      m->d[m->n - 1] = (uint8_t)(c + m->pend_len);
+      m->pend_len = 0;
+      return;
+    }
+  }
+  if (m->pend_len > 0x3F) {
+    int nz = 0;
+    for (int shift = 30; shift > 0; shift -= 6) {
+      int prefix = (m->pend_len >> shift) & 0x3F;
+      if (prefix > 0 || nz) { om_push(m, OM_PREFIX, prefix); nz = 1; }
+    }
+  }
+  om_push(m, m->pend_op, m->pend_len & 0x3F);
+  m->pend_len = 0;
+}
+static void om_copy(offmap_t* m, int bytes) {                /* Copy :107-118 */
+  if (bytes == 0) return;
+  m->max_a += bytes; m->max_ap += bytes;
+  if (m->pend_op == OM_COPY) m->pend_len += bytes;
+  else { om_flush(m); m->pend_op = OM_COPY; m->pend_len = bytes; }
+}
+static void om_insert(offmap_t* m, int bytes) {              /* Insert :122-138 */
+  if (bytes == 0) return;
+  m->max_ap += bytes;
+  if (m->pend_op == OM_INSERT) m->pend_len += bytes;
+  else if (bytes == 1 && m->pend_op == OM_DELETE && m->pend_len == 1) m->pend_op = OM_COPY;
+  else { om_flush(m); m->pend_op = OM_INSERT; m->pend_len = bytes; }
+}
+static void om_delete(offmap_t* m, int bytes) {              /* Delete :141-156 */
+  if (bytes == 0) return;
+  m->max_a += bytes;
+  if (m->pend_op == OM_DELETE) m->pend_len += bytes;
+  else if (bytes == 1 && m->pend_op == OM_INSERT && m->pend_len == 1) m->pend_op = OM_COPY;
+  else { om_flush(m); m->pend_op = OM_DELETE; m->pend_len = bytes; }
+}
+static void om_maybe_flush_all(offmap_t* m) {                /* MaybeFlushAll / FlushAll :190-200 */
+  if (0 < m->pend_len || m->n == 0) { om_copy(m, 1); om_flush(m); }
+}
+static void om_reset(offmap_t* m) { om_maybe_flush_all(m); }  /* Reset :94-104 (window state is implicit) */
+/* MapBack :428-452.  The reference walks a window left/right; the range it
+ * settles on is the one of non-zero A' width holding aprime, so a scan from
+ * the left gives the same answer. */
+static int om_map_back(offmap_t* m, int ap) {
+  om_maybe_flush_all(m);
+  if (ap < 0) return 0;
+  if (m->max_ap <= ap) return (ap - m->max_ap) + m->max_a;
+  int lo_a = 0, lo_ap = 0, i = 0;
+  while (i < m->n) {
+    int op = OM_PREFIX, len = 0;
+    while (i < m->n && op == OM_PREFIX) {                    /* ParseNext :316-330 */
+      uint8_t c = m->d[i++];
+      op = c >> 6;
+      len = (len << 6) + (c & 0x3F);
+    }
+    if (op == OM_PREFIX) break;
+    int hi_a = lo_a + (op == OM_INSERT ? 0 : len), hi_ap = lo_ap + (op == OM_DELETE ? 0 : len);
+    if (ap < hi_ap) {
+      int a = ap - (lo_ap - lo_a);
+      return a >= hi_a ? hi_a : a;
+    }
+    lo_a = hi_a; lo_ap = hi_ap;
+  }
+  return (ap - m->max_ap) + m->max_a;     /* SetRight (not reached for well-formed maps) */
+}
+
+/* ResultChunk (compact_lang_det.h:147-153) and its vector */
+typedef struct { int32_t offset, bytes; uint16_t lang1, pad; } rchunk_t;
+typedef struct { rchunk_t* v; int n, cap; } rvec_t;
+static void rvec_push(rvec_t* r, rchunk_t c) {
+  if (r->n == r->cap) { r->cap = r->cap ? 2 * r->cap : 64; r->v = (rchunk_t*)realloc(r->v, sizeof(rchunk_t) * (size_t)r->cap); }
+  r->v[r->n++] = c;
+}
+
 /* --------------------------------------------------- UTF-8 state machines */
 static int utf8_len(uint8_t c) {            /* kUTF8LenTbl, utf8statetable.h:266-277 */
   return c < 0xC0 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
@@ -365,10 +464,10 @@ static int scan_to_letter_or_special(const uint8_t* isrc, int len) {
   return (int)(src - isrc);
 }
 
-/* UTF8GenericReplace(utf8repl_lettermarklower, plain text), offset map
- * omitted (it only feeds ResultChunkVector).  utf8statetable.cc:608-867 and
- * the kExitDoAgain driver loop :1138-1169.  Returns bytes filled. */
-static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen, int plain) {
+/* UTF8GenericReplace(utf8repl_lettermarklower), utf8statetable.cc:608-867
+ * and the kExitDoAgain driver loop :1138-1169, with the offset map
+ * (map2uplow_) when om != NULL.  Returns bytes filled. */
+static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen, int plain, offmap_t* om) {
   const sm_t* sm = &T.lower;
   int total_filled = 0;
   const uint8_t* in = isrc; int inlen = ilen;
@@ -377,6 +476,7 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen,
     int sh = (int)sm->shift;
     int nEntries = 1 << sh;
     const uint8_t* src = in;
+    const uint8_t* copystart = in;
     const uint8_t* srclimit = in + inlen;
     uint8_t* dst = out;
     uint8_t* dstlimit = out + outlen;
@@ -403,12 +503,18 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen,
         int offset = 0;
         switch (e) {
           case kExitReplace31:
-            dst -= 2; dst[-1] = (uint8_t)t8(sm, tb + c + nEntries * 1); goto do_state_table;
+            dst -= 2;
+            if (om) { om_copy(om, (int)(src - copystart) - 2); om_delete(om, 2); copystart = src; }
+            dst[-1] = (uint8_t)t8(sm, tb + c + nEntries * 1); goto do_state_table;
           case kExitReplace32:
-            dst--; dst[-2] = (uint8_t)t8(sm, tb + c + nEntries * 2);
+            dst--;
+            if (om) { om_copy(om, (int)(src - copystart) - 1); om_delete(om, 1); copystart = src; }
+            dst[-2] = (uint8_t)t8(sm, tb + c + nEntries * 2);
             dst[-1] = (uint8_t)t8(sm, tb + c + nEntries * 1); goto do_state_table;
           case kExitReplace21:
-            dst--; dst[-1] = (uint8_t)t8(sm, tb + c + nEntries * 1); goto do_state_table;
+            dst--;
+            if (om) { om_copy(om, (int)(src - copystart) - 1); om_delete(om, 1); copystart = src; }
+            dst[-1] = (uint8_t)t8(sm, tb + c + nEntries * 1); goto do_state_table;
           case kExitReplace3:
             dst[-3] = (uint8_t)t8(sm, tb + c + nEntries * 3);
             /* fallthrough */
@@ -443,6 +549,14 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen,
             for (int k = 0; k < add_len; ++k)
               dst[k] = ((uint32_t)(string_offset + k) < sm->n_rstr) ? sm->rstr[string_offset + k] : 0;
             dst += add_len;
+            if (om) {
+              if (add_len > del_len) {
+                om_copy(om, (int)(src - copystart)); om_insert(om, add_len - del_len); copystart = src;
+              } else if (add_len < del_len) {
+                om_copy(om, (int)(src - copystart) + add_len - del_len); om_delete(om, del_len - add_len);
+                copystart = src;
+              }
+            }
             if (re[0] & 0x80) {
               int ne = ((uint32_t)(string_offset + add_len) < sm->n_rstr) ? sm->rstr[string_offset + add_len] : 0;
               tb = tb0 + ((int64_t)ne << sh);
@@ -466,6 +580,7 @@ static int lower_replace(const uint8_t* isrc, int ilen, uint8_t* odst, int olen,
         e = kExitOK;
       }
     }
+    if (om && src > copystart) { om_copy(om, (int)(src - copystart)); copystart = src; }
   done_nobackup:;
     int consumed = (int)(src - in), filled = (int)(dst - out);
     total_filled += filled;
@@ -666,6 +781,8 @@ typedef struct {
   uint8_t* sbuf;            /* script_buffer_       kMaxScriptBuffer + pad */
   uint8_t* lbuf;            /* script_buffer_lower_ kMaxScriptLowerBuffer + pad */
   int plain;                /* is_plain_text_ */
+  offmap_t* map_orig;       /* map2original_ (ResultChunkVector mode only, else NULL) */
+  offmap_t* map_low;        /* map2uplow_ */
 } scanner_t;
 
 typedef struct {
@@ -707,6 +824,7 @@ static int skip_to_front_of_span(const uint8_t* src, int len, int* script, int p
 static int get_one_script_span(scanner_t* ss, span_t* span) {
   const int common = (int)T.meta.ulscript_common, inherited = (int)T.meta.ulscript_inherited;
   const int plain = ss->plain;
+  offmap_t* mo = ss->map_orig;     /* map2original_ (:833-1023), ResultChunkVector mode only */
   span->text = ss->sbuf; span->text_bytes = 0; span->offset = ss->next; span->ulscript = 0;
   int put_soft_limit = kMaxScriptBytes - kWithinScriptTail;
   if (kMaxScriptBytes <= ss->remaining && ss->remaining < 2 * kMaxScriptBytes)
@@ -715,9 +833,14 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
   uint8_t* sb = ss->sbuf;
   sb[0] = ' '; sb[1] = 0;
   int take = 0, put = 1;
+  if (mo) { om_clear(mo); om_delete(mo, span->offset); }
   int skip = skip_to_front_of_span(ss->buf + ss->next, ss->remaining, &spanscript, plain);
   ss->next += skip; ss->remaining -= skip;
-  if (ss->remaining <= 0) return 0;
+  if (mo) {
+    if (skip != 1) { om_delete(mo, skip); om_insert(mo, 1); }
+    else om_copy(mo, 1);
+  }
+  if (ss->remaining <= 0) { if (mo) om_reset(mo); return 0; }
   span->ulscript = spanscript;
   const uint8_t* nb = ss->buf + ss->next;
   int bl = ss->remaining;
@@ -744,11 +867,17 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
       }
       if (need_break) break;
       take += tlen; put += plen;
+      if (mo) {
+        if (tlen == plen) om_copy(mo, tlen);
+        else if (tlen < plen) { om_copy(mo, tlen); om_insert(mo, plen - tlen); }
+        else { om_copy(mo, plen); om_delete(mo, tlen - plen); }
+      }
       if (put >= kMaxScriptBytes) break;
     }
     while (take < bl) {
       tlen = scan_to_letter_or_special(nb + take, bl - take);
       take += tlen;
+      if (mo) om_delete(mo, tlen);
       if (take >= bl) break;
       if (!plain && is_special(nb[take])) {
         if (nb[take] == '<') {
@@ -767,27 +896,34 @@ static int get_one_script_span(scanner_t* ss, span_t* span) {
       }
       if (sc != 0) break;
       take += tlen;
+      if (mo) om_delete(mo, tlen);
     }
     sb[put++] = ' ';
+    if (mo) om_insert(mo, 1);
     if (sc != spanscript && sc != inherited) break;
     if (put >= put_soft_limit) break;
   }
+  /* back up to a character boundary: the map is not adjusted (:998-1004) */
   while (0 < take && take < bl && (nb[take] & 0xC0) == 0x80) { --take; --put; }
   ss->next += take; ss->remaining -= take;
   sb[put + 0] = ' '; sb[put + 1] = ' '; sb[put + 2] = ' '; sb[put + 3] = 0;
+  if (mo) { om_insert(mo, 4); om_reset(mo); }
   span->text_bytes = put;
   return 1;
 }
 
 /* ScriptScanner::LowerScriptSpan getonescriptspan.cc:1033-1054 */
 static void lower_script_span(scanner_t* ss, span_t* span) {
-  int filled = lower_replace(span->text, span->text_bytes + 3, ss->lbuf, kMaxScriptLowerBuffer, ss->plain);
+  if (ss->map_low) om_clear(ss->map_low);
+  int filled = lower_replace(span->text, span->text_bytes + 3, ss->lbuf, kMaxScriptLowerBuffer, ss->plain,
+                             ss->map_low);
   ss->lbuf[filled] = 0;
   /* bytes past `filled` are never semantically read (masked hash loads,
    * NUL-stopped advances); keep them NUL so invalid input is deterministic */
   ss->lbuf[filled + 1] = 0; ss->lbuf[filled + 2] = 0; ss->lbuf[filled + 3] = 0;
   span->text = ss->lbuf;
   span->text_bytes = filled - 3;
+  if (ss->map_low) om_reset(ss->map_low);
 }
 
 /* ----------------------------------------------------------- squeezing */
@@ -901,6 +1037,81 @@ static int cheap_squeeze_inplace(uint8_t* isrc, int src_len, int ichunksize, int
       }
       if (len > 0) { memmove(dst, src, (size_t)len); dst += len; }
     }
+    src += len;
+  }
+  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
+  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
+  return (int)(dst - isrc);
+}
+/* CheapRepWordsInplaceOverwrite :697-765 (ResultChunkVector mode): well-
+ * predicted words become '.' runs in place, the length is kept */
+static int cheap_rep_words_inplace_overwrite(uint8_t* isrc, int src_len, int* hash, int* tbl) {
+  const uint8_t* src = isrc;
+  const uint8_t* lim = isrc + src_len;
+  uint8_t* dst = isrc;
+  int h = *hash;
+  uint8_t* word_dst = dst;
+  int good = 0, wlen = 0;
+  while (src < lim) {
+    int c = src[0], incr = 1;
+    *dst++ = (uint8_t)c;
+    if (c == ' ') {
+      if (good * 2 > wlen)
+        for (uint8_t* p = word_dst; p < dst - 1; ++p) *p = '.';
+      word_dst = dst; good = 0; wlen = 0;
+    }
+    if (c < 0xC0) {
+    } else if ((c & 0xE0) == 0xC0) { *dst++ = src[1]; c = (c << 8) | src[1]; incr = 2; }
+    else if ((c & 0xF0) == 0xE0) { *dst++ = src[1]; *dst++ = src[2]; c = (c << 16) | (src[1] << 8) | src[2]; incr = 3; }
+    else {
+      *dst++ = src[1]; *dst++ = src[2]; *dst++ = src[3];
+      c = (int)(((uint32_t)c << 24) | ((uint32_t)src[1] << 16) | ((uint32_t)src[2] << 8) | src[3]); incr = 4;
+    }
+    src += incr;
+    wlen += incr;
+    int p = tbl[h];
+    tbl[h] = c;
+    if (c == p) good += incr;
+    h = ((h << 4) ^ c) & 0xFFF;
+  }
+  *hash = h;
+  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
+  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
+  return (int)(dst - isrc);
+}
+/* CheapSqueezeInplaceOverwrite :869-939 */
+static int cheap_squeeze_inplace_overwrite(uint8_t* isrc, int src_len, int ichunksize, int* tbl) {
+  uint8_t* src = isrc;
+  uint8_t* dst = src;
+  uint8_t* lim = src + src_len;
+  int skipping = 0, hash = 0;
+  memset(tbl, 0, kPredictionTableSize * sizeof(int));
+  int chunksize = ichunksize ? ichunksize : kChunksizeDefault;
+  int space_thresh = (chunksize * kSpacesThreshPercent) / 100;
+  int predict_thresh = (chunksize * kPredictThreshPercent) / 100;
+  ++src; ++dst;                                   /* always keep the leading space */
+  while (src < lim) {
+    int remaining = (int)(lim - src);
+    int len = remaining < chunksize ? remaining : chunksize;
+    while ((src[len] & 0xC0) == 0x80) ++len;
+    int space_n = count_spaces4(src, len);
+    int predb_n = count_predicted_bytes(src, len, &hash, tbl);
+    if (space_n >= space_thresh || predb_n >= predict_thresh) {
+      if (!skipping) {
+        int n = backscan_to_space(dst, (int)(dst - isrc));
+        for (uint8_t* p = dst - n; p < dst; ++p) *p = '.';
+        skipping = 1;
+      }
+      for (uint8_t* p = dst; p < dst + len; ++p) *p = '.';
+      dst[len - 1] = ' ';
+    } else {
+      if (skipping) {
+        int n = forwardscan_to_space(src, len);
+        for (uint8_t* p = dst; p < dst + n - 1; ++p) *p = '.';
+        skipping = 0;
+      }
+    }
+    dst += len;
     src += len;
   }
   if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
@@ -1061,6 +1272,8 @@ struct cldo_ctx {
   int trace_text;                              /* also trace each lowered span's bytes (hex) */
   int plain;                                   /* is_plain_text (HTML mode when 0) */
   uint32_t priors[16];                         /* ApplyHints result: boost latn[4] othr[4], whack latn[4] othr[4] */
+  rvec_t* vec;                                 /* ResultChunkVector being built, or NULL */
+  offmap_t map_orig, map_low;                  /* the scanner's maps (vec mode) */
 };
 
 static void tracef(struct cldo_ctx* c, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -1486,6 +1699,127 @@ static void trace_chunk(struct cldo_ctx* c, int i, const chunksum_t* cs) {
          cs->bytes, cs->grams, script_code(cs->ulscript), cs->rel_delta, cs->rel_score);
 }
 
+/* ------------------------------------------------- ResultChunkVector */
+static int same_close_set(int l1, int l2) {                  /* SameCloseSet scoreonescriptspan.cc:44-56 */
+  int c1 = close_set(l1);
+  return c1 != 0 && c1 == close_set(l2);
+}
+/* GetLangScore cldutil.cc:141-152 */
+static int get_lang_score(uint32_t lp, uint8_t pslang) {
+  const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
+  int r = 0;
+  if (((lp >> 8) & 0xFF) == pslang) r += e[5];
+  if (((lp >> 16) & 0xFF) == pslang) r += e[6];
+  if (((lp >> 24) & 0xFF) == pslang) r += e[7];
+  return r;
+}
+/* BetterBoundary scoreonescriptspan.cc:671-720 (debug output omitted) */
+static int better_boundary(const hitbuf_t* hb, uint8_t ps0, uint8_t ps1, int lin0, int lin1, int lin2) {
+  if (lin2 - lin0 <= 8) return lin1;
+  int running = 0, diff[8];
+  for (int i = lin0; i < lin0 + 8; ++i) {
+    int j = i & 7;
+    uint32_t lp = hb->linear[i].langprob;
+    diff[j] = get_lang_score(lp, ps0) - get_lang_score(lp, ps1);
+    if (i < lin0 + 4) running += diff[j]; else running -= diff[j];
+  }
+  int best_value = 0, best = lin1;
+  for (int i = lin0; i < lin2 - 8; ++i) {
+    int j = i & 7;
+    if (best_value < running) {
+      int plus = 0, minus = 0;
+      for (int kk = 0; kk < 8; ++kk) { if (diff[kk] > 0) plus = 1; if (diff[kk] < 0) minus = 1; }
+      if (plus && minus) { best_value = running; best = i + 4; }
+    }
+    uint32_t lp = hb->linear[i + 8].langprob;
+    int nd = get_lang_score(lp, ps0) - get_lang_score(lp, ps1);
+    int md = diff[(i + 4) & 7], od = diff[j];
+    diff[j] = nd;
+    running -= od; running += 2 * md; running -= nd;
+  }
+  return best;
+}
+/* SharpenBoundaries :764-829; sb[n] is the dummy end entry */
+static void sharpen_boundaries(const hitbuf_t* hb, int ulscript, chunksum_t* sb, int n) {
+  int prior_linear = sb[0].chunk_start;
+  uint16_t prior_lang = sb[0].lang1;
+  for (int i = 1; i < n; ++i) {
+    chunksum_t* cs = &sb[i];
+    uint16_t this_lang = cs->lang1;
+    if (this_lang == prior_lang) { prior_linear = cs->chunk_start; continue; }
+    int this_linear = cs->chunk_start, next_linear = sb[i + 1].chunk_start;
+    if (same_close_set(prior_lang, this_lang)) { prior_linear = this_linear; prior_lang = this_lang; continue; }
+    uint8_t ps0 = per_script_number(ulscript, prior_lang), ps1 = per_script_number(ulscript, this_lang);
+    int better = better_boundary(hb, ps0, ps1, prior_linear, this_linear, next_linear);
+    int old_off = hb->linear[this_linear].offset, new_off = hb->linear[better].offset;
+    cs->chunk_start = (uint16_t)better;
+    cs->offset = (uint16_t)new_off;
+    cs->bytes = (uint16_t)(cs->bytes - (new_off - old_off));
+    sb[i - 1].bytes = (uint16_t)(sb[i - 1].bytes + (new_off - old_off));
+    prior_linear = better;
+    prior_lang = this_lang;
+  }
+}
+/* ScriptScanner::MapBack getonescriptspan.cc:1076-1078 */
+static int scanner_map_back(struct cldo_ctx* c, int t) {
+  return om_map_back(&c->map_orig, om_map_back(&c->map_low, t));
+}
+/* ItemToVector :322-355 (kMaxResultChunkBytes = 0x7fffffff) */
+static void item_to_vector(rvec_t* vec, int new_lang, int mapped_offset, int mapped_len) {
+  if (vec->n > 0) {
+    rchunk_t* prior = &vec->v[vec->n - 1];
+    if (new_lang == prior->lang1) { prior->bytes = (mapped_offset + mapped_len) - prior->offset; return; }
+  }
+  rchunk_t rc = {mapped_offset, mapped_len, (uint16_t)new_lang, 0};
+  rvec_push(vec, rc);
+}
+/* SummaryBufferToVector :386-495 */
+static void summary_buffer_to_vector(struct cldo_ctx* c, const chunksum_t* sb, int n) {
+  rvec_t* vec = c->vec;
+  const uint8_t* buf = c->ss.buf;
+  const int unk = (int)T.meta.unknown_language;
+  for (int i = 0; i < n; ++i) {
+    const chunksum_t* cs = &sb[i];
+    int unmapped_offset = cs->offset, unmapped_len = cs->bytes;
+    int mapped_offset = scanner_map_back(c, unmapped_offset);
+    if (mapped_offset > 0) {
+      int prior_size = vec->n > 0 ? vec->v[vec->n - 1].bytes : 0;
+      int n_limit = prior_size - 3 < mapped_offset ? prior_size - 3 : mapped_offset;
+      if (n_limit > 12) n_limit = 12;
+      const uint8_t* us = buf + mapped_offset;
+      int k = 0;
+      while (k < n_limit && us[-k - 1] >= 0x41) ++k;
+      if (k >= n_limit) k = 0;
+      if (k < n_limit) {
+        uint8_t ch = us[-k - 1];
+        if (ch == '\'' || ch == '"' || ch == '#' || ch == '@') ++k;
+      }
+      if (k > 0) {
+        vec->v[vec->n - 1].bytes -= k;
+        mapped_offset -= k;
+      }
+    }
+    int mapped_len = scanner_map_back(c, unmapped_offset + unmapped_len) - mapped_offset;
+    int new_lang = cs->lang1;
+    int delta_bad = cs->rel_delta < kUnreliablePercentThreshold;
+    int score_bad = cs->rel_score < kUnreliablePercentThreshold;
+    uint16_t prior_lang = vec->n > 0 ? vec->v[vec->n - 1].lang1 : (uint16_t)unk;
+    if (prior_lang == cs->lang1) delta_bad = 0;
+    if (same_close_set(cs->lang1, prior_lang)) { new_lang = prior_lang; delta_bad = 0; }
+    if (same_close_set(cs->lang1, cs->lang2) && prior_lang == cs->lang2) { new_lang = prior_lang; delta_bad = 0; }
+    uint16_t next_lang = (i + 1 >= n) ? (uint16_t)unk : sb[i + 1].lang1;
+    if (delta_bad && prior_lang == cs->lang2 && next_lang == cs->lang2) { new_lang = prior_lang; delta_bad = 0; }
+    if (delta_bad || score_bad) new_lang = unk;
+    item_to_vector(vec, new_lang, mapped_offset, mapped_len);
+  }
+}
+/* JustOneItemToVector :499-530 */
+static void just_one_item_to_vector(struct cldo_ctx* c, int lang1, int unmapped_offset, int unmapped_len) {
+  int mapped_offset = scanner_map_back(c, unmapped_offset);
+  int mapped_len = scanner_map_back(c, unmapped_offset + unmapped_len) - mapped_offset;
+  item_to_vector(c->vec, lang1, mapped_offset, mapped_len);
+}
+
 /* ProcessHitBuffer :1067-1116 (vec == NULL) */
 static void process_hit_buffer(struct cldo_ctx* c, ctx_t* cx, const span_t* span, int score_cjk,
                                hitbuf_t* hb, doctote_t* dt) {
@@ -1513,6 +1847,11 @@ static void process_hit_buffer(struct cldo_ctx* c, ctx_t* cx, const span_t* span
     score_one_chunk(cx, hb, i, span->ulscript, &cs);
     if (n < kMaxSummaries) sb[n++] = cs;
   }
+  /* the dummy entry off the end (ScoreAllHits :289-297) */
+  memset(&sb[n], 0, sizeof(sb[n]));
+  sb[n].offset = hb->linear[hb->next_linear].offset;
+  sb[n].chunk_start = (uint16_t)hb->next_linear;
+  if (c->vec) sharpen_boundaries(hb, cx->ulscript, sb, n);
   if (c->trace) {
     tracef(c, "summary %d", n);
     for (int i = 0; i < n; ++i) trace_chunk(c, i, &sb[i]);
@@ -1522,6 +1861,7 @@ static void process_hit_buffer(struct cldo_ctx* c, ctx_t* cx, const span_t* span
     int rel = sb[i].rel_delta < sb[i].rel_score ? sb[i].rel_delta : sb[i].rel_score;
     doctote_add(dt, sb[i].lang1, sb[i].bytes, sb[i].score1, rel);
   }
+  if (c->vec) summary_buffer_to_vector(c, sb, n);
 }
 
 /* SpliceHitBuffer :1118-1127 */
@@ -1546,6 +1886,7 @@ static void score_one_script_span(struct cldo_ctx* c, ctx_t* cx, const span_t* s
   if (rt == RTypeNone || rt == RTypeOne) {
     int bytes = span->text_bytes;
     doctote_add(dt, (uint16_t)default_language(span->ulscript), bytes, bytes, 100);
+    if (c->vec) just_one_item_to_vector(c, default_language(span->ulscript), 1, bytes - 1);
     return;
   }
   hitbuf_t* hb = &c->hb;
@@ -1570,8 +1911,26 @@ static void score_one_script_span(struct cldo_ctx* c, ctx_t* cx, const span_t* s
 }
 
 /* ------------------------------------------------------ doc-level passes */
+/* MoveLang1ToLang2's ResultChunkVector half (compact_lang_det_impl.cc:1122-1147) */
+static void move_lang1_to_lang2_vec(rvec_t* vec, int lang1, int lang2) {
+  if (!vec) return;
+  int k = 0;
+  uint16_t prior_lang = (uint16_t)T.meta.unknown_language;
+  for (int i = 0; i < vec->n; ++i) {
+    rchunk_t* rc = &vec->v[i];
+    if (rc->lang1 == lang1) rc->lang1 = (uint16_t)lang2;
+    if (rc->lang1 == prior_lang && k > 0) {
+      vec->v[k - 1].bytes += rc->bytes;
+    } else {
+      vec->v[k] = vec->v[i];
+      ++k;
+    }
+    prior_lang = rc->lang1;
+  }
+  vec->n = k;
+}
 /* RefineScoredClosePairs + MoveLang1ToLang2 compact_lang_det_impl.cc:1105-1203 */
-static void refine_scored_close_pairs(doctote_t* d) {
+static void refine_scored_close_pairs(doctote_t* d, rvec_t* vec) {
   for (int s = 0; s < 24; ++s) {
     int cs = close_set(d->key[s]);
     if (cs == 0) continue;
@@ -1579,10 +1938,12 @@ static void refine_scored_close_pairs(doctote_t* d) {
       if (close_set(d->key[s2]) == cs) {
         int from, to;
         if (d->value[s] < d->value[s2]) { from = s; to = s2; } else { from = s2; to = s; }
+        const int from_lang = d->key[from], to_lang = d->key[to];
         d->value[to] += d->value[from];
         d->score[to] += d->score[from];
         d->rel[to] += d->rel[from];
         d->key[from] = kUnusedKey; d->score[from] = 0; d->rel[from] = 0;
+        move_lang1_to_lang2_vec(vec, from_lang, to_lang);
         break;
       }
     }
@@ -1754,6 +2115,9 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
     memcpy(cx.prior_whack, c->priors + 8, 8 * sizeof(uint32_t));
     scanner_t* ss = &c->ss;
     ss->buf = buf; ss->next = 0; ss->remaining = len; ss->plain = c->plain;
+    ss->map_orig = c->vec ? &c->map_orig : NULL;
+    ss->map_low = c->vec ? &c->map_low : NULL;
+    if (c->vec) c->vec->n = 0;              /* resultchunkvector->clear() (:1730-1732) */
     int hash = 0;
     if (flags & kCLDFlagRepeats) memset(c->predict, 0, sizeof(c->predict));
     int total = 0, restart = 0;
@@ -1777,7 +2141,8 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
         free(h);
       }
       if (flags & kCLDFlagSqueeze) {
-        span.text_bytes = cheap_squeeze_inplace(span.text, span.text_bytes, 0, c->sqz_tbl);
+        span.text_bytes = c->vec ? cheap_squeeze_inplace_overwrite(span.text, span.text_bytes, 0, c->sqz_tbl)
+                                 : cheap_squeeze_inplace(span.text, span.text_bytes, 0, c->sqz_tbl);
       } else if ((kCheapSqueezeTestThresh >> 1) < span.text_bytes && !(flags & kCLDFlagFinish)) {
         if (cheap_squeeze_trigger_test(span.text, span.text_bytes, kCheapSqueezeTestLen, c->sqz_tbl)) {
           flags |= kCLDFlagSqueeze; restart = 1;
@@ -1786,14 +2151,15 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
         }
       }
       if (flags & kCLDFlagRepeats)
-        span.text_bytes = cheap_rep_words_inplace(span.text, span.text_bytes, &hash, c->predict);
+        span.text_bytes = c->vec ? cheap_rep_words_inplace_overwrite(span.text, span.text_bytes, &hash, c->predict)
+                                 : cheap_rep_words_inplace(span.text, span.text_bytes, &hash, c->predict);
       cx.ulscript = span.ulscript;
       score_one_script_span(c, &cx, &span, &dt);
       total += span.text_bytes;
     }
     if (restart) continue;
     trace_doctote(c, &dt);
-    refine_scored_close_pairs(&dt);
+    refine_scored_close_pairs(&dt, c->vec);
     int rp3[3], lang3[3], pct3[3], tb, rel;
     double ns3[3];
     doctote_sort(&dt, 3);
@@ -1814,6 +2180,13 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
         r->reliable_percent3[i] = rp3[i];
       }
       r->text_bytes = tb; r->is_reliable = (uint8_t)rel; r->summary_lang = (uint16_t)summary;
+      if (c->vec && c->vec->n > 0) {         /* FinishResultVector(0, buffer_length) (:1688-1702) */
+        rchunk_t* rc = &c->vec->v[0];
+        if (rc->offset > 0) { int diff = rc->offset; rc->offset -= diff; rc->bytes += diff; }
+        rchunk_t* rc2 = &c->vec->v[c->vec->n - 1];
+        int hi2 = rc2->offset + rc2->bytes;
+        if (hi2 < len) rc2->bytes += len - hi2;
+      }
       if (c->trace) {
         char line[256]; int o = 0;
         for (int i = 0; i < 3; ++i)
@@ -1839,6 +2212,7 @@ cldo_ctx* cldo_ctx_new(void) {
 }
 void cldo_ctx_free(cldo_ctx* c) {
   if (!c) return;
+  free(c->map_orig.d); free(c->map_low.d);
   free(c->ss.sbuf); free(c->ss.lbuf); free(c->docbuf); free(c);
 }
 void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg) { c->trace = fn; c->trace_arg = arg; }
@@ -1858,6 +2232,24 @@ int cldo_detect(cldo_ctx* c, const char* text, int len, cldo_result* r) {
   memset(c->docbuf + len, 0, 16);
   memset(r, 0, sizeof(*r));
   return detect_summary_v2(c, c->docbuf, len, r);
+}
+
+/* ExtDetectLanguageSummary with a ResultChunkVector (compact_lang_det.h:261-294):
+ * up to cap chunks copied to out; returns the vector size (may exceed cap),
+ * or a negative error. */
+int cldo_detect_vec(cldo_ctx* c, const char* text, int len, int is_plain_text, const uint32_t* priors,
+                    cldo_result* r, cldo_rchunk* out, int cap) {
+  rvec_t vec = {NULL, 0, 0};
+  c->vec = &vec;
+  int lang = cldo_detect_ex(c, text, len, is_plain_text, priors, r);
+  c->vec = NULL;
+  if (lang < 0) { free(vec.v); return lang; }
+  for (int i = 0; i < vec.n && i < cap; ++i) {
+    out[i].offset = vec.v[i].offset; out[i].bytes = vec.v[i].bytes; out[i].lang1 = vec.v[i].lang1; out[i].pad = 0;
+  }
+  int n = vec.n;
+  free(vec.v);
+  return n;
 }
 
 /* wrapper.cc:7-16 + compact_lang_det.cc:91-93 (UNKNOWN -> ENGLISH) */
@@ -2049,7 +2441,7 @@ int cldo_read_entity(const char* text, int len, int* consumed) {
 }
 
 int cldo_lower(const char* in, int len, char* out, int olen) {
-  return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen, 1);
+  return lower_replace((const uint8_t*)in, len, (uint8_t*)out, olen, 1, NULL);
 }
 int cldo_script_num(const char* s) { return script_num((const uint8_t*)s); }
 

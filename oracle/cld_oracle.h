@@ -24,6 +24,11 @@ typedef struct {   /* ChunkSummary, scoreonescriptspan.h:240-252 */
   uint8_t rel_delta, rel_score;
 } cldo_chunk;
 
+typedef struct {   /* ResultChunk, compact_lang_det.h:147-153 */
+  int32_t offset, bytes;
+  uint16_t lang1, pad;
+} cldo_rchunk;
+
 typedef struct cldo_ctx cldo_ctx;
 typedef void (*cldo_trace_fn)(void* arg, const char* line);
 
@@ -40,6 +45,8 @@ int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_resu
  * othr[4]), NULL for none; batch forms take one flag / 16 priors per document. */
 int cldo_detect_ex(cldo_ctx* c, const char* text, int len, int is_plain_text, const uint32_t* priors,
                    cldo_result* r);
+int cldo_detect_vec(cldo_ctx* c, const char* text, int len, int is_plain_text, const uint32_t* priors,
+                    cldo_result* r, cldo_rchunk* out, int cap);
 int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
                          const uint32_t* priors, cldo_result* out, int threads);
 /* handlers.go:150-151 text preparation: flags 1 = StripExtras, 2 = C-string cut.

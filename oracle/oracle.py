@@ -39,6 +39,9 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
+CHUNK_DTYPE = np.dtype([("offset", "<i4"), ("bytes", "<i4"), ("lang1", "<u2"), ("pad", "<u2")])
+
+
 class Oracle:
     def __init__(self, tables=DEFAULT_TABLES):
         if not os.path.exists(LIB):
@@ -121,6 +124,22 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("cldo_detect_batch_ex rc=%d" % rc)
         return out
+
+    def detect_vec(self, doc, plain=True, priors=None):
+        """ExtDetectLanguageSummary with a ResultChunkVector -> (Result, chunks
+        as a structured array offset/bytes/lang1)."""
+        b = bytes(doc)
+        r = Result()
+        cap = len(b) + 16
+        ch = np.zeros(cap, dtype=CHUNK_DTYPE)
+        pr = None if priors is None else np.ascontiguousarray(priors, dtype=np.uint32)
+        self.lib.cldo_detect_vec.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.POINTER(Result), ctypes.c_void_p, ctypes.c_int]
+        n = self.lib.cldo_detect_vec(self.ctx, b, len(b), int(plain), None if pr is None else pr.ctypes.data,
+                                     ctypes.byref(r), ch.ctypes.data, cap)
+        if n < 0:
+            raise RuntimeError("cldo_detect_vec rc=%d" % n)
+        return r, ch[:n].copy()
 
     def prepare_batch(self, buf, offsets, flags):
         """handlers.go:150-151 (StripExtras = 1, C-string cut = 2) -> (buf, offsets)."""

@@ -118,3 +118,44 @@ def test_oracle_equals_reference_html_and_hints(oracles):
         pr = priors_for(cld_amd, buf, offs, False, hints)
         same(o.detect_batch_ex(buf, offs, priors=pr, threads=8), r.detect_batch(buf, offs, hints=hints, threads=8),
              cfg + " hints")
+
+
+def _vec(ch):
+    return [(int(x["offset"]), int(x["bytes"]), int(x["lang1"])) for x in ch]
+
+
+@needs_ref
+def test_result_chunk_vector_equals_reference(oracles):
+    """ExtDetectLanguageSummary with a ResultChunkVector: the oracle's offset
+    maps (OffsetMap in the scanner and the lowercaser), SharpenBoundaries /
+    BetterBoundary, SummaryBufferToVector, the Overwrite variants of
+    Squeeze/RepWords, MoveLang1ToLang2's vector merge and FinishResultVector
+    must give the reference's vector, chunk for chunk, and the same summary
+    fields (which SharpenBoundaries changes through the chunk byte counts)."""
+    import cld_amd
+    from test_gpu_html_hints import random_hints
+    o = _oracle(oracles, SYNTH)
+    r = ref(SYNTH)
+    cases = []
+    for cfg, n in (("c2", 1500), ("c3", 60), ("c4", 1000), ("c5", 1500)):
+        buf, offs = corpus.GENERATORS[cfg](n)
+        cases += [(bytes(buf[offs[i]:offs[i + 1]]), True, None) for i in range(n)]
+    buf, offs = corpus.c3(40, boiler_frac=0.5)                     # squeeze restarts: Overwrite variant
+    cases += [(bytes(buf[offs[i]:offs[i + 1]]), True, None) for i in range(40)]
+    buf, offs = corpus.html(300, seed=9)                            # HTML: tags and entities in the maps
+    cases += [(bytes(buf[offs[i]:offs[i + 1]]), False, None) for i in range(300)]
+    buf, offs = corpus.c2(800, seed=77)
+    hints = random_hints(cld_amd, 800, 78)
+    cases += [(bytes(buf[offs[i]:offs[i + 1]]), True, hints[i]) for i in range(800)]
+    multi = 0
+    for doc, plain, h in cases:
+        pri = None
+        if h is not None or not plain:
+            _, pri = cld_amd.hint_priors(doc, html=not plain, hints=h)
+        ra, ca = o.detect_vec(doc, plain=plain, priors=pri)
+        rb, cb = r.detect_vec(doc, plain=plain, hints=h)
+        assert _vec(ca) == _vec(cb), doc[:120]
+        assert (ra.summary_lang, list(ra.lang3), list(ra.percent3), ra.text_bytes, list(ra.normalized3)) == \
+            (rb["summary_lang"], list(rb["lang3"]), list(rb["percent3"]), rb["text_bytes"], list(rb["normalized3"]))
+        multi += len(ca) > 1
+    assert multi > 200
