@@ -58,6 +58,16 @@ typedef struct cld_result {
  * become hints (compact_lang_det_impl.cc:1596-1611). */
 #define CLD_FLAG_HTML 4u
 
+/* ResultChunk (compact_lang_det.h:147-153): one piece of a document in one
+ * language; offset/bytes index the document as given; lang1 is a Language
+ * enum, UNKNOWN_LANGUAGE (26) for unreliable or too-short pieces. */
+typedef struct cld_chunk {
+  int32_t offset;
+  int32_t bytes;
+  uint16_t lang1;
+  uint16_t pad;
+} cld_chunk;
+
 /* CLDHints (compact_lang_det.h:134-139): per-document priors. */
 typedef struct cld_hints {
   const char* content_language_hint;  /* "mi,en" boosts Maori and English; NULL / "" for none */
@@ -129,6 +139,23 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
  * are the same fields as cld_detect_batch.  Host buffers; blocks. */
 int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
                         uint32_t flags, cld_result* out);
+
+/* ExtDetectLanguageSummary with a ResultChunkVector per document
+ * (compact_lang_det.h:261-294): the same results as cld_detect_batch_ex plus
+ * each document's chunk vector -- pieces of the document as given, in one
+ * language each (SummaryBufferToVector / SharpenBoundaries / OffsetMap,
+ * scoreonescriptspan.cc:389-548, 671-845; offsetmap.cc).  Vector mode changes
+ * scoring the way the reference's does (SharpenBoundaries moves chunk bytes,
+ * Squeeze/RepWords overwrite instead of cutting), so `out` can differ from
+ * cld_detect_batch_ex's for the same document, exactly as there.
+ * chunk_offsets[n+1] receives document i's chunks as
+ * chunks[chunk_offsets[i] .. chunk_offsets[i+1]).  If chunk_cap is too small
+ * the call returns CLD_ENOMEM with out and chunk_offsets complete and chunks
+ * holding the first chunk_cap entries.  Every document runs the sequential
+ * kernel (not a high-throughput path, as in the reference). */
+int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
+                         uint32_t flags, cld_result* out, cld_chunk* chunks, size_t chunk_cap,
+                         uint64_t* chunk_offsets);
 
 /* Host-only (no GPU): the ApplyHints result for one document.  priors: the
  * CLDLangPriors (OneCLDLangPrior = (weight << 10) + Language, at most 14)

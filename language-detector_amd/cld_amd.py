@@ -37,7 +37,8 @@ EXPORTS = ("detect_language", "cld_init", "cld_init_device", "cld_shutdown", "cl
            "cld_load_data_from_file", "cld_load_data_from_raw_address", "cld_unload_data",
            "cld_is_data_dynamic", "cld_export_tables", "cld_convert_data_file",
            "cld_detect_batch_device_ex", "cld_prepare_batch", "cld_host_alloc", "cld_host_free",
-           "cld_kernel_times", "cld_detect_batch_ex", "cld_hint_priors")
+           "cld_kernel_times", "cld_detect_batch_ex", "cld_hint_priors", "cld_detect_batch_vec")
+CHUNK_DTYPE = np.dtype([("offset", "<i4"), ("bytes", "<i4"), ("lang1", "<u2"), ("pad", "<u2")])   # cld_chunk
 
 
 class Hints(ctypes.Structure):
@@ -104,6 +105,9 @@ def lib():
         L.cld_host_free.argtypes = [ctypes.c_void_p]
         L.cld_detect_batch_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p]
+        L.cld_detect_batch_vec.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p]
         L.cld_hint_priors.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(Hints),
                                       ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
@@ -250,6 +254,40 @@ def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False):
     if rc != 0:
         raise CldError("cld_detect_batch_ex failed: %d" % rc)
     return out
+
+
+def detect_batch_vec(docs=None, buf=None, offsets=None, hints=None, html=False, chunk_cap=None):
+    """ExtDetectLanguageSummary with a ResultChunkVector per document:
+    (results, chunks [CHUNK_DTYPE], chunk_offsets[n+1]); document i's vector is
+    chunks[chunk_offsets[i]:chunk_offsets[i+1]]."""
+    if docs is not None:
+        buf, offsets = pack(docs)
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    coffs = np.zeros(n + 1, dtype=np.uint64)
+    if n == 0:
+        return out, np.zeros(0, dtype=CHUNK_DTYPE), coffs
+    harr = None
+    if hints is not None:
+        if len(hints) != n:
+            raise ValueError("need one Hints per document")
+        harr = (Hints * n)(*hints)
+    cap = chunk_cap if chunk_cap is not None else 4 * n + 1024
+    bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+    for _ in range(2):                                     # second try with the exact size
+        chunks = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
+        rc = lib().cld_detect_batch_vec(bptr, offsets.ctypes.data, n,
+                                        ctypes.cast(harr, ctypes.c_void_p) if harr else None,
+                                        FLAG_HTML if html else 0, out.ctypes.data, chunks.ctypes.data, cap,
+                                        coffs.ctypes.data)
+        if rc == 0:
+            return out, chunks[:int(coffs[-1])], coffs
+        if rc != -12 or chunk_cap is not None:
+            break
+        cap = int(coffs[-1])
+    raise CldError("cld_detect_batch_vec failed: %d" % rc)
 
 
 def hint_priors(doc=b"", html=False, hints=None):

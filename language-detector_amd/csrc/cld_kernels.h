@@ -34,6 +34,16 @@ constexpr int kLongWPB = 4;
 
 extern "C" {
 size_t cld_general_work_bytes();
+size_t cld_vec_work_bytes();
+// ResultChunkVector mode: all n documents in k_general_vec; document i builds
+// its vector in pool[pool_off[i] .. pool_off[i+1]) and writes its size (or -1)
+// to n_chunks[i]; counters[kCtrDequeue2] must be zero.
+hipError_t cld_launch_general_vec(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+                                  cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
+                                  const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
+                                  const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s);
+hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
+                                 const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
 size_t cld_short_work_bytes();
 // special (nullable): per-document kSpecial* bits; such documents are appended
 // to special_list under counters[special_ctr] instead of being scored

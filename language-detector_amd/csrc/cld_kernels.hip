@@ -83,6 +83,66 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
   }
 }
 
+// ResultChunkVector mode (cld_detect_batch_vec): every document runs the
+// exact sequential pipeline with its offset maps and chunk vector, one lane
+// per document, in its own arena.  Capacities: map2original_ gets at most ~3
+// ranges per span byte (kMaxScriptBuffer), map2uplow_ at most ~2 per lowered
+// byte; a document that would exceed one (or its pool region) reports -1.
+constexpr int kMapOrigCap = 3 * kMaxScriptBuffer + 4096;
+constexpr int kMapLowCap = 2 * kMaxScriptLowerBuffer + 4096;
+struct VecWork {
+  GeneralWork g;
+  VecOut vo;
+  uint8_t map_o[kMapOrigCap];
+  uint8_t map_l[kMapLowCap];
+};
+
+__global__ __launch_bounds__(64) void k_general_vec(DevTables T, const uint8_t* __restrict__ buf,
+                                                   const uint64_t* __restrict__ offs, int n,
+                                                   cld_result* __restrict__ out,
+                                                   uint8_t* __restrict__ arena, uint64_t stride,
+                                                   uint32_t* __restrict__ counters,
+                                                   const uint8_t* __restrict__ special,
+                                                   const uint32_t* __restrict__ priors,
+                                                   cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
+                                                   int32_t* __restrict__ n_chunks) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  VecWork& w = *reinterpret_cast<VecWork*>(arena + (uint64_t)lane * stride);
+  for (;;) {
+    const uint32_t k = atomicAdd(&counters[kCtrDequeue2], 1u);
+    if (k >= (uint32_t)n) break;                 // every lane reaches this exit
+    const uint32_t i = k;
+    const uint64_t a = offs[i], b = offs[i + 1];
+    VecOut& vo = w.vo;
+    vo.orig.d = w.map_o; vo.orig.cap = kMapOrigCap; vo.orig.n = 0; vo.orig.over = false;
+    vo.low.d = w.map_l; vo.low.cap = kMapLowCap; vo.low.n = 0; vo.low.over = false;
+    dm_clear(vo.orig); dm_clear(vo.low);
+    vo.v = pool + pool_off[i]; vo.cap = (int)(pool_off[i + 1] - pool_off[i]); vo.n = 0; vo.over = false;
+    vo.doc = buf + a; vo.doc_len = (int)(b - a);
+    Status st{false};
+    DocView d{buf + a, (int)(b - a)};
+    const uint8_t sp = special ? special[i] : 0;
+    const int passes = detect_doc(T, d, w.g, &out[i], st, !(sp & kSpecialHtml),
+                                  (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, &vo);
+    const bool bad = passes < 1 || passes > 3 || st.requeue || vo.over || vo.orig.over || vo.low.over;
+    n_chunks[i] = bad ? -1 : vo.n;
+    if (!bad) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
+    else atomicAdd(&counters[kCtrError], 1u);
+  }
+}
+
+// Compaction of the per-document pool regions into document order.
+__global__ __launch_bounds__(256) void k_vec_gather(const cld_chunk* __restrict__ pool,
+                                                   const uint64_t* __restrict__ pool_off,
+                                                   const int32_t* __restrict__ n_chunks,
+                                                   const uint64_t* __restrict__ pos, int n,
+                                                   cld_chunk* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int m = n_chunks[i];
+  for (int k = 0; k < m; ++k) dst[pos[i] + k] = pool[pool_off[i] + k];
+}
+
 // One wavefront per document of <= CAP bytes, WPB documents per workgroup.
 // One wave (document) per workgroup (WAVE_WPB, cld_kernels.h): a block's LDS
 // is released as soon as its own document is done, not when the slowest of
@@ -311,6 +371,25 @@ hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_
 }
 
 size_t cld_general_work_bytes() { return sizeof(cld::GeneralWork); }
+size_t cld_vec_work_bytes() { return sizeof(cld::VecWork); }
+
+hipError_t cld_launch_general_vec(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+                                  cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
+                                  const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
+                                  const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  dim3 grid(lanes / 64), block(64);
+  hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, *T, buf, offs, n, out, arena, stride, counters, special,
+                     priors, pool, pool_off, n_chunks);
+  return hipGetLastError();
+}
+
+hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
+                                 const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cld::k_vec_gather, dim3((n + 255) / 256), dim3(256), 0, s, pool, pool_off, n_chunks, pos, n, dst);
+  return hipGetLastError();
+}
 size_t cld_short_work_bytes() { return sizeof(cld::ShortWork); }
 size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 

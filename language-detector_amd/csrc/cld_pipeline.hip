@@ -182,8 +182,12 @@ __device__ int scan_to_letter_or_special(const DevTables& T, const DocView& d, i
 // `olen` is the reference's logical output capacity (kMaxScriptLowerBuffer);
 // the physical buffer only needs 1.5x the input (max per-char expansion of
 // this table, verified by tests/test_tables.py) plus padding.
+struct DevMap;
+__device__ void dm_copy(DevMap& m, int b);
+__device__ void dm_insert(DevMap& m, int b);
+__device__ void dm_delete(DevMap& m, int b);
 __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
-                                bool plain = true) {
+                                bool plain = true, DevMap* om = nullptr) {
   const int sh = (int)sm.shift;
   const int nEntries = 1 << sh;
   int total_filled = 0;
@@ -193,6 +197,7 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
   int outlen = olen;
   for (;;) {
     const uint8_t* src = in;
+    const uint8_t* copystart = in;            // the map2uplow_ bookkeeping (ResultChunkVector mode)
     const uint8_t* srclimit = in + inlen;
     uint8_t* dst = out;
     uint8_t* dstlimit = out + outlen;
@@ -219,12 +224,18 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
         bool again = true;
         switch (e) {
           case kExitReplace31:
-            dst -= 2; dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
+            dst -= 2;
+            if (om) { dm_copy(*om, (int)(src - copystart) - 2); dm_delete(*om, 2); copystart = src; }
+            dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace32:
-            dst -= 1; dst[-2] = (uint8_t)sm8(sm, tb + c + nEntries * 2);
+            dst -= 1;
+            if (om) { dm_copy(*om, (int)(src - copystart) - 1); dm_delete(*om, 1); copystart = src; }
+            dst[-2] = (uint8_t)sm8(sm, tb + c + nEntries * 2);
             dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace21:
-            dst -= 1; dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
+            dst -= 1;
+            if (om) { dm_copy(*om, (int)(src - copystart) - 1); dm_delete(*om, 1); copystart = src; }
+            dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace3:
             dst[-3] = (uint8_t)sm8(sm, tb + c + nEntries * 3);
             dst[-2] = (uint8_t)sm8(sm, tb + c + nEntries * 2);
@@ -258,6 +269,14 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
             for (int k = 0; k < add_len; ++k)
               dst[k] = ((uint32_t)(soff + k) < sm.n_rstr) ? sm.rstr[soff + k] : 0;
             dst += add_len;
+            if (om) {
+              if (add_len > del_len) {
+                dm_copy(*om, (int)(src - copystart)); dm_insert(*om, add_len - del_len); copystart = src;
+              } else if (add_len < del_len) {
+                dm_copy(*om, (int)(src - copystart) + add_len - del_len); dm_delete(*om, del_len - add_len);
+                copystart = src;
+              }
+            }
             if (re[0] & 0x80) {
               int ne = ((uint32_t)(soff + add_len) < sm.n_rstr) ? sm.rstr[soff + add_len] : 0;
               tb = tb0 + ((int64_t)ne << sh);
@@ -282,6 +301,7 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
       } else {
         e = kExitOK;
       }
+      if (om && src > copystart) { dm_copy(*om, (int)(src - copystart)); copystart = src; }
     }
     int consumed = (int)(src - in), filled = (int)(dst - out);
     total_filled += filled;
@@ -292,8 +312,8 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
 }
 
 __device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
-                                             bool plain = true) {
-  return lower_replace_sm(T.lower, in0, ilen, out0, olen, plain);
+                                             bool plain = true, DevMap* om = nullptr) {
+  return lower_replace_sm(T.lower, in0, ilen, out0, olen, plain, om);
 }
 
 // ------------------------------------------------------------ lang/script
@@ -563,6 +583,105 @@ struct Span { uint8_t* text; int text_bytes; int ulscript; };
 // passes are needed: the document is re-queued for the general kernel.
 struct Status { bool requeue; };
 
+// ------------------------------------------------- ResultChunkVector mode
+// OffsetMap (offsetmap.cc:43-453): copy / insert / delete ranges from the
+// document (A) to the text built from it (A'), one byte per range in the
+// reference's coding (2-bit op, 6-bit length, prefix bytes for long ranges,
+// adjacent copies merged).  Built by the scanner (map2original_) and the
+// lowercaser (map2uplow_) only when a document asks for its chunk vector.
+enum { DM_PREFIX = 0, DM_COPY = 1, DM_INSERT = 2, DM_DELETE = 3 };
+struct DevMap {
+  uint8_t* d; int n, cap;
+  int pend_op, pend_len, max_a, max_ap;
+  bool over;                                  // capacity exceeded: the document reports an error
+};
+__device__ void dm_push(DevMap& m, int op, int len) {           // Emit :203-206
+  if (m.n >= m.cap) { m.over = true; return; }
+  m.d[m.n++] = (uint8_t)((op << 6) | (len & 0x3F));
+}
+__device__ void dm_clear(DevMap& m) { m.n = 0; m.pend_op = DM_COPY; m.pend_len = 0; m.max_a = 0; m.max_ap = 0; }
+__device__ void dm_flush(DevMap& m) {                           // Flush :158-187
+  if (m.pend_len == 0) return;
+  if (m.pend_op == DM_COPY && m.n > 0) {
+    const uint8_t c = m.d[m.n - 1];
+    if ((c >> 6) == DM_COPY && (c & 0x3F) + m.pend_len <= 0x3F) {
+      m.d[m.n - 1] = (uint8_t)(c + m.pend_len);
+      m.pend_len = 0;
+      return;
+    }
+  }
+  if (m.pend_len > 0x3F) {
+    bool nz = false;
+    for (int shift = 30; shift > 0; shift -= 6) {
+      const int prefix = (m.pend_len >> shift) & 0x3F;
+      if (prefix > 0 || nz) { dm_push(m, DM_PREFIX, prefix); nz = true; }
+    }
+  }
+  dm_push(m, m.pend_op, m.pend_len & 0x3F);
+  m.pend_len = 0;
+}
+__device__ void dm_copy(DevMap& m, int b) {                     // Copy :107-118
+  if (b == 0) return;
+  m.max_a += b; m.max_ap += b;
+  if (m.pend_op == DM_COPY) m.pend_len += b;
+  else { dm_flush(m); m.pend_op = DM_COPY; m.pend_len = b; }
+}
+__device__ void dm_insert(DevMap& m, int b) {                   // Insert :122-138
+  if (b == 0) return;
+  m.max_ap += b;
+  if (m.pend_op == DM_INSERT) m.pend_len += b;
+  else if (b == 1 && m.pend_op == DM_DELETE && m.pend_len == 1) m.pend_op = DM_COPY;
+  else { dm_flush(m); m.pend_op = DM_INSERT; m.pend_len = b; }
+}
+__device__ void dm_delete(DevMap& m, int b) {                   // Delete :141-156
+  if (b == 0) return;
+  m.max_a += b;
+  if (m.pend_op == DM_DELETE) m.pend_len += b;
+  else if (b == 1 && m.pend_op == DM_INSERT && m.pend_len == 1) m.pend_op = DM_COPY;
+  else { dm_flush(m); m.pend_op = DM_DELETE; m.pend_len = b; }
+}
+__device__ void dm_reset(DevMap& m) {                           // Reset -> MaybeFlushAll :190-200
+  if (0 < m.pend_len || m.n == 0) { dm_copy(m, 1); dm_flush(m); }
+}
+// MapBack :428-452: the range of non-zero A' width that holds ap (the
+// reference's window walk settles on the same one).
+__device__ int dm_map_back(DevMap& m, int ap) {
+  dm_reset(m);
+  if (ap < 0) return 0;
+  if (m.max_ap <= ap) return (ap - m.max_ap) + m.max_a;
+  int lo_a = 0, lo_ap = 0, i = 0;
+  while (i < m.n) {
+    int op = DM_PREFIX, len = 0;
+    while (i < m.n && op == DM_PREFIX) {
+      const uint8_t c = m.d[i++];
+      op = c >> 6;
+      len = (len << 6) + (c & 0x3F);
+    }
+    if (op == DM_PREFIX) break;
+    const int hi_a = lo_a + (op == DM_INSERT ? 0 : len), hi_ap = lo_ap + (op == DM_DELETE ? 0 : len);
+    if (ap < hi_ap) {
+      const int a = ap - (lo_ap - lo_a);
+      return a >= hi_a ? hi_a : a;
+    }
+    lo_a = hi_a; lo_ap = hi_ap;
+  }
+  return (ap - m.max_ap) + m.max_a;
+}
+
+// SetChunkSummary's fields (scoreonescriptspan.h:240-252) as the vector path keeps them
+struct ChunkSum { uint16_t offset, chunk_start, lang1, lang2, score1, bytes; uint8_t rd, rs; };
+constexpr int kVecLinear = 4 * (kMaxScoringHits + 8) + 8;
+
+// Per-document vector state (in the lane's arena) for k_general_vec.
+struct VecOut {
+  DevMap orig, low;                           // map2original_, map2uplow_
+  cld_chunk* v; int n, cap; bool over;        // the document's ResultChunkVector (its pool region)
+  const uint8_t* doc; int doc_len;            // the original document (SummaryBufferToVector backs up in it)
+  uint32_t lin_lp[kVecLinear];                // this round's linear[] langprobs and offsets
+  uint16_t lin_off[kVecLinear];
+  ChunkSum sb[kMaxSummaries + 1];             // the round's summary buffer + the dummy off the end
+};
+
 // ------------------------------------------------------------ HTML mode
 // IsSpecial (getonescriptspan.cc:470-477)
 __device__ __forceinline__ bool is_special(uint8_t c) { return c == '<' || c == '>' || c == '&'; }
@@ -805,9 +924,10 @@ __device__ int skip_to_front_of_span(const DevTables& T, const DocView& d, int s
 // `next`/`remaining` are next_byte_ - start_byte_ and byte_length_.
 template <class W>
 __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& next, int& remaining,
-                                    W& w, Span& span, Status& st, bool plain = true) {
+                                    W& w, Span& span, Status& st, bool plain = true, DevMap* mo = nullptr) {
   const int common = (int)T.common, inherited = (int)T.inherited;
   span.text = w.sbuf; span.text_bytes = 0; span.ulscript = 0;
+  if (mo) { dm_clear(*mo); dm_delete(*mo, next); }    // map2original_: MapBack(0) = span offset (:835-836)
   int put_soft_limit = kMaxScriptBytes - kWithinScriptTail;
   if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) put_soft_limit = remaining / 2;
   int spanscript, sc = 0, tlen = 0, plen = 0;
@@ -816,7 +936,11 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
   int take = 0, put = 1;
   int skip = skip_to_front_of_span(T, d, next, remaining, &spanscript, plain);
   next += skip; remaining -= skip;
-  if (remaining <= 0) return false;
+  if (mo) {
+    if (skip != 1) { dm_delete(*mo, skip); dm_insert(*mo, 1); }
+    else dm_copy(*mo, 1);
+  }
+  if (remaining <= 0) { if (mo) dm_reset(*mo); return false; }
   span.ulscript = spanscript;
   const int base = next, bl = remaining;
   while (take < bl) {
@@ -848,11 +972,17 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
       }
       if (need_break) break;
       take += tlen; put += plen;
+      if (mo) {
+        if (tlen == plen) dm_copy(*mo, tlen);
+        else if (tlen < plen) { dm_copy(*mo, tlen); dm_insert(*mo, plen - tlen); }
+        else { dm_copy(*mo, plen); dm_delete(*mo, tlen - plen); }
+      }
       if (put >= kMaxScriptBytes) break;
     }
     while (take < bl) {
       tlen = scan_to_letter_or_special(T, d, base + take, bl - take);
       take += tlen;
+      if (mo) dm_delete(*mo, tlen);
       if (take >= bl) break;
       const uint8_t c1 = d.at(base + take);
       if (!plain && is_special(c1)) {
@@ -873,9 +1003,11 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
       }
       if (sc != 0) break;
       take += tlen;
+      if (mo) dm_delete(*mo, tlen);
     }
     if (put + 1 > W::SB) { st.requeue = true; return false; }
     sb[put++] = ' ';
+    if (mo) dm_insert(*mo, 1);
     if (sc != spanscript && sc != inherited) break;
     if (put >= put_soft_limit) break;
   }
@@ -883,21 +1015,25 @@ __device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& n
   next += take; remaining -= take;
   if (put + 4 > W::SB) { st.requeue = true; return false; }
   sb[put] = ' '; sb[put + 1] = ' '; sb[put + 2] = ' '; sb[put + 3] = 0;
+  if (mo) { dm_insert(*mo, 4); dm_reset(*mo); }
   span.text_bytes = put;
   return true;
 }
 
 // ScriptScanner::LowerScriptSpan getonescriptspan.cc:1033-1054
 template <class W>
-__device__ void lower_script_span(const DevTables& T, W& w, Span& span, Status& st, bool plain = true) {
+__device__ void lower_script_span(const DevTables& T, W& w, Span& span, Status& st, bool plain = true,
+                                  DevMap* ml = nullptr) {
   int ilen = span.text_bytes + 3;
   // HTML mode may map a character to more bytes (the &amp;-style half of a
   // remap pair): then only the reference's own capacity bounds it
   if ((plain ? (ilen * 3) / 2 + 4 : kMaxScriptLowerBuffer) > W::LB) { st.requeue = true; return; }
-  int filled = lower_replace(T, span.text, ilen, w.lbuf, kMaxScriptLowerBuffer, plain);
+  if (ml) dm_clear(*ml);
+  int filled = lower_replace(T, span.text, ilen, w.lbuf, kMaxScriptLowerBuffer, plain, ml);
   w.lbuf[filled] = 0; w.lbuf[filled + 1] = 0; w.lbuf[filled + 2] = 0; w.lbuf[filled + 3] = 0;
   span.text = w.lbuf;
   span.text_bytes = filled - 3;
+  if (ml) dm_reset(*ml);
 }
 
 // ---------------------------------------------------------- squeezing
@@ -1013,6 +1149,78 @@ __device__ int cheap_squeeze_inplace(uint8_t* isrc, int src_len, int* tbl) {  //
         dst += len;
       }
     }
+    src += len;
+  }
+  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
+  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
+  return (int)(dst - isrc);
+}
+// ResultChunkVector mode keeps offsets: the Overwrite variants turn the
+// dropped text into '.' runs in place (:697-765, :869-939).
+__device__ int cheap_rep_words_inplace_overwrite(uint8_t* isrc, int src_len, int* hash, int* tbl) {
+  const uint8_t* src = isrc;
+  const uint8_t* lim = isrc + src_len;
+  uint8_t* dst = isrc;
+  int h = *hash;
+  uint8_t* word_dst = dst;
+  int good = 0, wlen = 0;
+  while (src < lim) {
+    int c = src[0];
+    *dst++ = (uint8_t)c;
+    if (c == ' ') {
+      if (good * 2 > wlen)
+        for (uint8_t* q = word_dst; q < dst - 1; ++q) *q = '.';
+      word_dst = dst; good = 0; wlen = 0;
+    }
+    int incr = 1;
+    if (c < 0xC0) {
+    } else if ((c & 0xE0) == 0xC0) { *dst++ = src[1]; c = (c << 8) | src[1]; incr = 2; }
+    else if ((c & 0xF0) == 0xE0) { *dst++ = src[1]; *dst++ = src[2]; c = (c << 16) | (src[1] << 8) | src[2]; incr = 3; }
+    else {
+      *dst++ = src[1]; *dst++ = src[2]; *dst++ = src[3];
+      c = (int)(((uint32_t)c << 24) | ((uint32_t)src[1] << 16) | ((uint32_t)src[2] << 8) | src[3]); incr = 4;
+    }
+    src += incr;
+    wlen += incr;
+    int p = tbl[h];
+    tbl[h] = c;
+    if (c == p) good += incr;
+    h = ((h << 4) ^ c) & 0xFFF;
+  }
+  *hash = h;
+  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
+  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
+  return (int)(dst - isrc);
+}
+__device__ int cheap_squeeze_inplace_overwrite(uint8_t* isrc, int src_len, int* tbl) {
+  uint8_t* src = isrc;
+  uint8_t* dst = src;
+  uint8_t* lim = src + src_len;
+  bool skipping = false;
+  int hash = 0;
+  for (int i = 0; i < kPredictionTableSize; ++i) tbl[i] = 0;
+  const int chunksize = 48, space_thresh = (48 * 25) / 100, predict_thresh = (48 * 40) / 100;
+  ++src; ++dst;                                      // always keep the leading space
+  while (src < lim) {
+    int remaining = (int)(lim - src);
+    int len = remaining < chunksize ? remaining : chunksize;
+    while ((src[len] & 0xC0) == 0x80) ++len;
+    int space_n = count_spaces4(src, len);
+    int predb_n = count_predicted_bytes(src, len, &hash, tbl);
+    if (space_n >= space_thresh || predb_n >= predict_thresh) {
+      if (!skipping) {
+        int n = backscan_to_space(dst, (int)(dst - isrc));
+        for (uint8_t* q = dst - n; q < dst; ++q) *q = '.';
+        skipping = true;
+      }
+      for (uint8_t* q = dst; q < dst + len; ++q) *q = '.';
+      dst[len - 1] = ' ';
+    } else if (skipping) {
+      int n = forwardscan_to_space(src, len);
+      for (uint8_t* q = dst; q < dst + n - 1; ++q) *q = '.';
+      skipping = false;
+    }
+    dst += len;
     src += len;
   }
   if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
@@ -1257,10 +1465,11 @@ struct Ctx {
   // ApplyHints result (compact_lang_det_impl.cc:1645-1684): langprior_boost
   // latn[4] othr[4], then langprior_whack latn[4] othr[4]; null for none
   const uint32_t* priors;
+  VecOut* vo;               // ResultChunkVector being built (k_general_vec), else null
 };
 
-// SetChunkSummary scoreonescriptspan.cc:60-96 + SummaryBufferToDocTote :305-315
-__device__ void finish_chunk(const DevTables& T, int ulscript, int lo, int hi, const Tote& t, DocTote& dt, bool to_doc) {
+// SetChunkSummary scoreonescriptspan.cc:60-96
+__device__ ChunkSum chunk_summary(const DevTables& T, int ulscript, int lo, int hi, int first_linear, const Tote& t) {
   int key3[3];
   t.top3(key3);
   int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
@@ -1272,17 +1481,163 @@ __device__ void finish_chunk(const DevTables& T, int ulscript, int lo, int hi, c
   if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
   int esub = lang1 * 4 + lscript4(T, ulscript);
   int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
-  uint16_t bytes = (uint16_t)len;
+  ChunkSum cs;
+  cs.offset = (uint16_t)lo;
+  cs.chunk_start = (uint16_t)first_linear;
+  cs.lang1 = (uint16_t)lang1;
+  cs.lang2 = (uint16_t)lang2;
+  cs.score1 = (uint16_t)sc1;
+  cs.bytes = (uint16_t)len;
   uint16_t grams = (uint16_t)t.score_count;
-  uint16_t s1 = (uint16_t)sc1, s2 = (uint16_t)sc2;
-  int rd = (uint8_t)reliability_delta(s1, s2, grams);
+  int rd = (uint8_t)reliability_delta((uint16_t)sc1, (uint16_t)sc2, grams);
   int c1 = close_set(T, lang1);
   if (c1 != 0 && c1 == close_set(T, lang2)) rd = 100;
-  int rs = (uint8_t)reliability_expected(actual, expected);
-  if (to_doc) {
-    int rel = rd < rs ? rd : rs;
-    dt.add((uint16_t)lang1, bytes, s1, rel);
+  cs.rd = (uint8_t)rd;
+  cs.rs = (uint8_t)reliability_expected(actual, expected);
+  return cs;
+}
+// SummaryBufferToDocTote :305-315, one entry
+__device__ __forceinline__ void chunk_to_doc(const ChunkSum& cs, DocTote& dt) {
+  int rel = cs.rd < cs.rs ? cs.rd : cs.rs;
+  dt.add(cs.lang1, cs.bytes, cs.score1, rel);
+}
+
+// ---------------------------------------------- chunk vector (vec mode)
+__device__ __forceinline__ bool same_close_set(const DevTables& T, int l1, int l2) {   // :44-56
+  int c1 = close_set(T, l1);
+  return c1 != 0 && c1 == close_set(T, l2);
+}
+__device__ int get_lang_score(const DevTables& T, uint32_t lp, uint8_t pslang) {     // cldutil.cc:141-152
+  const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
+  int r = 0;
+  if (((lp >> 8) & 0xFF) == pslang) r += e[5];
+  if (((lp >> 16) & 0xFF) == pslang) r += e[6];
+  if (((lp >> 24) & 0xFF) == pslang) r += e[7];
+  return r;
+}
+__device__ uint8_t per_script_number(const DevTables& T, int ulscript, int lang) {  // lang_script.cc:320-326
+  if (ulscript < 0 || (uint32_t)ulscript >= T.n_scripts) return 0;
+  if (T.rtype[ulscript] == RTypeNone) return 1;
+  if (lang < 0 || (uint32_t)lang >= T.l2p_size) return 0;
+  return T.l2p[lang];
+}
+// BetterBoundary scoreonescriptspan.cc:671-720
+__device__ int better_boundary(const DevTables& T, const VecOut& vo, uint8_t ps0, uint8_t ps1, int lin0, int lin1,
+                               int lin2) {
+  if (lin2 - lin0 <= 8) return lin1;
+  int running = 0, diff[8];
+  for (int i = lin0; i < lin0 + 8; ++i) {
+    uint32_t lp = vo.lin_lp[i];
+    diff[i & 7] = get_lang_score(T, lp, ps0) - get_lang_score(T, lp, ps1);
+    if (i < lin0 + 4) running += diff[i & 7]; else running -= diff[i & 7];
   }
+  int best_value = 0, best = lin1;
+  for (int i = lin0; i < lin2 - 8; ++i) {
+    if (best_value < running) {
+      bool plus = false, minus = false;
+      for (int kk = 0; kk < 8; ++kk) { plus |= diff[kk] > 0; minus |= diff[kk] < 0; }
+      if (plus && minus) { best_value = running; best = i + 4; }
+    }
+    uint32_t lp = vo.lin_lp[i + 8];
+    int nd = get_lang_score(T, lp, ps0) - get_lang_score(T, lp, ps1);
+    int md = diff[(i + 4) & 7], od = diff[i & 7];
+    diff[i & 7] = nd;
+    running += 2 * md - od - nd;
+  }
+  return best;
+}
+// SharpenBoundaries :764-829 over vo.sb[0..n] (sb[n] = the dummy off the end)
+__device__ void sharpen_boundaries(const DevTables& T, VecOut& vo, int ulscript, int n) {
+  int prior_linear = vo.sb[0].chunk_start;
+  uint16_t prior_lang = vo.sb[0].lang1;
+  for (int i = 1; i < n; ++i) {
+    ChunkSum& cs = vo.sb[i];
+    const uint16_t this_lang = cs.lang1;
+    if (this_lang == prior_lang) { prior_linear = cs.chunk_start; continue; }
+    const int this_linear = cs.chunk_start, next_linear = vo.sb[i + 1].chunk_start;
+    if (same_close_set(T, prior_lang, this_lang)) { prior_linear = this_linear; prior_lang = this_lang; continue; }
+    const uint8_t ps0 = per_script_number(T, ulscript, prior_lang), ps1 = per_script_number(T, ulscript, this_lang);
+    const int better = better_boundary(T, vo, ps0, ps1, prior_linear, this_linear, next_linear);
+    const int old_off = vo.lin_off[this_linear], new_off = vo.lin_off[better];
+    cs.chunk_start = (uint16_t)better;
+    cs.offset = (uint16_t)new_off;
+    cs.bytes = (uint16_t)(cs.bytes - (new_off - old_off));
+    vo.sb[i - 1].bytes = (uint16_t)(vo.sb[i - 1].bytes + (new_off - old_off));
+    prior_linear = better;
+    prior_lang = this_lang;
+  }
+}
+__device__ __forceinline__ int scanner_map_back(VecOut& vo, int t) {      // ScriptScanner::MapBack :1076-1078
+  return dm_map_back(vo.orig, dm_map_back(vo.low, t));
+}
+__device__ void item_to_vector(VecOut& vo, int new_lang, int mapped_offset, int mapped_len) {  // ItemToVector :322-355
+  if (vo.n > 0) {
+    cld_chunk& prior = vo.v[vo.n - 1];
+    if (new_lang == prior.lang1) { prior.bytes = (mapped_offset + mapped_len) - prior.offset; return; }
+  }
+  if (vo.n >= vo.cap) { vo.over = true; return; }
+  cld_chunk rc;
+  rc.offset = mapped_offset; rc.bytes = mapped_len; rc.lang1 = (uint16_t)new_lang; rc.pad = 0;
+  vo.v[vo.n++] = rc;
+}
+// SummaryBufferToVector :386-495
+__device__ void summary_buffer_to_vector(const DevTables& T, VecOut& vo, int n) {
+  const int unk = (int)T.unknown_lang;
+  for (int i = 0; i < n; ++i) {
+    const ChunkSum cs = vo.sb[i];
+    const int unmapped_offset = cs.offset, unmapped_len = cs.bytes;
+    int mapped_offset = scanner_map_back(vo, unmapped_offset);
+    if (mapped_offset > 0) {
+      const int prior_size = vo.n > 0 ? vo.v[vo.n - 1].bytes : 0;
+      int n_limit = prior_size - 3 < mapped_offset ? prior_size - 3 : mapped_offset;
+      if (n_limit > 12) n_limit = 12;
+      auto at = [&](int k) -> uint8_t {           // us[-k - 1] in the original document
+        const int q = mapped_offset - k - 1;
+        return (unsigned)q < (unsigned)vo.doc_len ? vo.doc[q] : 0;
+      };
+      int k = 0;
+      while (k < n_limit && at(k) >= 0x41) ++k;
+      if (k >= n_limit) k = 0;
+      if (k < n_limit) {
+        const uint8_t ch = at(k);
+        if (ch == '\'' || ch == '"' || ch == '#' || ch == '@') ++k;
+      }
+      if (k > 0) { vo.v[vo.n - 1].bytes -= k; mapped_offset -= k; }
+    }
+    const int mapped_len = scanner_map_back(vo, unmapped_offset + unmapped_len) - mapped_offset;
+    int new_lang = cs.lang1;
+    bool delta_bad = cs.rd < 75, score_bad = cs.rs < 75;       // kUnreliablePercentThreshold (:33)
+    const uint16_t prior_lang = vo.n > 0 ? vo.v[vo.n - 1].lang1 : (uint16_t)unk;
+    if (prior_lang == cs.lang1) delta_bad = false;
+    if (same_close_set(T, cs.lang1, prior_lang)) { new_lang = prior_lang; delta_bad = false; }
+    if (same_close_set(T, cs.lang1, cs.lang2) && prior_lang == cs.lang2) { new_lang = prior_lang; delta_bad = false; }
+    const uint16_t next_lang = (i + 1 >= n) ? (uint16_t)unk : vo.sb[i + 1].lang1;
+    if (delta_bad && prior_lang == cs.lang2 && next_lang == cs.lang2) { new_lang = prior_lang; delta_bad = false; }
+    if (delta_bad || score_bad) new_lang = unk;
+    item_to_vector(vo, new_lang, mapped_offset, mapped_len);
+  }
+}
+__device__ void just_one_item_to_vector(VecOut& vo, int lang1, int unmapped_offset, int unmapped_len) {  // :499-530
+  const int mapped_offset = scanner_map_back(vo, unmapped_offset);
+  const int mapped_len = scanner_map_back(vo, unmapped_offset + unmapped_len) - mapped_offset;
+  item_to_vector(vo, lang1, mapped_offset, mapped_len);
+}
+// MoveLang1ToLang2's vector half (compact_lang_det_impl.cc:1122-1147)
+__device__ void move_lang1_to_lang2_vec(const DevTables& T, VecOut& vo, int lang1, int lang2) {
+  int k = 0;
+  uint16_t prior_lang = (uint16_t)T.unknown_lang;
+  for (int i = 0; i < vo.n; ++i) {
+    cld_chunk rc = vo.v[i];
+    if (rc.lang1 == lang1) rc.lang1 = (uint16_t)lang2;
+    if (rc.lang1 == prior_lang && k > 0) {
+      vo.v[k - 1].bytes += rc.bytes;
+    } else {
+      vo.v[k] = rc;
+      ++k;
+    }
+    prior_lang = rc.lang1;
+  }
+  vo.n = k;
 }
 
 // ProcessHitBuffer (:1067-1116) for one round: LinearizeAll + ChunkAll +
@@ -1304,6 +1659,9 @@ __device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb,
   bool have = lin.next(cur);               // the seed always exists
   int left = nb;
   int nchunks = 0;
+  VecOut* vo = cx.vo;
+  int li = 0;                              // linear[] subscript (chunk_start values)
+  int nsb = 0;
   // ChunkAll: with no base hits, one dummy chunk holding every entry
   bool single = (left <= 0);
   while (single || left > 0) {
@@ -1313,8 +1671,11 @@ __device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb,
     bool last = single || (left - blen <= 0);
     t.reinit();
     int lo = have ? cur.offset : dummy_off;
+    const int first_li = li;
     int cnt = 0;
     while (have && (last || cnt < blen)) {
+      if (vo) { vo->lin_lp[li] = cur.langprob; vo->lin_off[li] = (uint16_t)cur.offset; }
+      ++li;
       add_lang_prob(T, cur.langprob, t);
       if (cur.type <= QUADHIT) t.score_count++;
       if (cur.type == DISTINCTHIT) { db.lp[db.n] = cur.langprob; db.n = (db.n + 1) & (kMaxBoosts - 1); }
@@ -1331,10 +1692,26 @@ __device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb,
       for (int k = 0; k < kMaxBoosts; ++k)
         if (cx.priors[8 + so + k] > 0) t.score[(cx.priors[8 + so + k] >> 8) & 0xFF] = 0;
     int hi = have ? cur.offset : dummy_off;
-    finish_chunk(T, ulscript, lo, hi, t, dt, nchunks < kMaxSummaries);
+    if (nchunks < kMaxSummaries) {
+      const ChunkSum cs = chunk_summary(T, ulscript, lo, hi, first_li, t);
+      if (vo) vo->sb[nsb++] = cs;
+      else chunk_to_doc(cs, dt);
+    }
     ++nchunks;
     if (single) break;
     left -= blen;
+  }
+  if (vo) {
+    // ProcessHitBuffer with a vector (:1097-1115): dummy entry off the end
+    // (ScoreAllHits :289-297), SharpenBoundaries, then the doc tote and the vector
+    ChunkSum& dm = vo->sb[nsb];
+    dm = ChunkSum{};
+    dm.offset = (uint16_t)dummy_off;
+    dm.chunk_start = (uint16_t)li;
+    vo->lin_off[li] = (uint16_t)dummy_off;
+    sharpen_boundaries(T, *vo, cx.ulscript, nsb);
+    for (int i = 0; i < nsb; ++i) chunk_to_doc(vo->sb[i], dt);
+    summary_buffer_to_vector(T, *vo, nsb);
   }
 }
 
@@ -1346,6 +1723,7 @@ __device__ void score_one_script_span(const DevTables& T, Ctx& cx, W& w, const S
   if (rt == RTypeNone || rt == RTypeOne) {
     int bytes = span.text_bytes;
     dt.add((uint16_t)default_language(T, span.ulscript), bytes, bytes, 100);
+    if (cx.vo) just_one_item_to_vector(*cx.vo, default_language(T, span.ulscript), 1, bytes - 1);
     return;
   }
   const bool cjk = (rt == RTypeCJK);
@@ -1372,7 +1750,7 @@ __device__ void score_one_script_span(const DevTables& T, Ctx& cx, W& w, const S
 
 // ------------------------------------------------------ document level
 // RefineScoredClosePairs + MoveLang1ToLang2 compact_lang_det_impl.cc:1105-1203
-__device__ void refine_scored_close_pairs(const DevTables& T, DocTote& d) {
+__device__ void refine_scored_close_pairs(const DevTables& T, DocTote& d, VecOut* vo = nullptr) {
   for (int s = 0; s < 24; ++s) {
     int cs = close_set(T, d.key[s]);
     if (cs == 0) continue;
@@ -1380,8 +1758,10 @@ __device__ void refine_scored_close_pairs(const DevTables& T, DocTote& d) {
       if (close_set(T, d.key[s2]) == cs) {
         int from, to;
         if (d.value[s] < d.value[s2]) { from = s; to = s2; } else { from = s2; to = s; }
+        const int from_lang = d.key[from], to_lang = d.key[to];
         d.value[to] += d.value[from]; d.score[to] += d.score[from]; d.rel[to] += d.rel[from];
         d.key[from] = kUnusedKey; d.score[from] = 0; d.rel[from] = 0;
+        if (vo) move_lang1_to_lang2_vec(T, *vo, from_lang, to_lang);
         break;
       }
     }
@@ -1527,11 +1907,12 @@ __device__ void write_result(cld_result* r, const Extract& x, int summary, bool 
 // st.requeue set.
 template <class W>
 __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result* out, Status& st,
-                          bool plain = true, const uint32_t* priors = nullptr) {
+                          bool plain = true, const uint32_t* priors = nullptr, VecOut* vo = nullptr) {
   const int unk = (int)T.unknown_lang;
   int flags = 0;
   int passes = 0;
   Extract x;
+  if (vo) vo->n = 0;
   if (d.len == 0) {
     for (int i = 0; i < 3; ++i) { x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; x.rp3[i] = 0; }
     x.text_bytes = 0;
@@ -1546,6 +1927,8 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     cx.ulscript = 0;
     cx.latn.n = 0; cx.othr.n = 0;
     cx.priors = priors;
+    cx.vo = vo;
+    if (vo) vo->n = 0;                       // resultchunkvector->clear() (:1730-1732)
     for (int k = 0; k < kMaxBoosts; ++k) { cx.latn.lp[k] = 0; cx.othr.lp[k] = 0; }
     int next = 0, remaining = d.len;
     int hash = 0;
@@ -1555,11 +1938,13 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     int total = 0;
     bool restart = false;
     Span span;
-    while (get_one_script_span(T, d, next, remaining, w, span, st, plain)) {
-      lower_script_span(T, w, span, st, plain);
+    while (get_one_script_span(T, d, next, remaining, w, span, st, plain, vo ? &vo->orig : nullptr)) {
+      lower_script_span(T, w, span, st, plain, vo ? &vo->low : nullptr);
       if (st.requeue) return 0;
       if (flags & kCLDFlagSqueeze) {
-        if constexpr (W::MULTIPASS) span.text_bytes = cheap_squeeze_inplace(span.text, span.text_bytes, w.sqz);
+        if constexpr (W::MULTIPASS)
+          span.text_bytes = vo ? cheap_squeeze_inplace_overwrite(span.text, span.text_bytes, w.sqz)
+                               : cheap_squeeze_inplace(span.text, span.text_bytes, w.sqz);
       } else if (2048 < span.text_bytes && !(flags & kCLDFlagFinish)) {
         if constexpr (W::MULTIPASS) {
           if (cheap_squeeze_trigger_test(span.text, span.text_bytes, w.sqz)) {
@@ -1570,7 +1955,9 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
         }
       }
       if (flags & kCLDFlagRepeats) {
-        if constexpr (W::MULTIPASS) span.text_bytes = cheap_rep_words_inplace(span.text, span.text_bytes, &hash, w.predict);
+        if constexpr (W::MULTIPASS)
+          span.text_bytes = vo ? cheap_rep_words_inplace_overwrite(span.text, span.text_bytes, &hash, w.predict)
+                               : cheap_rep_words_inplace(span.text, span.text_bytes, &hash, w.predict);
       }
       cx.ulscript = span.ulscript;
       score_one_script_span(T, cx, w, span, dt, st);
@@ -1579,7 +1966,7 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     }
     if (st.requeue) return 0;
     if (restart) continue;
-    refine_scored_close_pairs(T, dt);
+    refine_scored_close_pairs(T, dt, vo);
     dt.sort3();
     extract_lang_etc(T, dt, total, x);
     bool good = (flags & kCLDFlagFinish) || total <= 256 ||
@@ -1591,6 +1978,12 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
       bool rel;
       int summary = calc_summary_lang(T, total, x, rel);
       write_result(out, x, summary, rel);
+      if (vo && vo->n > 0) {                 // FinishResultVector(0, buffer_length) (:1688-1702)
+        cld_chunk& a = vo->v[0];
+        if (a.offset > 0) { a.bytes += a.offset; a.offset = 0; }
+        cld_chunk& z = vo->v[vo->n - 1];
+        if (z.offset + z.bytes < d.len) z.bytes += d.len - (z.offset + z.bytes);
+      }
       return passes;
     }
     if constexpr (!W::MULTIPASS) { st.requeue = true; return 0; }

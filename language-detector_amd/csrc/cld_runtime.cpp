@@ -376,6 +376,20 @@ struct Device {
   hipStream_t up_stream = nullptr, down_stream = nullptr;
   uint32_t* h_ctr = nullptr;        // pinned: per-chunk counter snapshots (kCtrSlots each)
   size_t h_ctr_cap = 0;
+  // ResultChunkVector mode (cld_detect_batch_vec): its own lane arena, made on first use
+  struct Vec {
+    uint8_t* arena = nullptr; uint64_t stride = 0; int lanes = 0;
+    uint8_t* in = nullptr; size_t in_cap = 0;
+    uint64_t* offs = nullptr; size_t offs_cap = 0;
+    cld_result* out = nullptr; size_t out_cap = 0;
+    uint8_t* sp = nullptr; size_t sp_cap = 0;
+    uint32_t* pri = nullptr; size_t pri_cap = 0;
+    cld_chunk* pool = nullptr; size_t pool_cap = 0;
+    uint64_t* pool_off = nullptr; size_t pool_off_cap = 0;
+    int32_t* nch = nullptr; size_t nch_cap = 0;
+    uint64_t* pos = nullptr; size_t pos_cap = 0;
+    cld_chunk* compact = nullptr; size_t compact_cap = 0;
+  } vec;
   std::mutex mu;
 };
 
@@ -837,6 +851,85 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   return err ? CLD_EIO : CLD_OK;
 }
 
+// ResultChunkVector mode on one device: documents in sub-batches (the
+// kernel is the exact sequential pipeline; no overlap needed), each
+// document building its vector in a pool region of len + len/4 + 8 chunks,
+// then a gather into document order.  Appends the chunks of documents
+// [0, n) to *chunks and their counts to *counts.
+int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out,
+                  const uint8_t* special, const uint32_t* priors, std::vector<cld_chunk>* chunks,
+                  std::vector<int32_t>* counts) {
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_OK(hipSetDevice(d->id));
+  Device::Vec& V = d->vec;
+  if (!V.arena) {
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, d->id));
+    V.stride = (cld_vec_work_bytes() + 255) & ~(uint64_t)255;
+    int lanes = prop.multiProcessorCount * 32;
+    if (const char* e = getenv("CLD_VEC_LANES")) lanes = atoi(e);
+    lanes = std::max(64, (lanes / 64) * 64);
+    while ((uint64_t)lanes * V.stride > (8ull << 30) && lanes > 64) lanes -= 64;
+    if (hipMalloc(&V.arena, (uint64_t)lanes * V.stride) != hipSuccess) { V.arena = nullptr; return CLD_ENOMEM; }
+    V.lanes = lanes;
+  }
+  const size_t kSub = 256 * 1024;
+  const uint64_t kSubBytes = 32ull << 20;
+  size_t a = 0;
+  std::vector<uint64_t> pool_off, pos;
+  std::vector<int32_t> nch;
+  while (a < n) {
+    size_t m = 1;                                       // at least one document, then up to the limits
+    while (a + m < n && m < kSub && offs[a + m + 1] - offs[a] <= kSubBytes) ++m;
+    const uint64_t base = offs[a], bytes = offs[a + m] - base;
+    pool_off.assign(m + 1, 0);
+    for (size_t i = 0; i < m; ++i) {
+      const uint64_t len = offs[a + i + 1] - offs[a + i];
+      pool_off[i + 1] = pool_off[i] + len + len / 4 + 8;
+    }
+    if (grow(&V.in, &V.in_cap, std::max<size_t>(bytes, 1)) || grow(&V.offs, &V.offs_cap, m + 1) ||
+        grow(&V.out, &V.out_cap, m) || grow(&V.pool, &V.pool_cap, pool_off[m]) ||
+        grow(&V.pool_off, &V.pool_off_cap, m + 1) || grow(&V.nch, &V.nch_cap, m) || grow(&V.pos, &V.pos_cap, m))
+      return CLD_ENOMEM;
+    if (special && grow(&V.sp, &V.sp_cap, m)) return CLD_ENOMEM;
+    if (priors && grow(&V.pri, &V.pri_cap, 16 * m)) return CLD_ENOMEM;
+    hipStream_t s = d->stream;
+    HIP_OK(hipStreamWaitEvent(s, d->done, 0));
+    if (bytes) HIP_OK(hipMemcpyAsync(V.in, buf + base, bytes, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(V.offs, offs + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(V.pool_off, pool_off.data(), (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    if (special) HIP_OK(hipMemcpyAsync(V.sp, special + a, m, hipMemcpyHostToDevice, s));
+    if (priors) HIP_OK(hipMemcpyAsync(V.pri, priors + 16 * a, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
+    HIP_OK(cld_launch_general_vec(&d->T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
+                                  special ? V.sp : nullptr, priors ? V.pri : nullptr, V.pool, V.pool_off, V.nch, s));
+    nch.resize(m);
+    HIP_OK(hipMemcpyAsync(out + a, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    pos.assign(m, 0);
+    uint64_t total = 0;
+    bool err = false;
+    for (size_t i = 0; i < m; ++i) {
+      pos[i] = total;
+      if (nch[i] < 0) err = true;
+      else total += (uint64_t)nch[i];
+    }
+    if (err) { HIP_OK(hipEventRecord(d->done, s)); return CLD_EIO; }
+    if (grow(&V.compact, &V.compact_cap, std::max<uint64_t>(total, 1))) return CLD_ENOMEM;
+    HIP_OK(hipMemcpyAsync(V.pos, pos.data(), m * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIP_OK(cld_launch_vec_gather(V.pool, V.pool_off, V.nch, V.pos, (int)m, V.compact, s));
+    const size_t at = chunks->size();
+    chunks->resize(at + total);
+    if (total) HIP_OK(hipMemcpyAsync(chunks->data() + at, V.compact, total * sizeof(cld_chunk), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(d->done, s));
+    HIP_OK(hipStreamSynchronize(s));
+    counts->insert(counts->end(), nch.begin(), nch.end());
+    a += m;
+  }
+  return CLD_OK;
+}
+
 // ------------------------------------------------ detect_language batching
 // Host copy of the tables: the CLDT at `tables_path` (or the default), unless
 // a cld2 dynamic data file was loaded first (cld_load_data_*).  Caller holds g_init_mu.
@@ -1013,6 +1106,10 @@ void cld_shutdown(void) {
       (void)hipEventDestroy(h.up); (void)hipEventDestroy(h.comp); (void)hipEventDestroy(h.down);
     }
     (void)hipHostFree(d->h_ctr);
+    for (void* p : {(void*)d->vec.arena, (void*)d->vec.in, (void*)d->vec.offs, (void*)d->vec.out, (void*)d->vec.sp,
+                    (void*)d->vec.pri, (void*)d->vec.pool, (void*)d->vec.pool_off, (void*)d->vec.nch,
+                    (void*)d->vec.pos, (void*)d->vec.compact})
+      if (p) (void)hipFree(p);
     (void)hipEventDestroy(d->done);
     (void)hipStreamDestroy(d->up_stream);
     (void)hipStreamDestroy(d->down_stream);
@@ -1066,50 +1163,69 @@ int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld
   return n;
 }
 
-int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
-                        uint32_t flags, cld_result* out) {
-  if ((flags & ~CLD_FLAG_HTML) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
-  if (n == 0) return CLD_OK;
+}  // extern "C"
+
+namespace {
+// ApplyHints per document on the host (a few table lookups, and for HTML a
+// scan of the first 8 KB), split over host threads: the routing bits and,
+// when any document has a prior, the 16 langprobs per document.
+int apply_hints(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints, bool html,
+                std::vector<uint8_t>* special, std::vector<uint32_t>* priors) {
+  if (html && !g_tab.offs.ent_names) return CLD_EINVAL;     // tables without the HTML sections
+  if ((html || hints) && !g_tab.hints.ok()) return CLD_EINVAL;
+  special->assign(n, html ? kSpecialHtml : 0);
+  priors->clear();
+  if (!(html || hints)) return CLD_OK;
+  priors->assign(16 * n, 0);
+  std::atomic<bool> any(false);
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()),
+                                                           (n + 4095) / 4096));
+  auto work = [&](size_t lo, size_t hi) {
+    bool a = false;
+    for (size_t i = lo; i < hi; ++i) {
+      int16_t p[cld::kMaxPriors];
+      const int k = cld::hint_priors(g_tab.hints, buf + offsets[i], offsets[i + 1] - offsets[i], !html,
+                                     hints ? hints + i : nullptr, p);
+      if (k <= 0) continue;
+      uint32_t* o = priors->data() + 16 * i;
+      cld::hint_boosts(g_tab.hints, p, k, o);
+      bool nz = false;
+      for (int j = 0; j < 16; ++j) nz |= o[j] != 0;
+      if (nz) { (*special)[i] |= kSpecialPriors; a = true; }
+    }
+    if (a) any = true;
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+  work(0, n / nt);
+  for (auto& x : th) x.join();
+  if (!any) priors->clear();
+  return CLD_OK;
+}
+
+int check_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, const void* out) {
+  if (n > 0 && (!buf || !offsets || !out)) return CLD_EINVAL;
   if (n > 0x7FFFFFFFu) return CLD_EINVAL;
   for (size_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return CLD_EINVAL;
+  return CLD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
+                        uint32_t flags, cld_result* out) {
+  if ((flags & ~CLD_FLAG_HTML) != 0) return CLD_EINVAL;
+  if (int rc = check_batch(buf, offsets, n, out)) return rc;
+  if (n == 0) return CLD_OK;
   int rc = cld_init(nullptr, 0);
   if (rc) return rc;
-  const bool html = (flags & CLD_FLAG_HTML) != 0;
-  if (html && !g_tab.offs.ent_names) return CLD_EINVAL;     // tables without the HTML sections
-  if ((html || hints) && !g_tab.hints.ok()) return CLD_EINVAL;
-  // ApplyHints per document on the host (a few table lookups, and for HTML a
-  // scan of the first 8 KB), split over host threads
-  std::vector<uint8_t> special(n, html ? kSpecialHtml : 0);
+  std::vector<uint8_t> special;
   std::vector<uint32_t> priors;
-  if (html || hints) {
-    priors.assign(16 * n, 0);
-    std::atomic<bool> any(false);
-    const int nt = (int)std::max<size_t>(1, std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()),
-                                                             (n + 4095) / 4096));
-    auto work = [&](size_t lo, size_t hi) {
-      bool a = false;
-      for (size_t i = lo; i < hi; ++i) {
-        int16_t p[cld::kMaxPriors];
-        const int k = cld::hint_priors(g_tab.hints, buf + offsets[i], offsets[i + 1] - offsets[i], !html,
-                                       hints ? hints + i : nullptr, p);
-        if (k <= 0) continue;
-        uint32_t* o = priors.data() + 16 * i;
-        cld::hint_boosts(g_tab.hints, p, k, o);
-        bool nz = false;
-        for (int j = 0; j < 16; ++j) nz |= o[j] != 0;
-        if (nz) { special[i] |= kSpecialPriors; a = true; }
-      }
-      if (a) any = true;
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
-    work(0, n / nt);
-    for (auto& x : th) x.join();
-    if (!any) priors.clear();
-  }
-  bool any_special = html || !priors.empty();
-  const uint8_t* sp = any_special ? special.data() : nullptr;
+  const bool html = (flags & CLD_FLAG_HTML) != 0;
+  if ((rc = apply_hints(buf, offsets, n, hints, html, &special, &priors))) return rc;
+  const uint8_t* sp = (html || !priors.empty()) ? special.data() : nullptr;
   const uint32_t* pr = priors.empty() ? nullptr : priors.data();
   const size_t ndev = g_devs.size();
   std::vector<size_t> cut(ndev + 1, 0);
@@ -1127,6 +1243,49 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
   for (auto& t : th) t.join();
   for (int r : rcs) if (r) return r;
   return CLD_OK;
+}
+
+int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
+                         uint32_t flags, cld_result* out, cld_chunk* chunks, size_t chunk_cap,
+                         uint64_t* chunk_offsets) {
+  if ((flags & ~CLD_FLAG_HTML) != 0 || !chunk_offsets || (chunk_cap > 0 && !chunks)) return CLD_EINVAL;
+  if (int rc = check_batch(buf, offsets, n, out)) return rc;
+  chunk_offsets[0] = 0;
+  if (n == 0) return CLD_OK;
+  int rc = cld_init(nullptr, 0);
+  if (rc) return rc;
+  std::vector<uint8_t> special;
+  std::vector<uint32_t> priors;
+  const bool html = (flags & CLD_FLAG_HTML) != 0;
+  if ((rc = apply_hints(buf, offsets, n, hints, html, &special, &priors))) return rc;
+  const uint8_t* sp = (html || !priors.empty()) ? special.data() : nullptr;
+  const uint32_t* pr = priors.empty() ? nullptr : priors.data();
+  const size_t ndev = g_devs.size();
+  std::vector<size_t> cut(ndev + 1, 0);
+  cld_plan_shards(offsets, n, (int)ndev, cut.data());
+  std::vector<std::vector<cld_chunk>> vs(ndev);
+  std::vector<std::vector<int32_t>> cs(ndev);
+  std::vector<int> rcs(ndev, CLD_OK);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < ndev; ++k) {
+    if (cut[k + 1] == cut[k]) continue;
+    auto job = [&, k] {
+      rcs[k] = run_vec_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k],
+                             sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr, &vs[k], &cs[k]);
+    };
+    if (ndev == 1) job(); else th.emplace_back(job);
+  }
+  for (auto& t : th) t.join();
+  for (int r : rcs) if (r) return r;
+  size_t i = 0;
+  uint64_t total = 0;
+  for (size_t k = 0; k < ndev; ++k) {
+    for (int32_t c : cs[k]) { total += (uint64_t)c; chunk_offsets[++i] = total; }
+    const uint64_t at = total - vs[k].size();
+    if (at < chunk_cap)
+      memcpy(chunks + at, vs[k].data(), std::min<uint64_t>(vs[k].size(), chunk_cap - at) * sizeof(cld_chunk));
+  }
+  return total > chunk_cap ? CLD_ENOMEM : CLD_OK;
 }
 
 int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,

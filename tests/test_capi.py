@@ -33,3 +33,9 @@ def test_result_record_layout():
     assert cld_amd.RESULT_DTYPE.itemsize == 40
     assert [cld_amd.RESULT_DTYPE.fields[f][1] for f in ("lang3", "summary_lang", "percent3", "is_reliable",
                                                        "text_bytes", "normalized3")] == [0, 6, 8, 11, 12, 16]
+
+
+def test_chunk_record_layout():
+    """cld_chunk = ResultChunk (compact_lang_det.h:147-153): int offset, int32 bytes, uint16 lang1, uint16 pad."""
+    assert cld_amd.CHUNK_DTYPE.itemsize == 12
+    assert [cld_amd.CHUNK_DTYPE.fields[f][1] for f in ("offset", "bytes", "lang1", "pad")] == [0, 4, 8, 10]

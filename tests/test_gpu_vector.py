@@ -1,0 +1,96 @@
+"""cld_detect_batch_vec (ResultChunkVector) on the GPU vs the oracle, chunk for
+chunk, and vs the reference CLD2 itself when oracle/_ref/librefcld2.so is
+present (it travels with the tree; the oracle's vector is pinned to the
+reference by tests/test_reference_pin.py either way)."""
+import os
+
+import numpy as np
+import pytest
+
+import corpus
+from test_gpu_html_hints import random_hints
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def vecs(chunks, coffs):
+    return [[(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]]
+            for i in range(len(coffs) - 1)]
+
+
+def oracle_vecs(oracle, gpu, buf, offs, html=False, hints=None):
+    res, out = [], []
+    for i in range(len(offs) - 1):
+        doc = bytes(buf[offs[i]:offs[i + 1]])
+        pri = None
+        if html or hints is not None:
+            _, pri = gpu.hint_priors(doc, html=html, hints=hints[i] if hints is not None else None)
+        r, ch = oracle.detect_vec(doc, plain=not html, priors=pri)
+        res.append(r)
+        out.append([(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in ch])
+    return res, out
+
+
+def check(gpu, oracle, buf, offs, what, html=False, hints=None):
+    got, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs, html=html, hints=hints)
+    gv = vecs(chunks, coffs)
+    rr, ov = oracle_vecs(oracle, gpu, buf, offs, html, hints)
+    for i, (g, o) in enumerate(zip(gv, ov)):
+        assert g == o, "%s doc %d: gpu %s oracle %s" % (what, i, g[:6], o[:6])
+        r = rr[i]
+        assert (int(got[i]["summary_lang"]), list(got[i]["lang3"]), list(got[i]["percent3"]),
+                int(got[i]["text_bytes"]), list(got[i]["normalized3"])) == \
+            (r.summary_lang, list(r.lang3), list(r.percent3), r.text_bytes, list(r.normalized3)), (what, i)
+    return gv
+
+
+@pytest.mark.parametrize("cfg,n", [("c2", 3000), ("c3", 60), ("c4", 2000), ("c5", 2000)])
+def test_vector_corpora(gpu, oracle, cfg, n):
+    buf, offs = corpus.GENERATORS[cfg](n)
+    gv = check(gpu, oracle, buf, offs, cfg)
+    assert sum(len(v) for v in gv) >= n
+
+
+def test_vector_squeeze_html_hints(gpu, oracle):
+    buf, offs = corpus.c3(30, boiler_frac=0.5)
+    gv = check(gpu, oracle, buf, offs, "squeeze")
+    assert max(len(v) for v in gv) > 5
+    buf, offs = corpus.html(300, seed=12)
+    check(gpu, oracle, buf, offs, "html", html=True)
+    buf, offs = corpus.c2(1500, seed=13)
+    check(gpu, oracle, buf, offs, "hints", hints=random_hints(gpu, 1500, 14))
+    from test_gpu_parity import EDGE
+    b, o = gpu.pack(EDGE)
+    check(gpu, oracle, b, o, "edge")
+
+
+def test_vector_matches_reference_directly(gpu):
+    """GPU vs the reference's own ExtDetectLanguageSummary vector (the
+    prebuilt checker library), where it is available."""
+    import refcld
+    if not os.path.exists(refcld.LIB):
+        pytest.skip("oracle/_ref/librefcld2.so not built")
+    r = refcld.instance(os.environ["CLD_MI355X_TABLES"])
+    buf, offs = corpus.c5(1500, seed=15)
+    got, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs)
+    gv = vecs(chunks, coffs)
+    for i in range(len(offs) - 1):
+        doc = bytes(buf[offs[i]:offs[i + 1]])
+        rb, cb = r.detect_vec(doc)
+        assert gv[i] == [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in cb], i
+        assert int(got[i]["summary_lang"]) == int(rb["summary_lang"])
+
+
+def test_vector_capacity_contract(gpu):
+    buf, offs = corpus.c2(200, seed=16)
+    _, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs)
+    import ctypes
+    n = len(offs) - 1
+    out = np.zeros(n, dtype=gpu.RESULT_DTYPE)
+    co = np.zeros(n + 1, dtype=np.uint64)
+    small = np.zeros(3, dtype=gpu.CHUNK_DTYPE)
+    rc = gpu.lib().cld_detect_batch_vec(buf.ctypes.data, offs.ctypes.data, n, None, 0, out.ctypes.data,
+                                        small.ctypes.data, 3, co.ctypes.data)
+    assert rc == -12 and int(co[-1]) == len(chunks)       # CLD_ENOMEM with the needed size
+    assert np.array_equal(co, coffs)
