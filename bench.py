@@ -76,31 +76,44 @@ def host_cores():
 
 
 def cpu_baseline(cfg, buf, offs, gpu_out, seconds, sample_docs):
-    """The oracle (oracle/cld_oracle.c, the C restatement) on the host cores,
-    bounded sample.  Also checks the GPU results of that sample bit-for-bit
+    """The CPU path timed on the host cores over a bounded sample: the
+    reference CLD2 itself when its checker build travels with the tree
+    (oracle/_ref/librefcld2.so: the reference's own sources in its
+    dynamic-data mode, tables loaded from a data file written from the same
+    CLDT as the GPU's), else the oracle (oracle/cld_oracle.c, the C
+    restatement).  Also checks the GPU results of that sample bit-for-bit
     (checker role)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from oracle import Oracle
-    ob = Oracle()
     cores, nproc, model = host_cores()
     threads = int(os.environ.get("CLD_CPU_THREADS", cores))
     n = len(offs) - 1
     sample = min(n, sample_docs)
     o = offs[:sample + 1]
     b = buf[:int(o[-1])]
-    ref = ob.detect_batch(b, o, threads=threads)            # warm + parity sample
-    same = all(bool(np.array_equal(ref[f], gpu_out[f][:sample])) for f in FIELDS)
+    import refcld
+    if os.path.exists(refcld.LIB) and os.environ.get("CLD_CPU_BASELINE", "reference") == "reference":
+        eng = refcld.instance(os.environ["CLD_MI355X_TABLES"])
+        kind, what = "reference", "reference CLD2 (oracle/_ref/librefcld2.so, DetectLanguageSummaryV2)"
+        fields = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
+    else:
+        from oracle import Oracle
+        eng = Oracle()
+        kind, what = "port", "oracle/cld_oracle.c"
+        fields = FIELDS
+    ref = eng.detect_batch(b, o, threads=threads)            # warm + parity sample
+    same = all(bool(np.array_equal(ref[f].astype(np.float64), gpu_out[f][:sample].astype(np.float64)))
+               for f in fields)
     docs, t0 = 0, time.perf_counter()
     while True:
-        ob.detect_batch(b, o, threads=threads)
+        eng.detect_batch(b, o, threads=threads)
         docs += sample
         dt = time.perf_counter() - t0
         if dt >= seconds:
             break
-    return {"value": docs / dt, "unit": "docs/s", "cores": threads, "kind": "port",
+    return {"value": docs / dt, "unit": "docs/s", "cores": threads, "kind": kind,
             "input_GBps": docs / sample * float(o[-1]) / dt / 1e9,
-            "sample": "%d %s documents (%.1f MB), %d passes in %.1f s, oracle/cld_oracle.c x %d threads"
-                      % (sample, cfg, o[-1] / 1e6, docs // sample, dt, threads),
+            "sample": "%d %s documents (%.1f MB), %d passes in %.1f s, %s x %d threads"
+                      % (sample, cfg, o[-1] / 1e6, docs // sample, dt, what, threads),
             "host": {"nproc": nproc, "usable_cores": cores, "cpu_model": model},
             "gpu_bit_exact_on_sample": same}
 
