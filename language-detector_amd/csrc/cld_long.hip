@@ -67,6 +67,11 @@ constexpr int kListCap = kLB / 2;                    // words / spaces / chain e
 constexpr int kHB = 1024;                            // hits per round (reference: <= 1000)
 constexpr int kEB = 2048;                            // base emissions per round (<= 2 per hit)
 constexpr int kMaxCh = 64;                           // chunks per round (<= 50 + 1)
+// Span cache: pass 1 builds every lowered span into lbd (16-byte aligned, each
+// followed by its pads), so pass 2 (Repeats) reads them back instead of
+// re-running the span builder over the per-byte classes.
+constexpr int kLbdCap = 160 * 1024;
+constexpr int kMaxSpans = 1024;
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 // A lowered span of up to kLdsText - 48 bytes (pads included) is scored from
 // LDS: the chain walk, the gram hashes and the word scans then read the text
@@ -91,6 +96,10 @@ struct Slot {
   uint64_t aux[2][kSpanWords];           // Squeeze: predicted starts of 2/4-byte, 3/4-byte characters
   uint64_t chm[kSpanWords];              // Squeeze: chunk starts
   alignas(16) uint8_t lb[2][kLB];        // lowered span text; [1] = after CheapRepWords
+  alignas(16) uint8_t lbd[kLbdCap];      // pass 1's lowered spans, back to back (span cache)
+  int32_t sp_off[kMaxSpans];             //   their offsets in lbd, text_bytes and scripts
+  int32_t sp_tb[kMaxSpans];
+  int32_t sp_ul[kMaxSpans];
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
   uint16_t chain[kListCap];              // quad chain of the span
@@ -1636,27 +1645,48 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
   // Squeeze|Repeats|Finish.  The Repeats predictor is document-wide (pred),
   // the Squeeze one is fresh per span (pred2).
   bool sq = false;
+  int nsp = 0, cur = 0;                          // span cache (pass 1): spans recorded, bytes used
+  bool cache_ok = true;
   for (int pass = 1; pass <= 3; ++pass) {
     const bool rep = pass == 3 || (pass == 2 && !sq);    // Repeats always comes with Finish
+    const bool from_cache = pass == 2 && rep && cache_ok;
     if (lane == 0) s.dt.init();
     if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
     uint32_t hcarry = 0, ep = 0;
     if (rep) ep = new_epoch(S.epoch, S.pred, lane);
     wsync();
-    int next = 0, total = 0;
+    int next = 0, total = 0, ci = 0;
     bool restart = false;
     for (;;) {
-      int ul = 0, st = 0;
+      int ul = 0, st = 0, tb;
+      uint8_t* lb = S.lb[0];
       if constexpr (D) trace(tr, lane, doc, 3, next);
-      int tb = stored ? next_span<true>(T, dv, S, S.lb[0], next, ul, st, lane)
-                      : next_span<false>(T, dv, S, S.lb[0], next, ul, st, lane);
+      if (from_cache) {
+        if (ci >= nsp) break;
+        tb = ufl(S.sp_tb[ci]);
+        ul = ufl(S.sp_ul[ci]);
+        lb = S.lbd + ufl(S.sp_off[ci]);
+        ++ci;
+      } else {
+        const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
+        if (pass == 1 && !rec) cache_ok = false;
+        if (rec) lb = S.lbd + cur;
+        tb = stored ? next_span<true>(T, dv, S, lb, next, ul, st, lane)
+                    : next_span<false>(T, dv, S, lb, next, ul, st, lane);
+        if (st == 0) break;
+        if (st < 0) return -kWhySpan;
+        if (rec) {
+          if (lane == 0) { S.sp_off[nsp] = cur; S.sp_tb[nsp] = tb; S.sp_ul[nsp] = ul; }
+          ++nsp;
+          cur += (tb + 64 + 15) & ~15;           // text, its pads and the hash read slack
+        }
+      }
       if constexpr (D) trace(tr, lane, doc, 4, tb);
       if constexpr (D) mark(s, lane, 1, t);
-      if (st == 0) break;
-      if (st < 0) return -kWhySpan;
       if (pass == 1) {
-        if (tb > 2048 && squeeze_trigger(S, S.lb[0], careful, lane)) {   // recursion with Squeeze (:1867-1900)
+        if (tb > 2048 && squeeze_trigger(S, lb, careful, lane)) {   // recursion with Squeeze (:1867-1900)
           restart = true;
+          cache_ok = false;
           break;
         }
         if constexpr (D) mark(s, lane, 2, t);
@@ -1666,7 +1696,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         // the span (and its pads) fits in LDS: 16 bytes per lane per step
         const int n16 = (tb + 48 + 15) >> 4;
         for (int i = lane; i < n16; i += 64)
-          reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(S.lb[0])[i];
+          reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(lb)[i];
         wsync();
         if (sq) tb = squeeze_span(S, s.text, tb, careful, lane);             // in place, as the reference does
         if (rep) {
@@ -1682,11 +1712,11 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         }
         ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc);
       } else {
-        const uint8_t* text = S.lb[0];
-        if (sq) tb = squeeze_span(S, S.lb[0], tb, careful, lane);
+        const uint8_t* text = lb;
+        if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
         if (rep) {
           bool okr;
-          tb = rep_words(S, S.lb[0], S.lb[1], tb, hcarry, ep, careful, okr, lane);
+          tb = rep_words(S, lb, S.lb[1], tb, hcarry, ep, careful, okr, lane);
           if (!okr) return -kWhySpan;
           text = S.lb[1];
           if constexpr (D) mark(s, lane, 3, t);
