@@ -35,6 +35,7 @@ struct DevTables {
   const uint16_t* deflang;
   const uint16_t* closest;
   const uint64_t* cpt;        // per-character properties of 1-3 byte sequences (cld_long.hip, built on device)
+  const uint64_t* keytab;     // per (script, key): language, close set, expected score (k_long, built on device)
   const uint8_t* close_set;
   const uint8_t* ent_names;   // HTML mode: entity name string section (CLDT_ENTITY_NAMES), or null
   const int32_t* ent_values;  //   and their code points

@@ -64,6 +64,8 @@ hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, con
 size_t cld_long_slot_bytes();
 size_t cld_cpt_entries();
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);
+size_t cld_keytab_entries();
+hipError_t cld_build_keytab(const DevTables* T, uint64_t* out, hipStream_t s);
 int cld_long_waves_per_simd();
 size_t cld_strip_scratch_bytes(int n);
 hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,

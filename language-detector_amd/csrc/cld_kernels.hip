@@ -226,7 +226,6 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
   if (total == 0) return;                       // empty re-queue list: no dequeue atomics at all
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
-  if (lane == 0) smem[wv].kscript = -1;
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
   for (;;) {
     // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
@@ -308,6 +307,13 @@ __global__ __launch_bounds__(256) void k_len_scatter(const uint32_t* __restrict_
   }
 }
 
+// Per (script, key) language / close set / expected score table for k_long.
+__global__ __launch_bounds__(256) void k_build_keytab(DevTables T, uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 256 * 256) return;
+  out[i] = lng::keytab_eval(T, i >> 8, i & 255);
+}
+
 // Character property table (lng::cpt_eval over every 1-3 byte sequence).
 __global__ __launch_bounds__(256) void k_build_cpt(DevTables T, uint64_t* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -338,6 +344,11 @@ extern "C" {
 size_t cld_cpt_entries() { return cld::lng::kCptSize; }
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(cld::k_build_cpt, dim3((cld::lng::kCptSize + 255) / 256), dim3(256), 0, s, *T, out);
+  return hipGetLastError();
+}
+size_t cld_keytab_entries() { return 256 * 256; }
+hipError_t cld_build_keytab(const DevTables* T, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(cld::k_build_keytab, dim3(256), dim3(256), 0, s, *T, out);
   return hipGetLastError();
 }
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,

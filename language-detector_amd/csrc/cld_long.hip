@@ -125,9 +125,6 @@ struct alignas(16) Smem {
   uint16_t bst[kMaxCh + 1];
   uint16_t st[2][kMaxCh + 1];            // first delta [0] / distinct [1] emission of chunk k
   uint64_t ring[2][4];                   // distinct boosts (as tote adds), latn / othr, oldest first
-  uint32_t kl[256];                      // per key of the span script: language | close set << 16
-  int16_t ke[256];                       //   and expected score (kAvgDeltaOctaScore) of that language
-  int kscript;                           // script the key table holds (-1: none)
   DocTote dt;
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
   uint32_t dbg_pos;
@@ -1247,20 +1244,16 @@ __device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
          ((uint64_t)((e >> 16) & 0xFF) << 24) | ((uint64_t)(lp >> 24) << 32) | ((uint64_t)(e >> 24) << 40);
 }
 
-// Per-key language, close set and expected score for a span script
+// Per (script, key): language | close set << 16 | expected score << 32
 // (FromPerScriptNumber, close sets, kAvgDeltaOctaScore: lang_script.cc:328-341,
-// 261-310; scoreonescriptspan.cc:75-80), so a chunk summary reads only LDS.
-__device__ void key_table(const DevTables& T, Smem& s, int ulscript, int lane) {
-  if (s.kscript == ulscript) return;
-  const int ls4 = lscript4(T, ulscript);
-  for (int k = lane; k < 256; k += 64) {
-    const int lang = from_per_script_number(T, ulscript, (uint8_t)k);
-    const int esub = lang * 4 + ls4;
-    s.kl[k] = (uint32_t)(uint16_t)lang | ((uint32_t)close_set(T, lang) << 16);
-    s.ke[k] = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : (int16_t)0;
-  }
-  if (lane == 0) s.kscript = ulscript;
-  wsync();
+// 261-310; scoreonescriptspan.cc:75-80), one table per GPU built by
+// k_build_keytab, L2-resident and shared by every wave (it used to be a
+// per-wave LDS copy; the LDS now goes to occupancy).
+__device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
+  const int lang = from_per_script_number(T, ulscript, (uint8_t)k);
+  const int esub = lang * 4 + lscript4(T, ulscript);
+  const int16_t ex = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : (int16_t)0;
+  return (uint64_t)(uint16_t)lang | ((uint64_t)close_set(T, lang) << 16) | ((uint64_t)(uint16_t)ex << 32);
 }
 
 // ------------------------------------- linearize + chunk + score (one round)
@@ -1493,16 +1486,17 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     lo = lo_k == kInf ? dummy_off : (int)lo_k;
     hi = dummy_off;
     if (lane + 1 < K && s.lo[lane + 1] != kInf) hi = (int)s.lo[lane + 1];
-    const uint32_t i1 = s.kl[(uint8_t)ck1], i2 = s.kl[(uint8_t)ck2];
+    const uint64_t* kt = T.keytab + 256 * (uint32_t)ulscript;
+    const uint64_t i1 = kt[(uint8_t)ck1], i2 = kt[(uint8_t)ck2];
     lang1 = (int)(i1 & 0xFFFF); lang2 = (int)(i2 & 0xFFFF);
     const int len = hi - lo;
     int actual = 0;
     if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
-    const int expected = s.ke[(uint8_t)ck1];
+    const int expected = (int16_t)(uint16_t)(i1 >> 32);
     const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2, grams = (uint16_t)cgr;
     rd = (uint8_t)reliability_delta(s1, s2, grams);
-    const int c1 = (int)(i1 >> 16);
-    if (c1 != 0 && c1 == (int)(i2 >> 16)) rd = 100;
+    const int c1 = (int)((i1 >> 16) & 0xFFFF);
+    if (c1 != 0 && c1 == (int)((i2 >> 16) & 0xFFFF)) rd = 100;
     rsc = (uint8_t)reliability_expected(actual, expected);
     cs1 = s1; cs2 = s2; cgr = grams;
   }
@@ -1569,7 +1563,6 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
     return true;
   }
   if (tb <= 1) return true;
-  key_table(T, s, ulscript, lane);
   int off = 1;
   long long t = (D && s.prof) ? (long long)clock64() : 0;
   if (rt == RTypeCJK) {

@@ -434,6 +434,7 @@ int grow(T** p, size_t* cap, size_t need) {
 struct StagedTables {
   uint8_t* blob = nullptr;
   uint64_t* cpt = nullptr;
+  uint64_t* keytab = nullptr;
   DevTables T{};
 };
 
@@ -445,8 +446,11 @@ int stage_tables(Device* d, const HostTables& t, StagedTables* st) {
   // per-character property table for the long-document kernel, built from the uploaded machines
   HIP_OK(hipMalloc(&st->cpt, cld_cpt_entries() * sizeof(uint64_t)));
   HIP_OK(cld_build_cpt(&st->T, st->cpt, d->stream));
+  HIP_OK(hipMalloc(&st->keytab, cld_keytab_entries() * sizeof(uint64_t)));
+  HIP_OK(cld_build_keytab(&st->T, st->keytab, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   st->T.cpt = st->cpt;
+  st->T.keytab = st->keytab;
   return CLD_OK;
 }
 
@@ -454,6 +458,7 @@ void discard_tables(Device* d, StagedTables* st) {
   (void)hipSetDevice(d->id);
   if (st->blob) (void)hipFree(st->blob);
   if (st->cpt) (void)hipFree(st->cpt);
+  if (st->keytab) (void)hipFree(st->keytab);
   *st = StagedTables();
 }
 
@@ -463,6 +468,7 @@ int commit_tables(Device* d, StagedTables* st) {
   HIP_OK(hipDeviceSynchronize());   // batches enqueued on caller streams may still read the old blob
   if (d->d_blob) (void)hipFree(d->d_blob);
   if (d->T.cpt) (void)hipFree((void*)d->T.cpt);
+  if (d->T.keytab) (void)hipFree((void*)d->T.keytab);
   d->d_blob = st->blob;
   d->T = st->T;
   *st = StagedTables();
@@ -1095,7 +1101,7 @@ void cld_shutdown(void) {
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
-    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
+    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
