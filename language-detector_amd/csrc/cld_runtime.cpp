@@ -683,11 +683,19 @@ void watch_trace(Device* d, hipStream_t s) {
   }
 }
 
-// Chunking of the streamed host path: a chunk is at most kChunkBytes of
-// document text and kChunkDocs documents, so two chunks in flight stay small
-// next to HBM while each is still a full-chip launch.
-constexpr uint64_t kChunkBytes = 64ull << 20;
-constexpr size_t kChunkDocs = 512 * 1024;
+// Chunking of the streamed host path: a chunk is at most 32 MB of document
+// text and 8K documents per MB, so two chunks in flight stay small next to HBM
+// while each is still a full-chip launch (C2 host path, pinned buffers: 16 MB
+// chunks 69%, 32 MB 74%, 64 MB 72% of kernel-only docs/s; gpurun_out/r2r).
+// CLD_CHUNK_MB overrides the byte limit.
+uint64_t chunk_bytes() {
+  static const uint64_t v = [] {
+    uint64_t mb = 32;
+    if (const char* e = getenv("CLD_CHUNK_MB")) mb = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    return mb << 20;
+  }();
+  return v;
+}
 
 bool host_pinned(const void* p) {
   hipPointerAttribute_t a;
@@ -743,6 +751,8 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   std::vector<size_t> cut{0};
   while (cut.back() < n) {
     const size_t a = cut.back();
+    const uint64_t kChunkBytes = chunk_bytes();
+    const size_t kChunkDocs = (size_t)(kChunkBytes >> 7);    // 8K documents per MB
     size_t lo = a + 1, hi = std::min(n, a + kChunkDocs);     // largest b <= hi with bytes <= kChunkBytes (>= 1 doc)
     while (lo < hi) {
       const size_t mid = (lo + hi + 1) / 2;
