@@ -23,7 +23,7 @@ for p in "${PASSES[@]}"; do
   i=$((i+1))
   echo "[$(date +%T)] pass $i: $p" | tee -a "$O/session.log"
   timeout -s KILL 120 rocprofv3 --pmc $p --kernel-include-regex "$KRE" -d "$O/pmc$i" -o $CFG --output-format csv -- \
-      python3 "$R/bench.py" --config $CFG --steps 2 --warmup 1 --no-cpu-baseline $EXTRA > "$O/pmc$i.log" 2>&1
+      python3 "$R/bench.py" --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-sub --no-host $EXTRA > "$O/pmc$i.log" 2>&1
   rc=$?
   echo "[$(date +%T)] rc=$rc" | tee -a "$O/session.log"
   if [ $rc -ne 0 ]; then tail -30 "$O/pmc$i.log"; exit $rc; fi
