@@ -38,7 +38,7 @@ size_t cld_vec_work_bytes();
 // ResultChunkVector mode: all n documents in k_general_vec; document i builds
 // its vector in pool[pool_off[i] .. pool_off[i+1]) and writes its size (or -1)
 // to n_chunks[i]; counters[kCtrDequeue2] must be zero.
-hipError_t cld_launch_general_vec(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
                                   const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s);
@@ -55,7 +55,7 @@ size_t cld_wave_smem_bytes();
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                             const uint8_t* special, uint32_t* special_list, int special_ctr, hipStream_t s);
-hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
+hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               const uint8_t* special, const uint32_t* priors, hipStream_t s);
@@ -72,7 +72,10 @@ hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, in
                                     uint64_t* out_offs, void* scratch, hipStream_t s);
 hipError_t cld_launch_strip_write(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,
                                   const uint64_t* out_offs, uint8_t* out, hipStream_t s);
-hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+// d_T: the device's DevTables copy in HBM (k_long reads the table set through
+// it: holding the by-value kernel argument in registers made the kernel spill
+// it to scratch and reload table fields from there at every probe)
+hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, hipStream_t s);

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __res
   }
 }
 
-__global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
                                                const uint64_t* __restrict__ offs,
                                                const uint32_t* __restrict__ list,
                                                cld_result* __restrict__ out,
@@ -59,6 +59,7 @@ __global__ __launch_bounds__(64) void k_general(DevTables T, const uint8_t* __re
                                                uint32_t* __restrict__ counters, int ctr_count, int ctr_deq,
                                                const uint8_t* __restrict__ special,
                                                const uint32_t* __restrict__ priors) {
+  const DevTables& T = *Tp;
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
   const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -97,7 +98,7 @@ struct VecWork {
   uint8_t map_l[kMapLowCap];
 };
 
-__global__ __launch_bounds__(64) void k_general_vec(DevTables T, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
                                                    const uint64_t* __restrict__ offs, int n,
                                                    cld_result* __restrict__ out,
                                                    uint8_t* __restrict__ arena, uint64_t stride,
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(64) void k_general_vec(DevTables T, const uint8_t* 
                                                    const uint32_t* __restrict__ priors,
                                                    cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
                                                    int32_t* __restrict__ n_chunks) {
+  const DevTables& T = *Tp;
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   VecWork& w = *reinterpret_cast<VecWork*>(arena + (uint64_t)lane * stride);
   for (;;) {
@@ -207,7 +209,8 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
 #define LNG_WPS 4
 #endif
 template <int WPB, bool DIAG>
-__global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __restrict__ Tp,
+                                                  const uint8_t* __restrict__ buf,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ list,
                                                   cld_result* __restrict__ out, uint8_t* __restrict__ slots,
@@ -216,6 +219,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(DevTables T, const u
                                                   uint32_t* dbg, uint32_t dbg_doc,
                                                   unsigned long long* prof) {
   __shared__ lng::Smem smem[WPB];
+  const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
   // address) is then scalar instead of a VGPR pair per field
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -364,7 +368,7 @@ hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, con
 size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }
 int cld_long_waves_per_simd() { return LNG_WPS; }
 
-hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, hipStream_t s) {
@@ -373,10 +377,10 @@ hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
-    hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, *T, buf, offs, list, out, slots,
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof);
   else
-    hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, *T, buf, offs, list, out, slots,
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof);
   return hipGetLastError();
 }
@@ -384,13 +388,13 @@ hipError_t cld_launch_long(const DevTables* T, const uint8_t* buf, const uint64_
 size_t cld_general_work_bytes() { return sizeof(cld::GeneralWork); }
 size_t cld_vec_work_bytes() { return sizeof(cld::VecWork); }
 
-hipError_t cld_launch_general_vec(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
+hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
                                   const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   dim3 grid(lanes / 64), block(64);
-  hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, *T, buf, offs, n, out, arena, stride, counters, special,
+  hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
                      priors, pool, pool_off, n_chunks);
   return hipGetLastError();
 }
@@ -426,12 +430,12 @@ hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64
   return hipGetLastError();
 }
 
-hipError_t cld_launch_general(const DevTables* T, const uint8_t* buf, const uint64_t* offs,
+hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               const uint8_t* special, const uint32_t* priors, hipStream_t s) {
   dim3 grid(lanes / 64), block(64);
-  hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, *T, buf, offs, list, out, arena, stride,
+  hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, d_T, buf, offs, list, out, arena, stride,
                      counters, ctr_count, ctr_deq, special, priors);
   return hipGetLastError();
 }

@@ -318,6 +318,7 @@ struct Device {
   hipStream_t stream = nullptr;
   uint8_t* d_blob = nullptr;
   DevTables T{};
+  DevTables* d_T = nullptr;   // T in HBM (k_long reads the table set through a pointer)
   uint8_t* d_arena = nullptr;
   uint64_t stride = 0;
   int lanes = 0;
@@ -472,6 +473,8 @@ int commit_tables(Device* d, StagedTables* st) {
   d->d_blob = st->blob;
   d->T = st->T;
   *st = StagedTables();
+  if (!d->d_T) HIP_OK(hipMalloc(&d->d_T, sizeof(DevTables)));
+  HIP_OK(hipMemcpy(d->d_T, &d->T, sizeof(DevTables), hipMemcpyHostToDevice));
   return CLD_OK;
 }
 
@@ -596,15 +599,15 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       HIP_OK(cld_launch_order_long(offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
       list = d->d_lsorted;
     }
-    HIP_OK(cld_launch_long(&d->T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
+    HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, s));
     HIP_OK(hipEventRecord(ev[2], s));
-    HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
+    HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, s));
   } else {
     HIP_OK(hipEventRecord(ev[2], s));
-    HIP_OK(cld_launch_general(&d->T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
+    HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
                               d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
@@ -917,7 +920,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     if (special) HIP_OK(hipMemcpyAsync(V.sp, special + a, m, hipMemcpyHostToDevice, s));
     if (priors) HIP_OK(hipMemcpyAsync(V.pri, priors + 16 * a, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
-    HIP_OK(cld_launch_general_vec(&d->T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
+    HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
                                   special ? V.sp : nullptr, priors ? V.pri : nullptr, V.pool, V.pool_off, V.nch, s));
     nch.resize(m);
     HIP_OK(hipMemcpyAsync(out + a, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
@@ -1111,7 +1114,7 @@ void cld_shutdown(void) {
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
-    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
+    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree(d->d_T); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
