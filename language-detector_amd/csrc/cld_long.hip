@@ -59,9 +59,15 @@ constexpr int kDocCap = 1 << 20;                     // longest document taken (
 constexpr int kLB = kMaxScriptLowerBuffer + 256;     // lowered span + pads + hash read slack
 constexpr int kDocWords = kDocCap / 64 + 2;
 // Documents up to this size keep their per-byte classes in the slot (classify
-// writes them once, both passes' span builders stream them back, prefetching
-// a window ahead); longer ones recompute them in the span builder.
-constexpr int kClsCap = 65536 + 128;
+// writes them once, the span builder streams them back, prefetching a window
+// ahead); longer ones recompute them in the span builder.  Since the span
+// cache, pass 2 never rebuilds spans, and recomputing beats the 8 B/byte slot
+// round trip (C3 828K -> 867K, C5 18.9M -> 19.2M docs/s; profiles/round2_s3_*),
+// so by default nothing is stored (a cap of 64 stores no document).
+#ifndef LNG_CLSCAP
+#define LNG_CLSCAP 64
+#endif
+constexpr int kClsCap = LNG_CLSCAP;
 constexpr int kSpanWords = kLB / 64 + 1;
 constexpr int kListCap = kLB / 2;                    // words / spaces / chain entries per span
 constexpr int kHB = 1024;                            // hits per round (reference: <= 1000)
@@ -115,15 +121,23 @@ struct Slot {
   uint64_t x_add[kHB];
 };
 
-// Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4)
+// Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4).  The
+// scoring state and the Repeats predictor are never live together (pass 2
+// runs CheapRepWordsInplace over every cached span before scoring any, see
+// rep_all), so they share the first 8 KB.
 struct alignas(16) Smem {
-  uint8_t text[kLdsText];                // the current span's lowered text when it fits (see kLdsText)
-  uint32_t tote[256];                    // chunk tote, one key per word (uint16 wrap applied at read)
-  int32_t theta[kMaxCh];                 // chunk k takes delta/distinct emissions with offset <= theta_k
-  uint32_t lo[kMaxCh];                   // first offset of chunk k
-  uint16_t E[kMaxCh];                    // base emission number closing chunk k
-  uint16_t bst[kMaxCh + 1];
-  uint16_t st[2][kMaxCh + 1];            // first delta [0] / distinct [1] emission of chunk k
+  union {
+    struct {
+      uint8_t text[kLdsText];            // the current span's lowered text when it fits (see kLdsText)
+      uint32_t tote[256];                // chunk tote, one key per word (uint16 wrap applied at read)
+      int32_t theta[kMaxCh];             // chunk k takes delta/distinct emissions with offset <= theta_k
+      uint32_t lo[kMaxCh];               // first offset of chunk k
+      uint16_t E[kMaxCh];                // base emission number closing chunk k
+      uint16_t bst[kMaxCh + 1];
+      uint16_t st[2][kMaxCh + 1];        // first delta [0] / distinct [1] emission of chunk k
+    };
+    uint16_t pred[kPredictionTableSize]; // Repeats predictor, 16-bit codes (pred_code)
+  };
   uint64_t ring[2][4];                   // distinct boosts (as tote adds), latn / othr, oldest first
   DocTote dt;
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
@@ -131,14 +145,25 @@ struct alignas(16) Smem {
   unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
 };
 
-#ifndef LNG_PROF_ON
-
-#endif
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
 // 3 repeats, 4 word lists + quad chain, 5 quad hits, 6 octa/uni/bi hits,
-// 7 linearize/chunk/score
+// 7 linearize/chunk/score.  Built with -DLNG_PROF_SUB, slots 0-5 instead split
+// score_round (mark_sub) and every other stage lands in slot 6.
+#ifdef LNG_PROF_SUB
+constexpr bool kProfSub = true;
+#else
+constexpr bool kProfSub = false;
+#endif
 __device__ __forceinline__ void mark(Smem& s, int lane, int stage, long long& t) {
+  if (kProfSub && stage != 7) stage = 6;
   if (s.prof) {
+    const long long now = (long long)clock64();
+    if (lane == 0) atomicAdd(&s.prof[stage], (unsigned long long)(now - t));
+    t = now;
+  }
+}
+__device__ __forceinline__ void mark_sub(Smem& s, int lane, int stage, long long& t) {
+  if (kProfSub && s.prof) {
     const long long now = (long long)clock64();
     if (lane == 0) atomicAdd(&s.prof[stage], (unsigned long long)(now - t));
     t = now;
@@ -666,6 +691,154 @@ __device__ bool predict_window(uint64_t* tbl, uint32_t epoch, uint64_t lm, uint3
   hcarry = rdlu(h, topbit(lm));
   gsync();
   return me && c == pc;
+}
+
+// The Repeats predictor in LDS.  The reference's table holds the packed UTF-8
+// bytes of a character (next_char_code; up to 32 bits); the LDS table holds a
+// 16-bit code that is one-to-one on every value a table entry is compared
+// against, except a sentinel class whose full value goes to the slot's
+// overflow table (S.pred, low 32 bits):
+//   1 byte (c < 0xC0)                        c                  0x0000-0x00BF
+//   2 bytes, continuation second byte        0xD800 | 11 bits   0xD800-0xDFFF
+//   3 bytes, well formed, not overlong,      the 16-bit scalar  0x0800-0xFFFF
+//     not a surrogate                                           minus 0xD800-0xDFFF
+//   anything else (4 bytes, malformed)       kPredSent          0x07FF
+// The ranges are disjoint, so equal codes <=> equal values outside the
+// sentinel class.  The empty table (all 0) reads as the reference's 0.
+constexpr uint32_t kPredSent = 0x07FF;
+__device__ __forceinline__ uint32_t pred_code(uint32_t b0, uint32_t b1, uint32_t b2, int incr) {
+  if (incr == 1) return b0;
+  const bool c1 = (b1 & 0xC0) == 0x80, c2 = (b2 & 0xC0) == 0x80;
+  if (incr == 2) return c1 ? 0xD800u | ((b0 & 0x1F) << 6) | (b1 & 0x3F) : kPredSent;
+  if (incr == 3 && c1 && c2) {
+    const uint32_t v = ((b0 & 0xF) << 12) | ((b1 & 0x3F) << 6) | (b2 & 0x3F);
+    if (v >= 0x800 && (v < 0xD800 || v > 0xDFFF)) return v;
+  }
+  return kPredSent;
+}
+
+// predict_window on the LDS table: the first lane of a key in the window
+// reads the code (and, for the sentinel, the overflow value); the last lane of
+// a key writes it.
+__device__ __forceinline__ bool predict_window_lds(uint16_t* tbl, uint64_t* ovf, uint64_t lm, uint32_t c,
+                                                   uint32_t code, uint32_t& hcarry, int lane) {
+  const bool me = (lm >> lane) & 1;
+  const uint64_t below = lm & lanemask_lt(lane);
+  const int p1 = below ? topbit(below) : -1;
+  const uint64_t below2 = p1 > 0 ? (below & lanemask_lt(p1)) : 0ull;
+  const int p2 = below2 ? topbit(below2) : -1;
+  const uint32_t c1 = shfl32(c, p1 < 0 ? lane : p1);
+  const uint32_t c2 = shfl32(c, p2 < 0 ? lane : p2);
+  uint32_t h;
+  if (p1 < 0) h = (c ^ (hcarry << 4)) & 0xFFFu;
+  else if (p2 < 0) h = (c ^ (c1 << 4) ^ (hcarry << 8)) & 0xFFFu;
+  else h = (c ^ (c1 << 4) ^ (c2 << 8)) & 0xFFFu;
+  const uint32_t hp = shfl32(h, p1 < 0 ? lane : p1);
+  const uint32_t key = p1 < 0 ? hcarry : hp;
+  uint64_t eq = lm;
+#pragma unroll
+  for (int b = 0; b < 12; ++b) {
+    const bool bit = (key >> b) & 1;
+    const uint64_t m = __ballot(bit);
+    eq &= bit ? m : ~m;
+  }
+  const uint64_t earlier = eq & lanemask_lt(lane);
+  const uint32_t pc = shfl32(c, earlier ? topbit(earlier) : lane);
+  bool pr = me && earlier && c == pc;
+  if (me && !earlier) {
+    const uint32_t pcode = tbl[key];
+    pr = pcode == kPredSent ? (uint32_t)ovf[key] == c : pcode == code;
+  }
+  const bool last = (eq & ~mask_le(lane)) == 0;
+  const bool wr = me && last;
+  if (wr) tbl[key] = (uint16_t)code;
+  hcarry = rdlu(h, topbit(lm));
+  if (__ballot(wr && code == kPredSent)) {
+    if (wr && code == kPredSent) ovf[key] = c;
+    gsync();
+  }
+  return pr;
+}
+
+// CheapRepWordsInplace (compact_lang_det_impl.cc:610-692) on one span of the
+// span cache, in place, in one pass: like the reference, every byte goes to
+// dst as it is read, and a space whose segment was mostly predicted rewinds
+// dst to the start of its word.  Per 64-byte window the pieces that end at a
+// space of the window are decided; a deleted piece is not written (the
+// reference writes it and then rewinds over it: only bytes past the final
+// length differ, and nothing reads those), a kept piece and the open piece at
+// the window end are written at their dst positions (<= their source
+// positions, so in place is safe).  The next window's bytes are loaded while
+// the current one is processed.  hcarry carries from span to span.
+__device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len, uint32_t& hcarry, bool careful,
+                            bool& ok, int lane) {
+  const int nw = (len + 63) >> 6;
+  int D = 0, WD = 0;                     // dst, word_dst (as offsets)
+  int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
+  int carry = 0;
+  uint32_t n0 = text[lane], n1 = text[lane + 1], n2 = text[lane + 2];
+  for (int w = 0; w < nw; ++w) {
+    const int base = w << 6, x = base + lane;
+    const uint32_t b0 = n0, b1 = n1, b2 = n2;
+    if (w + 1 < nw) {
+      n0 = text[x + 64];
+      n1 = text[x + 65];
+      n2 = text[x + 66];
+    }
+    const bool valid = x < len;
+    const uint64_t st = char_starts(text, base, len, nullptr, carry, careful, lane);
+    const bool lead = valid && ((st >> lane) & 1);
+    int incr = 1;
+    uint32_t c = 0, code = 0;
+    if (lead) {
+      incr = b0 < 0xC0 ? 1 : (b0 & 0xE0) == 0xC0 ? 2 : (b0 & 0xF0) == 0xE0 ? 3 : 4;
+      if (incr == 1) c = b0;
+      else if (incr == 2) c = (b0 << 8) | b1;
+      else if (incr == 3) c = (b0 << 16) | (b1 << 8) | b2;
+      else c = (b0 << 24) | (b1 << 16) | (b2 << 8) | (uint32_t)text[x + 3];
+      code = pred_code(b0, b1, b2, incr);
+    }
+    const uint64_t lm = __ballot(lead);
+    const bool pr = lm ? predict_window_lds(tbl, ovf, lm, c, code, hcarry, lane) : false;
+    const int wl = lead ? incr : 0, gd = (lead && pr) ? incr : 0;
+    const bool sp = lead && b0 == ' ';
+    const uint64_t spm = __ballot(sp);
+    const int ewl = excl_scan(wl, lane), egd = excl_scan(gd, lane);
+    const uint64_t psp = spm & lanemask_lt(lane);
+    const int ps = psp ? topbit(psp) : lane;
+    const int ewl_ps = __shfl(ewl, ps, 64), egd_ps = __shfl(egd, ps, 64);
+    const int swl = psp ? ewl - ewl_ps : cwl + ewl;
+    const int sgd = psp ? egd - egd_ps : cgd + egd;
+    const uint64_t dm = __ballot(sp && sgd * 2 > swl);
+    const int twl = rdl(ewl + wl, 63), tgd = rdl(egd + gd, 63);
+    // pieces: a byte belongs to the first space at or after it in the window
+    const uint64_t ge = spm & ~lanemask_lt(lane);
+    const bool write = valid && (!ge || !((dm >> __builtin_ctzll(ge)) & 1));
+    const uint64_t km = __ballot(write);
+    const int bD = (spm && ((dm >> __builtin_ctzll(spm)) & 1)) ? WD : D;   // first piece deleted: rewind
+    if (write) text[bD + __popcll(km & lanemask_lt(lane))] = (uint8_t)b0;
+    if (spm) {
+      const int ls = topbit(spm);
+      WD = bD + __popcll(km & mask_le(ls));
+      cwl = twl - rdl(ewl, ls);
+      cgd = tgd - rdl(egd, ls);
+    } else {
+      cwl += twl;
+      cgd += tgd;
+    }
+    D = bD + __popcll(km);
+  }
+  // a last character claiming bytes past the span would make the reference
+  // copy pad bytes too: k_general takes that (malformed) document
+  ok = carry == 0;
+  // "   \0" if at least 4 bytes went, else a single ' ' if any went (:684-689)
+  if (D < len - 3) {
+    if (lane < 4) text[D + lane] = lane < 3 ? ' ' : 0;
+  } else if (D < len) {
+    if (lane == 0) text[D] = ' ';
+  }
+  gsync();
+  return D;
 }
 
 // CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) on a lowered span
@@ -1274,6 +1447,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   const DevTbl& dob = cjk ? T.deltabi : T.deltaocta;
   const DevTbl& xob = cjk ? T.distinctbi : T.distinctocta;
   const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
+  long long t2 = (D && kProfSub && s.prof) ? (long long)clock64() : 0;
 
   // base hits -> base emissions (1 or 2 langprobs, zeros dropped)
   int eb = 0;
@@ -1313,6 +1487,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       S.be_add[o + 1] = tote_adds(T, l2);
     }
   }
+  if constexpr (D) mark_sub(s, lane, 0, t2);
   // delta / distinct emissions, compacted in place (ind -> langprob)
   int ed = 0, ex = 0;
   for (int j0 = 0; j0 < nd; j0 += 64) {
@@ -1337,6 +1512,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       S.x_add[o] = tote_adds(T, lp);
     }
   }
+  if constexpr (D) mark_sub(s, lane, 1, t2);
   // chunk plan from the base-hit count (ChunkAll :978-1031)
   int K = 0;
   if (nb <= 0) {
@@ -1412,6 +1588,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     s.lo[k] = m;
   }
   wsync();
+  if constexpr (D) mark_sub(s, lane, 2, t2);
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
@@ -1478,6 +1655,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     }
     wsync();
   }
+  if constexpr (D) mark_sub(s, lane, 3, t2);
   // SetChunkSummary (scoreonescriptspan.cc:60-96) for every chunk at once, one
   // lane per chunk (K <= kMaxCh = 64); the DocTote adds then run in chunk order on lane 0
   int lo = 0, hi = 0, lang1 = 0, lang2 = 0, rd = 0, rsc = 0;
@@ -1531,6 +1709,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
   wsync();
+  if constexpr (D) mark_sub(s, lane, 4, t2);
 }
 
 __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, int lane) {
@@ -1646,7 +1825,23 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
     if (lane == 0) s.dt.init();
     if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
     uint32_t hcarry = 0, ep = 0;
-    if (rep) ep = new_epoch(S.epoch, S.pred, lane);
+    if (from_cache) {
+      // Repeats over every cached span first, predictor in LDS (the scoring
+      // state it shares the LDS with is dead until the span loop below)
+      for (int i = lane; i < kPredictionTableSize / 8; i += 64) reinterpret_cast<uint4*>(s.pred)[i] = make_uint4(0, 0, 0, 0);
+      wsync();
+      for (int i = 0; i < nsp; ++i) {
+        bool okr;
+        const int tb = rep_span_lds(s.pred, S.pred, S.lbd + ufl(S.sp_off[i]), ufl(S.sp_tb[i]), hcarry, careful, okr, lane);
+        if (!okr) return -kWhySpan;
+        if (lane == 0) S.sp_tb[i] = tb;
+      }
+      gsync();
+      if constexpr (D) mark(s, lane, 3, t);
+    } else if (rep) {
+      ep = new_epoch(S.epoch, S.pred, lane);
+    }
+    const bool rep_inline = rep && !from_cache;
     wsync();
     int next = 0, total = 0, ci = 0;
     bool restart = false;
@@ -1692,7 +1887,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
           reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(lb)[i];
         wsync();
         if (sq) tb = squeeze_span(S, s.text, tb, careful, lane);             // in place, as the reference does
-        if (rep) {
+        if (rep_inline) {
           bool okr;
           tb = rep_words(S, s.text, s.text, tb, hcarry, ep, careful, okr, lane);   // in place, as the reference does
           if (!okr) return -kWhySpan;
@@ -1707,7 +1902,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
       } else {
         const uint8_t* text = lb;
         if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
-        if (rep) {
+        if (rep_inline) {
           bool okr;
           tb = rep_words(S, lb, S.lb[1], tb, hcarry, ep, careful, okr, lane);
           if (!okr) return -kWhySpan;
