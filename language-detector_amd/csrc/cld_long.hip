@@ -309,31 +309,74 @@ __device__ __noinline__ uint64_t char_slow(DevSM script, DevSM scan, DevSM lower
          ((uint64_t)olen << 20) | ((o & 0xFFFFFFFFull) << 32);
 }
 
+// The document bytes p..p+7 (NULs past its end) as three aligned dwords: a
+// dword is loaded only if it holds a byte of the document, so nothing past
+// the buffer is touched.  Lanes load them a window ahead (raw_load), and
+// raw_bytes realigns them when the window is processed.
+__device__ __forceinline__ void raw_load(const DocView& dv, int p, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
+  const uintptr_t a = (uintptr_t)(dv.p + p) & ~(uintptr_t)3, end = (uintptr_t)(dv.p + dv.len);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
+  d0 = a < end ? q[0] : 0u;
+  d1 = a + 4 < end ? q[1] : 0u;
+  d2 = a + 8 < end ? q[2] : 0u;
+}
+__device__ __forceinline__ void raw_bytes(const DocView& dv, int p, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t& lo,
+                                          uint32_t& hi) {
+  const uint32_t sh = (uint32_t)((uintptr_t)(dv.p + p) & 3);
+  lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const int v = dv.len - p;                      // bytes of the document from p on
+  if (v < 8) {
+    if (v <= 0) lo = hi = 0;
+    else if (v < 4) { lo &= (1u << (8 * v)) - 1u; hi = 0; }
+    else hi &= v == 4 ? 0u : (1u << (8 * (v - 4))) - 1u;
+  }
+}
+
 // Per byte p of the document: the class word (cls_* above) and, for a lead
 // byte, the lowered bytes of its character (LowerScriptSpan is per character
 // once each one starts and ends in state 0, checked by lower_char).  The 8
-// bytes a lane needs are loaded up front (one round trip), then one
-// property-table lookup per character; 4-byte and cut characters run the
-// machines.  bad: the character breaks the local formulation; need/conts
-// count the continuation bytes the lead bytes claim / that are present.
-// Nothing is stored: classify() and the span builder both call this, so the
-// per-wave slot holds no per-byte state.
-template <bool SN2 = true>
-__device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView& dv, int p, uint32_t& lw, int& bad,
-                                               int& need, int& conts) {
+// bytes a lane needs come in as lo/hi (raw_bytes); the property-table gathers
+// for this character and the next one are issued first, then pf() (the
+// caller's prefetch of its next window, so that those loads overlap this
+// window's gathers and work), then the gathers are used.  4-byte and cut
+// characters run the machines.  bad: the character breaks the local
+// formulation; need/conts count the continuation bytes the lead bytes claim /
+// that are present.  Nothing is stored: classify() and the span builder both
+// call this, so the per-wave slot holds no per-byte state.
+template <bool SN2, class Pf>
+__device__ __forceinline__ uint32_t char_props_b(const DevTables& T, const DocView& dv, int p, uint32_t lo, uint32_t hi,
+                                                 uint32_t& lw, int& bad, int& need, int& conts, Pf&& pf) {
   const int L = dv.len;
-  lw = 0;
-  if (p >= L) return 0u;
   uint32_t b[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) b[k] = dv.at(p + k);
+  for (int k = 0; k < 4; ++k) {
+    b[k] = (lo >> (8 * k)) & 0xFF;
+    b[k + 4] = (hi >> (8 * k)) & 0xFF;
+  }
   const uint32_t c = b[0];
-  if ((c & 0xC0) == 0x80) {
+  const bool inr = p < L, cont = (c & 0xC0) == 0x80;
+  const int n = utf8_len((uint8_t)c);
+  const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
+  const bool fast = inr && !cont && avail == n && n <= 3;
+  // script of the next character (its bytes are b[n..n+3]; NULs past the end)
+  const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
+  const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
+  const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
+  const int n2 = utf8_len((uint8_t)c2);
+  int i2 = -1;
+  if (c2 < 0x80) i2 = (int)c2;
+  else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) i2 = cpt_index(c2, d1, 0, 2);
+  else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80) i2 = cpt_index(c2, d1, d2, 3);
+  const uint64_t e = T.cpt[fast ? cpt_index(b[0], b[1], b[2], n) : 0];
+  const uint64_t e2 = SN2 ? T.cpt[i2 >= 0 ? i2 : 0] : 0ull;
+  pf();
+  lw = 0;
+  if (!inr) return 0u;
+  if (cont) {
     ++conts;
     return 0u;
   }
-  const int n = utf8_len((uint8_t)c);
-  const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
   bool wf = true;
 #pragma unroll
   for (int k = 1; k < 4; ++k)
@@ -342,8 +385,7 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
   need += avail - 1;
   int sn, st, olen = 0;
   bool lowok;
-  if (avail == n && n <= 3) {
-    const uint64_t e = T.cpt[cpt_index(b[0], b[1], b[2], n)];
+  if (fast) {
     sn = (int)(e & 0xFF);
     st = (int)((e >> 8) & 3);
     if (st == 3) st = -1;
@@ -351,30 +393,30 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
     olen = (int)((e >> 11) & 15);
     lw = (uint32_t)(e >> 32);
   } else {                                   // 4-byte or cut: run the machines (out of line)
-    const uint64_t e = char_slow(T.script, T.scan, T.lower, dv, p, n, avail);
-    sn = (int)(e & 0xFF);
-    st = (int)(int8_t)((e >> 8) & 0xFF);
-    lowok = (e >> 16) & 1;
-    olen = (int)((e >> 20) & 15);
-    lw = (uint32_t)(e >> 32);
+    const uint64_t es = char_slow(T.script, T.scan, T.lower, dv, p, n, avail);
+    sn = (int)(es & 0xFF);
+    st = (int)(int8_t)((es >> 8) & 0xFF);
+    lowok = (es >> 16) & 1;
+    olen = (int)((es >> 20) & 15);
+    lw = (uint32_t)(es >> 32);
   }
-  // script of the next character (its bytes are b[n..n+3]; NULs past the end)
   int sn2 = 0;
-  if constexpr (SN2) {
-  const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
-  const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
-  const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
-  const int n2 = utf8_len((uint8_t)c2);
-  if (c2 < 0x80) sn2 = (int)(T.cpt[c2] & 0xFF);
-  else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) sn2 = (int)(T.cpt[cpt_index(c2, d1, 0, 2)] & 0xFF);
-  else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80)
-    sn2 = (int)(T.cpt[cpt_index(c2, d1, d2, 3)] & 0xFF);
-  else sn2 = script_num(T, dv, p + n);
-  }
+  if constexpr (SN2) sn2 = i2 >= 0 ? (int)(e2 & 0xFF) : script_num(T, dv, p + n);
   if (st < 0) bad = 1;
   const bool ls = st > 0 && sn != 0;
   return (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
          ((uint32_t)(avail < n) << 21) | ((uint32_t)!lowok << 22) | ((uint32_t)olen << 24);
+}
+struct NoPf {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <bool SN2 = true>
+__device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView& dv, int p, uint32_t& lw, int& bad,
+                                               int& need, int& conts) {
+  uint32_t d0, d1, d2, lo, hi;
+  raw_load(dv, p, d0, d1, d2);
+  raw_bytes(dv, p, d0, d1, d2, lo, hi);
+  return char_props_b<SN2>(T, dv, p, lo, hi, lw, bad, need, conts, NoPf{});
 }
 
 // Validity of the per-character formulation over the whole document, and the
@@ -387,10 +429,15 @@ __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& c
   int bad = 0, conts = 0, need = 0;
   cut = false;
   const int nw = (L + 63) >> 6;
+  uint32_t r0, r1, r2;                           // raw dwords of the next window
+  raw_load(dv, lane, r0, r1, r2);
   for (int w = 0; w < nw; ++w) {
     const int p = (w << 6) + lane;
-    uint32_t lw;
-    const uint32_t cw = char_props<ST>(T, dv, p, lw, bad, need, conts);
+    uint32_t lw, lo, hi;
+    raw_bytes(dv, p, r0, r1, r2, lo, hi);
+    const uint32_t cw = char_props_b<ST>(T, dv, p, lo, hi, lw, bad, need, conts, [&]() {
+      if (w + 1 < nw) raw_load(dv, p + 64, r0, r1, r2);
+    });
     if constexpr (ST) {
       if (p < L) {
         S.cls[p] = cw;
@@ -452,8 +499,11 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   if (lane == 0) lb[0] = ' ';
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
-  // stored classes: window w+1's words are loaded while window w is processed
+  // stored classes: window w+1's words are loaded while window w is processed;
+  // else window w+1's raw bytes are
   uint32_t ncw = 0, nlw = 0;
+  uint32_t r0 = 0, r1 = 0, r2 = 0;
+  if constexpr (!ST) raw_load(dv, ((q >> 6) << 6) + lane, r0, r1, r2);
   if constexpr (ST) {
     const int x0 = ((q >> 6) << 6) + lane;
     if (x0 >= q && x0 < L) {
@@ -476,7 +526,15 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       }
     } else {
       int ignore2 = 0;
-      if (x >= q) cw = char_props(T, dv, x, lw, ignore2, ignore2, ignore2);
+      uint32_t lo, hi;
+      raw_bytes(dv, x, r0, r1, r2, lo, hi);
+      cw = char_props_b<true>(T, dv, x, lo, hi, lw, ignore2, ignore2, ignore2, [&]() {
+        raw_load(dv, x + 64, r0, r1, r2);        // (guarded: nothing past the document is read)
+      });
+      if (x < q) {
+        cw = 0;
+        lw = 0;
+      }
     }
     const bool lead = cls_lead(cw);
     const int n = cls_n(cw);
