@@ -84,9 +84,14 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 // at LDS latency instead of through the per-wave HBM slot.  Longer spans run
 // the same code on the slot copy.
 #ifndef LNG_TEXT
-#define LNG_TEXT 5632
+#define LNG_TEXT 6128                    // fills the 8 KB the scoring state shares with the Repeats predictor
 #endif
 constexpr int kLdsText = LNG_TEXT;
+// Read-ahead of the slot's streams (bit 1 word starts, 2 quad chain, 4 octa
+// word ends, 8 hit streams in score_round): overlap vs the registers it costs.
+#ifndef LNG_PF
+#define LNG_PF 4
+#endif
 
 // Per-wave working set in HBM (one per resident wavefront of the persistent grid).
 struct Slot {
@@ -144,6 +149,7 @@ struct alignas(16) Smem {
   uint32_t dbg_pos;
   unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
 };
+static_assert(sizeof(Smem) <= 8640, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
 
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
 // 3 repeats, 4 word lists + quad chain, 5 quad hits, 6 octa/uni/bi hits,
@@ -844,7 +850,9 @@ __device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len
       n2 = text[x + 66];
     }
     const bool valid = x < len;
-    const uint64_t st = char_starts(text, base, len, nullptr, carry, careful, lane);
+    // (well-formed text: the starts come from the bytes already in registers)
+    const uint64_t st = careful ? char_starts(text, base, len, nullptr, carry, careful, lane)
+                                : __ballot(valid && (b0 & 0xC0) != 0x80);
     const bool lead = valid && ((st >> lane) & 1);
     int incr = 1;
     uint32_t c = 0, code = 0;
@@ -1183,13 +1191,13 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
 
 __device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int lane) {
   int nch = 0;
+  int sn = (LNG_PF & 1) && lane < nws ? S.wst[lane] : 0;       // word starts one block ahead
   for (int i0 = 0; i0 < nws; i0 += 64) {
     const int i = i0 + lane;
-    int cnt = 0, s = 0;
-    if (i < nws) {
-      s = S.wst[i];
-      cnt = walk_word(text, s, tb, nullptr);
-    }
+    int cnt = 0;
+    const int s = (LNG_PF & 1) ? sn : (i < nws ? S.wst[i] : 0);
+    if (LNG_PF & 1) sn = i + 64 < nws ? S.wst[i + 64] : 0;
+    if (i < nws) cnt = walk_word(text, s, tb, nullptr);
     const int pre = excl_scan(cnt, lane);
     const int tot = rdl(pre + cnt, 63);
     if (nch + tot > kListCap) return -1;
@@ -1207,13 +1215,16 @@ __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* tex
                           int lane) {
   nb = 0;
   uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
+  int pn = (LNG_PF & 2) && c0 + lane < nch ? S.chain[c0 + lane] : 0;   // chain entries one block ahead
   for (int i0 = c0; i0 < nch; i0 += 64) {
     const int i = i0 + lane;
     bool hit = false;
     uint32_t hv = 0, ind = 0;
     int p = 0;
+    const int pc = (LNG_PF & 2) ? pn : (i < nch ? S.chain[i] : 0);
+    if (LNG_PF & 2) pn = i + 64 < nch ? S.chain[i + 64] : 0;
     if (i < nch) {
-      p = S.chain[i];
+      p = pc;
       int e = p;
       e += adv_but_space(text[e]);
       e += adv_but_space(text[e]);
@@ -1299,19 +1310,28 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
   nd = 0;
   nx = 0;
   uint64_t A = 0, B = 0;                 // last two kept word hashes
-  const int jfirst = j0;
+  // word-ending spaces one block ahead; a word's start and the one before
+  // come from the previous lanes (lanes 0/1: the previous block's last two)
+  int en = (LNG_PF & 4) && j0 + lane < nsp ? S.wsp[j0 + lane] : 0x7FFFFFFF;
+  int c1 = start - 1, c2 = start - 1;    // wsp[jb - 1], wsp[jb - 2] as "start - 1" before jfirst
   for (int jb = j0;; jb += 64) {
     const int j = jb + lane;
-    const bool v = j < nsp && (int)S.wsp[j] < lim;
+    const int ej = (LNG_PF & 4) ? en : (j < nsp ? S.wsp[j] : 0x7FFFFFFF);
+    if (LNG_PF & 4) en = j + 64 < nsp ? S.wsp[j + 64] : 0x7FFFFFFF;
+    const bool v = j < nsp && ej < lim;
     const uint64_t vm = __ballot(v);
     if (!vm) break;
     const int nv = __popcll(vm);
+    const int e1 = (int)wave::wshr1((uint32_t)ej, (uint32_t)c1);          // wsp[j - 1]
+    const int e2 = (int)wave::wshr1((uint32_t)e1, (uint32_t)c2);          // wsp[j - 2]
+    c1 = rdl(ej, 63);
+    c2 = rdl(ej, 62);
     int a = start, pws = start, e = 0;
     uint64_t wh = 0;
     if (v) {
-      e = S.wsp[j];
-      a = j == jfirst ? start : S.wsp[j - 1] + 1;
-      pws = j <= jfirst + 1 ? start : S.wsp[j - 2] + 1;
+      e = ej;
+      a = e1 + 1;
+      pws = e2 + 1;
       int we = a, q = a, cc = 0;
       while (q < e) {
         ++cc;
@@ -1508,14 +1528,25 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   long long t2 = (D && kProfSub && s.prof) ? (long long)clock64() : 0;
 
   // base hits -> base emissions (1 or 2 langprobs, zeros dropped)
+  // (each stream is read one block ahead, so its load overlaps the current
+  // block's table gathers)
   int eb = 0;
+  const bool pf = LNG_PF & 8;
+  int noff = pf && lane < nb ? S.b_off[lane] : 0;
+  uint32_t nind = pf && lane < nb ? S.b_ind[lane] : 0u;
   for (int j0 = 0; j0 < nb; j0 += 64) {
     const int j = j0 + lane;
     uint32_t l1 = 0, l2 = 0;
     int off = 0;
+    const int coff = pf ? noff : (j < nb ? S.b_off[j] : 0);
+    const uint32_t cind = pf ? nind : (j < nb ? S.b_ind[j] : 0u);
+    if (pf) {
+      noff = j + 64 < nb ? S.b_off[j + 64] : 0;
+      nind = j + 64 < nb ? S.b_ind[j + 64] : 0u;
+    }
     if (j < nb) {
-      off = S.b_off[j];
-      uint32_t ind = S.b_ind[j];
+      off = coff;
+      uint32_t ind = cind;
       const DevTbl* lb = &bo;
       if (ind & 0x80000000u) {
         lb = &bo2;
@@ -1548,10 +1579,17 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   if constexpr (D) mark_sub(s, lane, 0, t2);
   // delta / distinct emissions, compacted in place (ind -> langprob)
   int ed = 0, ex = 0;
+  uint32_t dni = pf && lane < nd ? S.d_ind[lane] : 0u;
+  uint16_t dno = pf && lane < nd ? S.d_off[lane] : (uint16_t)0;
   for (int j0 = 0; j0 < nd; j0 += 64) {
     const int j = j0 + lane;
-    const uint32_t lp = j < nd ? ind_at(dob, S.d_ind[j]) : 0u;
-    const uint16_t off = j < nd ? S.d_off[j] : (uint16_t)0;
+    const uint32_t ci = pf ? dni : (j < nd ? S.d_ind[j] : 0u);
+    const uint16_t off = pf ? dno : (j < nd ? S.d_off[j] : (uint16_t)0);
+    if (pf) {
+      dni = j + 64 < nd ? S.d_ind[j + 64] : 0u;
+      dno = j + 64 < nd ? S.d_off[j + 64] : (uint16_t)0;
+    }
+    const uint32_t lp = j < nd ? ind_at(dob, ci) : 0u;
     const int o = ed + excl_scan(lp != 0, lane);
     ed = rdl(o + (lp != 0), 63);
     if (lp) {
@@ -1559,10 +1597,17 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       S.d_add[o] = tote_adds(T, lp);
     }
   }
+  uint32_t xni = pf && lane < nx ? S.x_ind[lane] : 0u;
+  uint16_t xno = pf && lane < nx ? S.x_off[lane] : (uint16_t)0;
   for (int j0 = 0; j0 < nx; j0 += 64) {
     const int j = j0 + lane;
-    const uint32_t lp = j < nx ? ind_at(xob, S.x_ind[j]) : 0u;
-    const uint16_t off = j < nx ? S.x_off[j] : (uint16_t)0;
+    const uint32_t ci = pf ? xni : (j < nx ? S.x_ind[j] : 0u);
+    const uint16_t off = pf ? xno : (j < nx ? S.x_off[j] : (uint16_t)0);
+    if (pf) {
+      xni = j + 64 < nx ? S.x_ind[j + 64] : 0u;
+      xno = j + 64 < nx ? S.x_off[j + 64] : (uint16_t)0;
+    }
+    const uint32_t lp = j < nx ? ind_at(xob, ci) : 0u;
     const int o = ex + excl_scan(lp != 0, lane);
     ex = rdl(o + (lp != 0), 63);
     if (lp) {
