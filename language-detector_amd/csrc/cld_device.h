@@ -18,6 +18,8 @@ struct DevSM {
 struct DevTbl {
   const uint32_t* b;          // n_buckets x 4 keyvalues
   const uint32_t* ind;        // indirect langprobs
+  const uint64_t* adds;       // per indirect entry: its langprob's three tote adds (lng::tote_adds),
+                              // bit 63 set if the langprob is non-zero (k_long; built on device)
   uint32_t size_one, size, key_mask, n_ind, n_buckets;
 };
 

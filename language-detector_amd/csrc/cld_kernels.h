@@ -66,6 +66,11 @@ size_t cld_cpt_entries();
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);
 size_t cld_keytab_entries();
 hipError_t cld_build_keytab(const DevTables* T, uint64_t* out, hipStream_t s);
+// ind -> tote adds for the seven scoring tables, back to back in `out`
+// (compat, deltabi, distinctbi, quad, quad2, deltaocta, distinctocta order);
+// sets each table's `adds` pointer in *T.
+size_t cld_adds_entries(const DevTables* T);
+hipError_t cld_build_adds(DevTables* T, uint64_t* out, hipStream_t s);
 int cld_long_waves_per_simd();
 size_t cld_strip_scratch_bytes(int n);
 hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,

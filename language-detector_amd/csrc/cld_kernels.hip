@@ -318,6 +318,15 @@ __global__ __launch_bounds__(256) void k_build_keytab(DevTables T, uint64_t* __r
   out[i] = lng::keytab_eval(T, i >> 8, i & 255);
 }
 
+// Tote adds per indirect entry of one scoring table (k_long reads them with
+// one gather instead of the indirect langprob and then its kLgProbV2Tbl row).
+__global__ __launch_bounds__(256) void k_build_adds(DevTables T, DevTbl t, uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.n_ind) return;
+  const uint32_t lp = t.ind[i];
+  out[i] = lp ? (lng::tote_adds(T, lp) | (1ull << 63)) : 0ull;
+}
+
 // Character property table (lng::cpt_eval over every 1-3 byte sequence).
 __global__ __launch_bounds__(256) void k_build_cpt(DevTables T, uint64_t* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -351,6 +360,18 @@ hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 size_t cld_keytab_entries() { return 256 * 256; }
+size_t cld_adds_entries(const DevTables* T) {
+  return (size_t)T->compat.n_ind + T->deltabi.n_ind + T->distinctbi.n_ind + T->quad.n_ind + T->quad2.n_ind +
+         T->deltaocta.n_ind + T->distinctocta.n_ind;
+}
+hipError_t cld_build_adds(DevTables* T, uint64_t* out, hipStream_t s) {
+  for (DevTbl* t : {&T->compat, &T->deltabi, &T->distinctbi, &T->quad, &T->quad2, &T->deltaocta, &T->distinctocta}) {
+    t->adds = out;
+    if (t->n_ind) hipLaunchKernelGGL(cld::k_build_adds, dim3((t->n_ind + 255) / 256), dim3(256), 0, s, *T, *t, out);
+    out += t->n_ind;
+  }
+  return hipGetLastError();
+}
 hipError_t cld_build_keytab(const DevTables* T, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(cld::k_build_keytab, dim3(256), dim3(256), 0, s, *T, out);
   return hipGetLastError();

@@ -1495,6 +1495,9 @@ __device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
          ((uint64_t)((e >> 16) & 0xFF) << 24) | ((uint64_t)(lp >> 24) << 32) | ((uint64_t)(e >> 24) << 40);
 }
 
+// The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
+__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? t.adds[i] : 0ull; }
+
 // Per (script, key): language | close set << 16 | expected score << 32
 // (FromPerScriptNumber, close sets, kAvgDeltaOctaScore: lang_script.cc:328-341,
 // 261-310; scoreonescriptspan.cc:75-80), one table per GPU built by
@@ -1536,7 +1539,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   uint32_t nind = pf && lane < nb ? S.b_ind[lane] : 0u;
   for (int j0 = 0; j0 < nb; j0 += 64) {
     const int j = j0 + lane;
-    uint32_t l1 = 0, l2 = 0;
+    uint64_t l1 = 0, l2 = 0;                // tote adds (bit 63: non-zero langprob)
     int off = 0;
     const int coff = pf ? noff : (j < nb ? S.b_off[j] : 0);
     const uint32_t cind = pf ? nind : (j < nb ? S.b_ind[j] : 0u);
@@ -1553,27 +1556,27 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
         ind &= ~0x80000000u;
       }
       if (ind < lb->size_one) {
-        l1 = ind_at(*lb, ind);
+        l1 = adds_at(*lb, ind);
       } else {
         ind += ind - lb->size_one;
-        l1 = ind_at(*lb, ind);
-        l2 = ind_at(*lb, ind + 1);
-        if (l1 == 0) {
+        l1 = adds_at(*lb, ind);
+        l2 = adds_at(*lb, ind + 1);
+        if (!(l1 >> 63)) {
           l1 = l2;
           l2 = 0;
         }
       }
     }
-    const int c = (l1 != 0) + (l2 != 0);
+    const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
     const int o = eb + excl_scan(c, lane);
     eb = rdl(o + c, 63);
-    if (l1) {
+    if (l1 >> 63) {
       S.be_off[o] = (uint16_t)off;
-      S.be_add[o] = tote_adds(T, l1);
+      S.be_add[o] = l1;
     }
-    if (l2) {
+    if (l2 >> 63) {
       S.be_off[o + 1] = (uint16_t)off;
-      S.be_add[o + 1] = tote_adds(T, l2);
+      S.be_add[o + 1] = l2;
     }
   }
   if constexpr (D) mark_sub(s, lane, 0, t2);
@@ -1589,12 +1592,13 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       dni = j + 64 < nd ? S.d_ind[j + 64] : 0u;
       dno = j + 64 < nd ? S.d_off[j + 64] : (uint16_t)0;
     }
-    const uint32_t lp = j < nd ? ind_at(dob, ci) : 0u;
-    const int o = ed + excl_scan(lp != 0, lane);
-    ed = rdl(o + (lp != 0), 63);
-    if (lp) {
+    const uint64_t a = j < nd ? adds_at(dob, ci) : 0ull;
+    const int nz = (int)(a >> 63);
+    const int o = ed + excl_scan(nz, lane);
+    ed = rdl(o + nz, 63);
+    if (nz) {
       S.d_off[o] = off;
-      S.d_add[o] = tote_adds(T, lp);
+      S.d_add[o] = a;
     }
   }
   uint32_t xni = pf && lane < nx ? S.x_ind[lane] : 0u;
@@ -1607,12 +1611,13 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       xni = j + 64 < nx ? S.x_ind[j + 64] : 0u;
       xno = j + 64 < nx ? S.x_off[j + 64] : (uint16_t)0;
     }
-    const uint32_t lp = j < nx ? ind_at(xob, ci) : 0u;
-    const int o = ex + excl_scan(lp != 0, lane);
-    ex = rdl(o + (lp != 0), 63);
-    if (lp) {
+    const uint64_t a = j < nx ? adds_at(xob, ci) : 0ull;
+    const int nz = (int)(a >> 63);
+    const int o = ex + excl_scan(nz, lane);
+    ex = rdl(o + nz, 63);
+    if (nz) {
       S.x_off[o] = off;
-      S.x_add[o] = tote_adds(T, lp);
+      S.x_add[o] = a;
     }
   }
   if constexpr (D) mark_sub(s, lane, 1, t2);
@@ -1692,6 +1697,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   }
   wsync();
   if constexpr (D) mark_sub(s, lane, 2, t2);
+  if (D && kProfSub && s.prof && lane == 0) atomicAdd(&s.prof[5], ((unsigned long long)K << 20) | 1ull);   // chunks, rounds
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
@@ -1703,7 +1709,6 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     const int seedn = k == 0 ? 1 : 0;
     const int nB = be - bs, nD = de - ds, nX = xe - xs;
     const int tot = seedn + nB + nD + nX + kMaxBoosts;
-    uint64_t gm = 0;
     for (int t = lane; t < tot; t += 64) {
       uint64_t a;
       int u = t;
@@ -1720,26 +1725,30 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
         a = v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_add[v];
       }
       const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
-      if (k1) { atomicAdd(&s.tote[k1], (uint32_t)(a >> 8) & 0xFF); gm |= 1ull << (k1 >> 2); }
-      if (k2) { atomicAdd(&s.tote[k2], (uint32_t)(a >> 24) & 0xFF); gm |= 1ull << (k2 >> 2); }
-      if (k3) { atomicAdd(&s.tote[k3], (uint32_t)(a >> 40) & 0xFF); gm |= 1ull << (k3 >> 2); }
+      // the low half sums the score (read with the reference's uint16 wrap), the
+      // high half counts the adds: a group (the 4 keys of one lane) is in use
+      // (Tote's in_use_mask_) iff one of its keys has a non-zero high half
+      if (k1) atomicAdd(&s.tote[k1], ((uint32_t)(a >> 8) & 0xFF) | 0x10000u);
+      if (k2) atomicAdd(&s.tote[k2], ((uint32_t)(a >> 24) & 0xFF) | 0x10000u);
+      if (k3) atomicAdd(&s.tote[k3], ((uint32_t)(a >> 40) & 0xFF) | 0x10000u);
     }
-    gm = wor64(gm);
     const int score_count = nB + seedn;
     wsync();
-    // top three keys of the in-use groups: (uint16 score desc, key asc)
+    // top keys of the in-use groups: (uint16 score desc, key asc).  The
+    // reference sorts three (CurrentTopThreeKeys) but SetChunkSummary reads
+    // only the first two (scoreonescriptspan.cc:60-96), so two rounds.
     const uint4 v4 = reinterpret_cast<const uint4*>(s.tote)[lane];
-    const bool inuse = (gm >> lane) & 1;
+    const bool inuse = ((v4.x | v4.y | v4.z | v4.w) >> 16) != 0;
     const uint32_t cand[4] = {v4.x & 0xFFFF, v4.y & 0xFFFF, v4.z & 0xFFFF, v4.w & 0xFFFF};
-    int key3[3] = {-1, -1, -1};
-    uint32_t sc3[3] = {0, 0, 0};
+    int key3[2] = {-1, -1};
+    uint32_t sc3[2] = {0, 0};
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 2; ++r) {
       uint32_t best = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = lane * 4 + i;
-        const bool taken = key == key3[0] || key == key3[1];
+        const bool taken = key == key3[0];
         const uint32_t comp = (inuse && !taken) ? ((cand[i] + 1) << 8) | (uint32_t)(255 - key) : 0u;
         best = comp > best ? comp : best;
       }

@@ -436,6 +436,7 @@ struct StagedTables {
   uint8_t* blob = nullptr;
   uint64_t* cpt = nullptr;
   uint64_t* keytab = nullptr;
+  uint64_t* adds = nullptr;
   DevTables T{};
 };
 
@@ -449,6 +450,8 @@ int stage_tables(Device* d, const HostTables& t, StagedTables* st) {
   HIP_OK(cld_build_cpt(&st->T, st->cpt, d->stream));
   HIP_OK(hipMalloc(&st->keytab, cld_keytab_entries() * sizeof(uint64_t)));
   HIP_OK(cld_build_keytab(&st->T, st->keytab, d->stream));
+  HIP_OK(hipMalloc(&st->adds, std::max<size_t>(cld_adds_entries(&st->T), 1) * sizeof(uint64_t)));
+  HIP_OK(cld_build_adds(&st->T, st->adds, d->stream));   // sets T.<table>.adds (compat.adds is the base)
   HIP_OK(hipStreamSynchronize(d->stream));
   st->T.cpt = st->cpt;
   st->T.keytab = st->keytab;
@@ -460,6 +463,7 @@ void discard_tables(Device* d, StagedTables* st) {
   if (st->blob) (void)hipFree(st->blob);
   if (st->cpt) (void)hipFree(st->cpt);
   if (st->keytab) (void)hipFree(st->keytab);
+  if (st->adds) (void)hipFree(st->adds);
   *st = StagedTables();
 }
 
@@ -470,6 +474,7 @@ int commit_tables(Device* d, StagedTables* st) {
   if (d->d_blob) (void)hipFree(d->d_blob);
   if (d->T.cpt) (void)hipFree((void*)d->T.cpt);
   if (d->T.keytab) (void)hipFree((void*)d->T.keytab);
+  if (d->T.compat.adds) (void)hipFree((void*)d->T.compat.adds);
   d->d_blob = st->blob;
   d->T = st->T;
   *st = StagedTables();
@@ -1114,7 +1119,7 @@ void cld_shutdown(void) {
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
-    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree(d->d_T); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
+    (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree((void*)d->T.compat.adds); (void)hipFree(d->d_T); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);

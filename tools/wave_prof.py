@@ -39,6 +39,12 @@ def main():
         print("   long cycles/doc total %.0f  " % (lt / nl) +
               "  ".join("%s %.0f (%.0f%%)" % (LSTAGES[i], c[8 + i] / nl, 100 * c[8 + i] / max(lt, 1)) for i in range(8)),
               flush=True)
+        if os.environ.get("CLD_PROF_SUB"):
+            sub = ["base emissions", "delta/distinct", "chunk plan", "tote loop", "summaries"]
+            st = c[8:13]
+            print("   score sub-stages/doc " + "  ".join("%s %.0f" % (sub[i], st[i] / nl) for i in range(5)) +
+                  "  rounds/doc %.1f  chunks/doc %.1f" % ((int(c[13]) & 0xFFFFF) / nl, (int(c[13]) >> 20) / nl),
+                  flush=True)
 
 
 if __name__ == "__main__":
