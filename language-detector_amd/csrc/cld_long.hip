@@ -1701,29 +1701,49 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
+  // chunk k's adds: t < seedn the seed, then its base, delta and distinct
+  // emissions, then the four boosts (the last four distinct langprobs so far)
+  auto fetch = [&](int t, int k, int tot, int bs, int nB, int ds, int nD, int xs, int nX, int xe) -> uint64_t {
+    if (t >= tot) return 0ull;
+    int u = t;
+    const int seedn = k == 0 ? 1 : 0;
+    if (u < seedn) return seed;
+    if ((u -= seedn) < nB) return S.be_add[bs + u];
+    if ((u -= nB) < nD) return S.d_add[ds + u];
+    if ((u -= nD) < nX) return S.x_add[xs + u];
+    const int v = xe - kMaxBoosts + (u - nX);
+    return v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_add[v];
+  };
+  // chunk plan of k: emission ranges and the number of adds
+  auto plan = [&](int k, int& bs, int& nB, int& ds, int& nD, int& xs, int& nX, int& xe) -> int {
+    bs = s.bst[k];
+    const int be = k == K - 1 ? eb : s.bst[k + 1];
+    ds = s.st[0][k];
+    xs = s.st[1][k];
+    xe = s.st[1][k + 1];
+    nB = be - bs;
+    nD = s.st[0][k + 1] - ds;
+    nX = xe - xs;
+    return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts;
+  };
+  // the first 128 adds of chunk k + 1 are loaded while chunk k is scored
+  int pbs, pnB, pds, pnD, pxs, pnX, pxe;
+  int ptot = plan(0, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  uint64_t n0 = fetch(lane, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  uint64_t n1 = fetch(lane + 64, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
   for (int k = 0; k < K; ++k) {
+    const int bs = pbs, nB = pnB, ds = pds, nD = pnD, xs = pxs, nX = pnX, xe = pxe, tot = ptot;
+    const uint64_t a0 = n0, a1 = n1;
+    if (k + 1 < K) {
+      ptot = plan(k + 1, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      n0 = fetch(lane, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      n1 = fetch(lane + 64, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+    }
     reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
-    const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
-    const int ds = s.st[0][k], de = s.st[0][k + 1], xs = s.st[1][k], xe = s.st[1][k + 1];
     wsync();
     const int seedn = k == 0 ? 1 : 0;
-    const int nB = be - bs, nD = de - ds, nX = xe - xs;
-    const int tot = seedn + nB + nD + nX + kMaxBoosts;
     for (int t = lane; t < tot; t += 64) {
-      uint64_t a;
-      int u = t;
-      if (u < seedn) {
-        a = seed;
-      } else if ((u -= seedn) < nB) {
-        a = S.be_add[bs + u];
-      } else if ((u -= nB) < nD) {
-        a = S.d_add[ds + u];
-      } else if ((u -= nD) < nX) {
-        a = S.x_add[xs + u];
-      } else {                               // boosts: the last four distinct langprobs so far
-        const int v = xe - kMaxBoosts + (u - nX);
-        a = v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_add[v];
-      }
+      const uint64_t a = t < 128 ? (t < 64 ? a0 : a1) : fetch(t, k, tot, bs, nB, ds, nD, xs, nX, xe);
       const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
       // the low half sums the score (read with the reference's uint16 wrap), the
       // high half counts the adds: a group (the 4 keys of one lane) is in use
