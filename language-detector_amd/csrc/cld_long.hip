@@ -58,16 +58,9 @@ using wave::wsync;
 constexpr int kDocCap = 1 << 20;                     // longest document taken (C5 caps at 64 KB; the slot holds 1 bit per byte)
 constexpr int kLB = kMaxScriptLowerBuffer + 256;     // lowered span + pads + hash read slack
 constexpr int kDocWords = kDocCap / 64 + 2;
-// Documents up to this size keep their per-byte classes in the slot (classify
-// writes them once, the span builder streams them back, prefetching a window
-// ahead); longer ones recompute them in the span builder.  Since the span
-// cache, pass 2 never rebuilds spans, and recomputing beats the 8 B/byte slot
-// round trip (C3 828K -> 867K, C5 18.9M -> 19.2M docs/s; profiles/round2_s3_*),
-// so by default nothing is stored (a cap of 64 stores no document).
-#ifndef LNG_CLSCAP
-#define LNG_CLSCAP 64
-#endif
-constexpr int kClsCap = LNG_CLSCAP;
+// No per-byte state is stored: classify() and the span builder both derive
+// the classes from the document bytes (round 2 measured storing them, 8 B per
+// byte written once and streamed back, as slower: C3 828K vs 867K docs/s).
 constexpr int kSpanWords = kLB / 64 + 1;
 constexpr int kListCap = kLB / 2;                    // words / spaces / chain entries per span
 constexpr int kHB = 1024;                            // hits per round (reference: <= 1000)
@@ -92,6 +85,9 @@ constexpr int kLdsText = LNG_TEXT;
 #ifndef LNG_PF
 #define LNG_PF 4
 #endif
+#ifndef LNG_REPX
+#define LNG_REPX 1                       // experiments: 2 = read-ahead of two windows in rep_span_lds, 3 = no predictor
+#endif
 
 // Per-wave working set in HBM (one per resident wavefront of the persistent grid).
 struct Slot {
@@ -100,8 +96,6 @@ struct Slot {
   uint64_t pred[kPredictionTableSize];   // Repeats predictor (doc-wide): (epoch << 32) | last char after hash h
   uint64_t pred2[kPredictionTableSize];  // Squeeze / trigger-test predictor (per span), epoch2
   uint64_t lsm[kDocWords];               // letter stops: char start, scanner stops, script != 0
-  uint32_t cls[kClsCap];                 // documents <= kClsCap - 64 bytes: class word per byte (cls_* below)
-  uint32_t low[kClsCap];                 //   and the lowered bytes of the character starting there
   uint64_t spm[kSpanWords];              // spaces of the lowered span (Repeats, Squeeze)
   uint64_t delm[kSpanWords];             // Repeats: delete flags at segment-ending spaces; Squeeze: predicted starts
   uint64_t aux[2][kSpanWords];           // Squeeze: predicted starts of 2/4-byte, 3/4-byte characters
@@ -114,12 +108,14 @@ struct Slot {
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
   uint16_t chain[kListCap];              // quad chain of the span
-  uint16_t b_off[kHB];
+  uint16_t b_off[kHB];                   // hits: base (CJK rounds; quad rounds only for the debug dump)
   uint32_t b_ind[kHB];
-  uint16_t d_off[kHB];
-  uint32_t d_ind[kHB];
+  uint16_t d_off[kHB];                   // delta / distinct emissions (offsets; adds below)
+  uint32_t d_ind[kHB];                   //   (CJK rounds: hits, compacted to emissions in place)
   uint16_t x_off[kHB];
   uint32_t x_ind[kHB];
+  uint16_t d_hoff[kHB];                  // octa rounds' delta / distinct hit offsets (debug dump only)
+  uint16_t x_hoff[kHB];
   uint16_t be_off[kEB];
   uint64_t be_add[kEB];                  // tote adds per emission (tote_adds), base / delta / distinct
   uint64_t d_add[kHB];
@@ -350,43 +346,52 @@ __device__ __forceinline__ void raw_bytes(const DocView& dv, int p, uint32_t d0,
 // formulation; need/conts count the continuation bytes the lead bytes claim /
 // that are present.  Nothing is stored: classify() and the span builder both
 // call this, so the per-wave slot holds no per-byte state.
-template <bool SN2, class Pf>
-__device__ __forceinline__ uint32_t char_props_b(const DevTables& T, const DocView& dv, int p, uint32_t lo, uint32_t hi,
-                                                 uint32_t& lw, int& bad, int& need, int& conts, Pf&& pf) {
+// Property-table indices of the character at p (i1; 0 when it needs the
+// machines or is not a lead byte) and of the next character (i2; -1 when its
+// bytes are not a well-formed 1-3 byte sequence).
+__device__ __forceinline__ void cp_index(const DocView& dv, int p, uint32_t lo, uint32_t hi, int& i1, int& i2) {
   const int L = dv.len;
-  uint32_t b[8];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    b[k] = (lo >> (8 * k)) & 0xFF;
-    b[k + 4] = (hi >> (8 * k)) & 0xFF;
-  }
-  const uint32_t c = b[0];
-  const bool inr = p < L, cont = (c & 0xC0) == 0x80;
-  const int n = utf8_len((uint8_t)c);
-  const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
-  const bool fast = inr && !cont && avail == n && n <= 3;
-  // script of the next character (its bytes are b[n..n+3]; NULs past the end)
-  const uint32_t c2 = n == 1 ? b[1] : n == 2 ? b[2] : n == 3 ? b[3] : b[4];
-  const uint32_t d1 = n == 1 ? b[2] : n == 2 ? b[3] : n == 3 ? b[4] : b[5];
-  const uint32_t d2 = n == 1 ? b[3] : n == 2 ? b[4] : n == 3 ? b[5] : b[6];
+  const uint32_t b0 = lo & 0xFF, b1 = (lo >> 8) & 0xFF, b2 = (lo >> 16) & 0xFF;
+  const int n = utf8_len((uint8_t)b0);
+  const int avail = p + n > L ? L - p : n;
+  const bool fast = p < L && (b0 & 0xC0) != 0x80 && avail == n && n <= 3;
+  i1 = fast ? cpt_index(b0, b1, b2, n) : 0;
+  // the next character's bytes are bytes n..n+3 of lo:hi
+  const uint64_t w = ((uint64_t)hi << 32) | lo;
+  const uint32_t nx = (uint32_t)(w >> (8 * (n < 4 ? n : 4)));
+  const uint32_t c2 = nx & 0xFF, d1 = (nx >> 8) & 0xFF, d2 = (nx >> 16) & 0xFF;
   const int n2 = utf8_len((uint8_t)c2);
-  int i2 = -1;
+  i2 = -1;
   if (c2 < 0x80) i2 = (int)c2;
   else if (n2 == 2 && (c2 & 0xE0) == 0xC0 && (d1 & 0xC0) == 0x80) i2 = cpt_index(c2, d1, 0, 2);
   else if (n2 == 3 && (d1 & 0xC0) == 0x80 && (d2 & 0xC0) == 0x80) i2 = cpt_index(c2, d1, d2, 3);
-  const uint64_t e = T.cpt[fast ? cpt_index(b[0], b[1], b[2], n) : 0];
-  const uint64_t e2 = SN2 ? T.cpt[i2 >= 0 ? i2 : 0] : 0ull;
-  pf();
+}
+// The gathers themselves: e = entry i1, e2 = the low word (script) of entry i2.
+template <bool SN2>
+__device__ __forceinline__ void cp_gather(const DevTables& T, int i1, int i2, uint64_t& e, uint32_t& e2) {
+  e = T.cpt[i1];
+  e2 = SN2 ? reinterpret_cast<const uint32_t*>(T.cpt)[2 * (i2 >= 0 ? i2 : 0)] : 0u;
+}
+// The class word of byte p from its bytes and gathered entries (cls_* above).
+template <bool SN2>
+__device__ __forceinline__ uint32_t cp_decode(const DevTables& T, const DocView& dv, int p, uint32_t lo, uint32_t hi,
+                                              uint64_t e, uint32_t e2, int i2, uint32_t& lw, int& bad, int& need,
+                                              int& conts) {
+  const int L = dv.len;
   lw = 0;
-  if (!inr) return 0u;
-  if (cont) {
+  if (p >= L) return 0u;
+  const uint32_t c = lo & 0xFF;
+  if ((c & 0xC0) == 0x80) {
     ++conts;
     return 0u;
   }
+  const int n = utf8_len((uint8_t)c);
+  const int avail = p + n > L ? L - p : n;   // a final character cut by the document end
+  const bool fast = avail == n && n <= 3;
   bool wf = true;
 #pragma unroll
   for (int k = 1; k < 4; ++k)
-    if (k < avail) wf &= (b[k] & 0xC0) == 0x80;
+    if (k < avail) wf &= ((lo >> (8 * k)) & 0xC0) == 0x80;
   bad |= !wf;
   need += avail - 1;
   int sn, st, olen = 0;
@@ -410,8 +415,21 @@ __device__ __forceinline__ uint32_t char_props_b(const DevTables& T, const DocVi
   if constexpr (SN2) sn2 = i2 >= 0 ? (int)(e2 & 0xFF) : script_num(T, dv, p + n);
   if (st < 0) bad = 1;
   const bool ls = st > 0 && sn != 0;
+  (void)hi;
   return (uint32_t)sn | ((uint32_t)sn2 << 8) | ((uint32_t)n << 16) | (1u << 19) | ((uint32_t)ls << 20) |
          ((uint32_t)(avail < n) << 21) | ((uint32_t)!lowok << 22) | ((uint32_t)olen << 24);
+}
+// All three in one: gathers, then pf() (the caller's read-ahead), then decode.
+template <bool SN2, class Pf>
+__device__ __forceinline__ uint32_t char_props_b(const DevTables& T, const DocView& dv, int p, uint32_t lo, uint32_t hi,
+                                                 uint32_t& lw, int& bad, int& need, int& conts, Pf&& pf) {
+  int i1, i2;
+  cp_index(dv, p, lo, hi, i1, i2);
+  uint64_t e;
+  uint32_t e2;
+  cp_gather<SN2>(T, i1, i2, e, e2);
+  pf();
+  return cp_decode<SN2>(T, dv, p, lo, hi, e, e2, i2, lw, bad, need, conts);
 }
 struct NoPf {
   __device__ __forceinline__ void operator()() const {}
@@ -429,27 +447,35 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // letter-stop bitmap (one bit per byte) the span builder searches for span
 // starts.  False if the document does not tile into characters with local
 // scanner behaviour (then k_general redoes it).
-template <bool ST>
 __device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
   cut = false;
   const int nw = (L + 63) >> 6;
-  uint32_t r0, r1, r2;                           // raw dwords of the next window
+  // software pipeline as in next_span: window w+1's gathers and window w+2's
+  // raw bytes are in flight while window w is decoded
+  uint32_t r0, r1, r2, lo, hi, e2;
+  uint64_t e;
+  int i1, i2;
   raw_load(dv, lane, r0, r1, r2);
+  raw_bytes(dv, lane, r0, r1, r2, lo, hi);
+  cp_index(dv, lane, lo, hi, i1, i2);
+  cp_gather<false>(T, i1, i2, e, e2);
+  raw_load(dv, lane + 64, r0, r1, r2);
   for (int w = 0; w < nw; ++w) {
     const int p = (w << 6) + lane;
-    uint32_t lw, lo, hi;
-    raw_bytes(dv, p, r0, r1, r2, lo, hi);
-    const uint32_t cw = char_props_b<ST>(T, dv, p, lo, hi, lw, bad, need, conts, [&]() {
-      if (w + 1 < nw) raw_load(dv, p + 64, r0, r1, r2);
-    });
-    if constexpr (ST) {
-      if (p < L) {
-        S.cls[p] = cw;
-        S.low[p] = lw;
-      }
-    }
+    uint32_t lw, lo1, hi1, e2n;
+    uint64_t en;
+    int j1, j2;
+    raw_bytes(dv, p + 64, r0, r1, r2, lo1, hi1);
+    cp_index(dv, p + 64, lo1, hi1, j1, j2);
+    cp_gather<false>(T, j1, j2, en, e2n);
+    if (w + 2 < nw) raw_load(dv, p + 128, r0, r1, r2);
+    const uint32_t cw = cp_decode<false>(T, dv, p, lo, hi, e, e2, i2, lw, bad, need, conts);
+    lo = lo1;
+    hi = hi1;
+    e = en;
+    i2 = j2;
     const uint64_t m = __ballot((cw >> 20) & 1);
     if (lane == 0) S.lsm[w] = m;
     cut |= __ballot(cls_cut(cw)) != 0;
@@ -483,7 +509,6 @@ __device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, ui
 // with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
-template <bool ST>
 __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane) {
   const int L = dv.len;
@@ -498,49 +523,47 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     status = 0;
     return 0;
   }
-  int ignore = 0;
-  uint32_t lq;
-  const int ss = ufl(cls_sn(ST ? S.cls[q] : char_props<false>(T, dv, q, lq, ignore, ignore, ignore)));
-  ulscript = ss;
+  int ss = 0;                                    // the span script: read off q's lane in the first window
   if (lane == 0) lb[0] = ' ';
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
-  // stored classes: window w+1's words are loaded while window w is processed;
-  // else window w+1's raw bytes are
-  uint32_t ncw = 0, nlw = 0;
-  uint32_t r0 = 0, r1 = 0, r2 = 0;
-  if constexpr (!ST) raw_load(dv, ((q >> 6) << 6) + lane, r0, r1, r2);
-  if constexpr (ST) {
+  // software pipeline: while window w is processed, window w+1's property
+  // gathers and window w+2's raw bytes are in flight
+  uint32_t r0 = 0, r1 = 0, r2 = 0, lo = 0, hi = 0, e2 = 0;
+  uint64_t e = 0;
+  int i2 = -1;
+  {
     const int x0 = ((q >> 6) << 6) + lane;
-    if (x0 >= q && x0 < L) {
-      ncw = S.cls[x0];
-      nlw = S.low[x0];
-    }
+    raw_load(dv, x0, r0, r1, r2);
+    raw_bytes(dv, x0, r0, r1, r2, lo, hi);
+    int i1;
+    cp_index(dv, x0, lo, hi, i1, i2);
+    cp_gather<true>(T, i1, i2, e, e2);
+    raw_load(dv, x0 + 64, r0, r1, r2);          // (guarded: nothing past the document is read)
   }
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
     uint32_t lw = 0, cw = 0;
-    if constexpr (ST) {
-      cw = ncw;
-      lw = nlw;
-      const int xn = x + 64;
-      ncw = 0;
-      nlw = 0;
-      if (xn < L) {
-        ncw = S.cls[xn];
-        nlw = S.low[xn];
-      }
-    } else {
+    {
+      uint32_t lo1, hi1, e2n;
+      uint64_t en;
+      int j1, j2;
+      raw_bytes(dv, x + 64, r0, r1, r2, lo1, hi1);
+      cp_index(dv, x + 64, lo1, hi1, j1, j2);
+      cp_gather<true>(T, j1, j2, en, e2n);
+      raw_load(dv, x + 128, r0, r1, r2);
       int ignore2 = 0;
-      uint32_t lo, hi;
-      raw_bytes(dv, x, r0, r1, r2, lo, hi);
-      cw = char_props_b<true>(T, dv, x, lo, hi, lw, ignore2, ignore2, ignore2, [&]() {
-        raw_load(dv, x + 64, r0, r1, r2);        // (guarded: nothing past the document is read)
-      });
+      cw = cp_decode<true>(T, dv, x, lo, hi, e, e2, i2, lw, ignore2, ignore2, ignore2);
+      lo = lo1;
+      hi = hi1;
+      e = en;
+      e2 = e2n;
+      i2 = j2;
       if (x < q) {
         cw = 0;
         lw = 0;
       }
+      if (w == (q >> 6)) ss = rdl(cls_sn(cw), q & 63);
     }
     const bool lead = cls_lead(cw);
     const int n = cls_n(cw);
@@ -613,6 +636,7 @@ __device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
   }
   next = nxt;
+  ulscript = ss;
   cutx = (int)wmax((uint32_t)(cutx + 1)) - 1;
   if (cutx >= 0) {                               // the cut last character: lowercaser tail
     int filled = 0;
@@ -840,6 +864,19 @@ __device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len
   int D = 0, WD = 0;                     // dst, word_dst (as offsets)
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
   int carry = 0;
+#if LNG_REPX == 2
+  uint32_t n0 = text[lane], n1 = text[lane + 1], n2 = text[lane + 2];
+  uint32_t m0 = text[lane + 64], m1 = text[lane + 65], m2 = text[lane + 66];
+  for (int w = 0; w < nw; ++w) {
+    const int base = w << 6, x = base + lane;
+    const uint32_t b0 = n0, b1 = n1, b2 = n2;
+    n0 = m0; n1 = m1; n2 = m2;
+    if (w + 2 < nw) {
+      m0 = text[x + 128];
+      m1 = text[x + 129];
+      m2 = text[x + 130];
+    }
+#else
   uint32_t n0 = text[lane], n1 = text[lane + 1], n2 = text[lane + 2];
   for (int w = 0; w < nw; ++w) {
     const int base = w << 6, x = base + lane;
@@ -849,6 +886,7 @@ __device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len
       n1 = text[x + 65];
       n2 = text[x + 66];
     }
+#endif
     const bool valid = x < len;
     // (well-formed text: the starts come from the bytes already in registers)
     const uint64_t st = careful ? char_starts(text, base, len, nullptr, carry, careful, lane)
@@ -865,7 +903,12 @@ __device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len
       code = pred_code(b0, b1, b2, incr);
     }
     const uint64_t lm = __ballot(lead);
+#if LNG_REPX == 3
+    const bool pr = false;
+    hcarry = 0;
+#else
     const bool pr = lm ? predict_window_lds(tbl, ovf, lm, c, code, hcarry, lane) : false;
+#endif
     const int wl = lead ? incr : 0, gd = (lead && pr) ? incr : 0;
     const bool sp = lead && b0 == ' ';
     const uint64_t spm = __ballot(sp);
@@ -1142,6 +1185,32 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
   return dst;
 }
 
+// The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
+__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? t.adds[i] : 0ull; }
+
+// Base emissions of one base hit (LinearizeAll, scoreonescriptspan.cc:856-960):
+// one or two langprobs as tote adds, zero langprobs dropped.  ind bit 31
+// selects the second quad table.
+__device__ __forceinline__ void base_adds(const DevTbl& t1, const DevTbl& t2, uint32_t ind, uint64_t& l1, uint64_t& l2) {
+  const DevTbl* lb = &t1;
+  if (ind & 0x80000000u) {
+    lb = &t2;
+    ind &= ~0x80000000u;
+  }
+  l2 = 0;
+  if (ind < lb->size_one) {
+    l1 = adds_at(*lb, ind);
+  } else {
+    ind += ind - lb->size_one;
+    l1 = adds_at(*lb, ind);
+    l2 = adds_at(*lb, ind + 1);
+    if (!(l1 >> 63)) {
+      l1 = l2;
+      l2 = 0;
+    }
+  }
+}
+
 // ---------------------------------------------------- quad chain of a span
 // GetQuadHits' chain (cldutil.cc:349-401): from src, e = 4 chars on (stopping
 // at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
@@ -1210,10 +1279,15 @@ __device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S,
 
 // GetQuadHits for one round from chain entry c0 (cldutil.cc:315-405): probes
 // per entry, the "not one of the last two hits" filter, the 1000-hit cut.
-// Returns the round end (the reference's `next`); c0 advances.
+// Each kept hit's base emissions go straight to be_off / be_add (eb of
+// them), so score_round does not read the hits back; the hit list itself is
+// kept only for the debug dump (D).  Returns the round end (the reference's
+// `next`); c0 advances.
+template <bool D>
 __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int nch, int& c0, int& nb,
-                          int lane) {
+                          int& eb, int lane) {
   nb = 0;
+  eb = 0;
   uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
   int pn = (LNG_PF & 2) && c0 + lane < nch ? S.chain[c0 + lane] : 0;   // chain entries one block ahead
   for (int i0 = c0; i0 < nch; i0 += 64) {
@@ -1281,12 +1355,28 @@ __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* tex
       lastl = nth_bit(keep, kMaxScoringHits - nb - 1);
       keep &= mask_le(lastl);
     }
-    if ((keep >> lane) & 1) {
+    const bool kept = (keep >> lane) & 1;
+    if (D && kept) {
       const int k = nb + __popcll(keep & lanemask_lt(lane));
       S.b_off[k] = (uint16_t)p;
       S.b_ind[k] = ind;
     }
     nb += __popcll(keep);
+    {
+      uint64_t l1 = 0, l2 = 0;
+      if (kept) base_adds(T.quad, T.quad2, ind, l1, l2);
+      const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
+      const int o = eb + excl_scan(c, lane);
+      eb = rdl(o + c, 63);
+      if (l1 >> 63) {
+        S.be_off[o] = (uint16_t)p;
+        S.be_add[o] = l1;
+      }
+      if (l2 >> 63) {
+        S.be_off[o + 1] = (uint16_t)p;
+        S.be_add[o + 1] = l2;
+      }
+    }
     if (lastl < 64) {
       c0 = i0 + lastl + 1;
       gsync();
@@ -1302,9 +1392,15 @@ __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* tex
 
 // GetOctaHits (cldutil.cc:416-533) over [off, next]: one lane per word (words
 // end at the spaces in [start, next]); the two-word repeat filter updates the
-// pair partner even when the probes miss; caps: 1000 delta / 999 distinct.
+// pair partner even when the probes miss; caps: 1000 delta / 999 distinct
+// hits.  As in quad_round, the hits become emissions here (ed delta / ex
+// distinct with non-zero langprobs, in hit order); the hit lists are kept
+// only for the debug dump (D).
+template <bool D>
 __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int nsp, int& j0, int off, int next,
-                           int& nd, int& nx, int lane) {
+                           int& nd, int& nx, int& edm, int& exm, int lane) {
+  edm = 0;
+  exm = 0;
   const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
   const int lim = next + 1;
   nd = 0;
@@ -1377,24 +1473,50 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
       xp = octa_lookup(T.distinctocta, wh);
       dp = octa_lookup(T.deltaocta, wh);
     }
+    // tote adds of the hits (issued before the cap arithmetic they do not depend on)
+    const uint32_t xm = ~T.distinctocta.key_mask, dmk = ~T.deltaocta.key_mask;
+    const uint64_t apx = pp ? adds_at(T.distinctocta, pp & xm) : 0ull;
+    const uint64_t axp = xp ? adds_at(T.distinctocta, xp & xm) : 0ull;
+    const uint64_t adp = dp ? adds_at(T.deltaocta, dp & dmk) : 0ull;
     const int cx = (pp != 0) + (xp != 0), cd = (dp != 0);
     const int ex = excl_scan(cx, lane), ed = excl_scan(cd, lane);
     const uint64_t capm = __ballot(v && (nx + ex + cx >= kMaxScoringHits - 1 || nd + ed + cd >= kMaxScoringHits));
     const int cut = capm ? __builtin_ctzll(capm) : 64;
-    if (lane <= cut) {
+    {
+      const bool in = lane <= cut;
+      const int mx = in ? (int)(apx >> 63) + (int)(axp >> 63) : 0, md = in ? (int)(adp >> 63) : 0;
+      int ox = exm + excl_scan(mx, lane);
+      const int od = edm + excl_scan(md, lane);
+      exm = rdl(ox + mx, 63);
+      edm = rdl(od + md, 63);
+      if (in && (apx >> 63)) {
+        S.x_off[ox] = (uint16_t)pws;
+        S.x_add[ox] = apx;
+        ++ox;
+      }
+      if (in && (axp >> 63)) {
+        S.x_off[ox] = (uint16_t)a;
+        S.x_add[ox] = axp;
+      }
+      if (in && (adp >> 63)) {
+        S.d_off[od] = (uint16_t)a;
+        S.d_add[od] = adp;
+      }
+    }
+    if (D && lane <= cut) {
       int o = nx + ex;
       if (pp) {
-        S.x_off[o] = (uint16_t)pws;
-        S.x_ind[o] = pp & ~T.distinctocta.key_mask;
+        S.x_hoff[o] = (uint16_t)pws;
+        S.x_ind[o] = pp & xm;
         ++o;
       }
       if (xp) {
-        S.x_off[o] = (uint16_t)a;
-        S.x_ind[o] = xp & ~T.distinctocta.key_mask;
+        S.x_hoff[o] = (uint16_t)a;
+        S.x_ind[o] = xp & xm;
       }
       if (dp) {
-        S.d_off[nd + ed] = (uint16_t)a;
-        S.d_ind[nd + ed] = dp & ~T.deltaocta.key_mask;
+        S.d_hoff[nd + ed] = (uint16_t)a;
+        S.d_ind[nd + ed] = dp & dmk;
       }
     }
     const int lastl = cut < 64 ? cut : 63;
@@ -1495,8 +1617,6 @@ __device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
          ((uint64_t)((e >> 16) & 0xFF) << 24) | ((uint64_t)(lp >> 24) << 32) | ((uint64_t)(e >> 24) << 40);
 }
 
-// The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
-__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? t.adds[i] : 0ull; }
 
 // Per (script, key): language | close set << 16 | expected score << 32
 // (FromPerScriptNumber, close sets, kAvgDeltaOctaScore: lang_script.cc:328-341,
@@ -1522,7 +1642,11 @@ __device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
 // range of each stream.
 template <bool D>
 __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
-                            int lowest, int dummy_off, int lane) {
+                            int lowest, int dummy_off, int lane, int feb = -1, int fed = 0, int fex = 0) {
+  // feb >= 0: the emissions were made by quad_round / octa_round (feb base,
+  // fed delta, fex distinct); else (CJK rounds) they are made here from the hits
+  const bool fused = feb >= 0;
+  const int hb = fused ? 0 : nb, hd = fused ? 0 : nd, hx = fused ? 0 : nx;
   const DevTbl& bo = cjk ? T.compat : T.quad;
   const DevTbl& bo2 = cjk ? T.compat : T.quad2;
   const DevTbl& dob = cjk ? T.deltabi : T.deltaocta;
@@ -1535,19 +1659,19 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   // block's table gathers)
   int eb = 0;
   const bool pf = LNG_PF & 8;
-  int noff = pf && lane < nb ? S.b_off[lane] : 0;
-  uint32_t nind = pf && lane < nb ? S.b_ind[lane] : 0u;
-  for (int j0 = 0; j0 < nb; j0 += 64) {
+  int noff = pf && lane < hb ? S.b_off[lane] : 0;
+  uint32_t nind = pf && lane < hb ? S.b_ind[lane] : 0u;
+  for (int j0 = 0; j0 < hb; j0 += 64) {
     const int j = j0 + lane;
     uint64_t l1 = 0, l2 = 0;                // tote adds (bit 63: non-zero langprob)
     int off = 0;
-    const int coff = pf ? noff : (j < nb ? S.b_off[j] : 0);
-    const uint32_t cind = pf ? nind : (j < nb ? S.b_ind[j] : 0u);
+    const int coff = pf ? noff : (j < hb ? S.b_off[j] : 0);
+    const uint32_t cind = pf ? nind : (j < hb ? S.b_ind[j] : 0u);
     if (pf) {
-      noff = j + 64 < nb ? S.b_off[j + 64] : 0;
-      nind = j + 64 < nb ? S.b_ind[j + 64] : 0u;
+      noff = j + 64 < hb ? S.b_off[j + 64] : 0;
+      nind = j + 64 < hb ? S.b_ind[j + 64] : 0u;
     }
-    if (j < nb) {
+    if (j < hb) {
       off = coff;
       uint32_t ind = cind;
       const DevTbl* lb = &bo;
@@ -1582,17 +1706,17 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   if constexpr (D) mark_sub(s, lane, 0, t2);
   // delta / distinct emissions, compacted in place (ind -> langprob)
   int ed = 0, ex = 0;
-  uint32_t dni = pf && lane < nd ? S.d_ind[lane] : 0u;
-  uint16_t dno = pf && lane < nd ? S.d_off[lane] : (uint16_t)0;
-  for (int j0 = 0; j0 < nd; j0 += 64) {
+  uint32_t dni = pf && lane < hd ? S.d_ind[lane] : 0u;
+  uint16_t dno = pf && lane < hd ? S.d_off[lane] : (uint16_t)0;
+  for (int j0 = 0; j0 < hd; j0 += 64) {
     const int j = j0 + lane;
-    const uint32_t ci = pf ? dni : (j < nd ? S.d_ind[j] : 0u);
-    const uint16_t off = pf ? dno : (j < nd ? S.d_off[j] : (uint16_t)0);
+    const uint32_t ci = pf ? dni : (j < hd ? S.d_ind[j] : 0u);
+    const uint16_t off = pf ? dno : (j < hd ? S.d_off[j] : (uint16_t)0);
     if (pf) {
-      dni = j + 64 < nd ? S.d_ind[j + 64] : 0u;
-      dno = j + 64 < nd ? S.d_off[j + 64] : (uint16_t)0;
+      dni = j + 64 < hd ? S.d_ind[j + 64] : 0u;
+      dno = j + 64 < hd ? S.d_off[j + 64] : (uint16_t)0;
     }
-    const uint64_t a = j < nd ? adds_at(dob, ci) : 0ull;
+    const uint64_t a = j < hd ? adds_at(dob, ci) : 0ull;
     const int nz = (int)(a >> 63);
     const int o = ed + excl_scan(nz, lane);
     ed = rdl(o + nz, 63);
@@ -1601,17 +1725,17 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       S.d_add[o] = a;
     }
   }
-  uint32_t xni = pf && lane < nx ? S.x_ind[lane] : 0u;
-  uint16_t xno = pf && lane < nx ? S.x_off[lane] : (uint16_t)0;
-  for (int j0 = 0; j0 < nx; j0 += 64) {
+  uint32_t xni = pf && lane < hx ? S.x_ind[lane] : 0u;
+  uint16_t xno = pf && lane < hx ? S.x_off[lane] : (uint16_t)0;
+  for (int j0 = 0; j0 < hx; j0 += 64) {
     const int j = j0 + lane;
-    const uint32_t ci = pf ? xni : (j < nx ? S.x_ind[j] : 0u);
-    const uint16_t off = pf ? xno : (j < nx ? S.x_off[j] : (uint16_t)0);
+    const uint32_t ci = pf ? xni : (j < hx ? S.x_ind[j] : 0u);
+    const uint16_t off = pf ? xno : (j < hx ? S.x_off[j] : (uint16_t)0);
     if (pf) {
-      xni = j + 64 < nx ? S.x_ind[j + 64] : 0u;
-      xno = j + 64 < nx ? S.x_off[j + 64] : (uint16_t)0;
+      xni = j + 64 < hx ? S.x_ind[j + 64] : 0u;
+      xno = j + 64 < hx ? S.x_off[j + 64] : (uint16_t)0;
     }
-    const uint64_t a = j < nx ? adds_at(xob, ci) : 0ull;
+    const uint64_t a = j < hx ? adds_at(xob, ci) : 0ull;
     const int nz = (int)(a >> 63);
     const int o = ex + excl_scan(nz, lane);
     ex = rdl(o + nz, 63);
@@ -1621,6 +1745,11 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     }
   }
   if constexpr (D) mark_sub(s, lane, 1, t2);
+  if (fused) {
+    eb = feb;
+    ed = fed;
+    ex = fex;
+  }
   // chunk plan from the base-hit count (ChunkAll :978-1031)
   int K = 0;
   if (nb <= 0) {
@@ -1844,16 +1973,16 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   if constexpr (D) mark_sub(s, lane, 4, t2);
 }
 
-__device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, int lane) {
+__device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, bool octa, int lane) {
   if (!s.dbg) return;
   const uint32_t h[6] = {'R', (uint32_t)off, (uint32_t)next, (uint32_t)nb, (uint32_t)nd, (uint32_t)nx};
   dbg_words(s, lane, h, 6);
   uint32_t* o = s.dbg + 1 + s.dbg_pos;
   for (int i = lane; i < nb; i += 64) { o[2 * i] = S.b_off[i]; o[2 * i + 1] = S.b_ind[i]; }
   o += 2 * nb;
-  for (int i = lane; i < nd; i += 64) { o[2 * i] = S.d_off[i]; o[2 * i + 1] = S.d_ind[i]; }
+  for (int i = lane; i < nd; i += 64) { o[2 * i] = octa ? S.d_hoff[i] : S.d_off[i]; o[2 * i + 1] = S.d_ind[i]; }
   o += 2 * nd;
-  for (int i = lane; i < nx; i += 64) { o[2 * i] = S.x_off[i]; o[2 * i + 1] = S.x_ind[i]; }
+  for (int i = lane; i < nx; i += 64) { o[2 * i] = octa ? S.x_hoff[i] : S.x_off[i]; o[2 * i + 1] = S.x_ind[i]; }
   wave::wsync();
   if (lane == 0) {
     s.dbg_pos += 2 * (nb + nd + nx);
@@ -1882,7 +2011,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
       if constexpr (D) trace(tr, lane, doc, 20, off);
       const int next = cjk_round(T, text, tb, S, off, nb, nd, nx, lane);
       if constexpr (D) trace(tr, lane, doc, 21, next);
-      if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, lane);
+      if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, false, lane);
       if constexpr (D) mark(s, lane, 6, t);
       score_round<D>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane);
       if constexpr (D) mark(s, lane, 7, t);
@@ -1902,14 +2031,15 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
   while (off < tb) {
     int nb, nd, nx;
     if constexpr (D) trace(tr, lane, doc, 12, off);
-    const int next = quad_round(T, text, tb, S, nch, c0, nb, lane);
+    int eb, edm, exm;
+    const int next = quad_round<D>(T, text, tb, S, nch, c0, nb, eb, lane);
     if constexpr (D) trace(tr, lane, doc, 13, next);
     if constexpr (D) mark(s, lane, 5, t);
-    octa_round(T, text, S, nsp, j0, off, next, nd, nx, lane);
+    octa_round<D>(T, text, S, nsp, j0, off, next, nd, nx, edm, exm, lane);
     if constexpr (D) trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
-    if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, lane);
+    if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
     if constexpr (D) mark(s, lane, 6, t);
-    score_round<D>(T, S, s, ulscript, false, nb, nd, nx, off, next, lane);
+    score_round<D>(T, S, s, ulscript, false, nb, nd, nx, off, next, lane, eb, edm, exm);
     if constexpr (D) mark(s, lane, 7, t);
     off = next;
   }
@@ -1937,9 +2067,9 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
   const DocView dv{g, L};
   if constexpr (D) trace(tr, lane, doc, 1, L);
   long long t = (D && s.prof) ? (long long)clock64() : 0;
-  const bool stored = L <= kClsCap - 64;
+
   bool careful;                                  // a cut last character: span text may be malformed
-  if (!(stored ? classify<true>(T, dv, S, careful, lane) : classify<false>(T, dv, S, careful, lane)))
+  if (!classify(T, dv, S, careful, lane))
     return -kWhyClassify;
   if constexpr (D) mark(s, lane, 0, t);
   if constexpr (D) trace(tr, lane, doc, 2, 0);
@@ -1991,8 +2121,7 @@ __device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem
         const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
-        tb = stored ? next_span<true>(T, dv, S, lb, next, ul, st, lane)
-                    : next_span<false>(T, dv, S, lb, next, ul, st, lane);
+        tb = next_span(T, dv, S, lb, next, ul, st, lane);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {

@@ -990,19 +990,21 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     gm = wor64(gm);
     const int score_count = wsum(cnt);
     wsync();
-    // top three keys of the in-use groups: (score desc, key asc)
+    // top keys of the in-use groups: (score desc, key asc).  The reference
+    // sorts three (CurrentTopThreeKeys) but SetChunkSummary reads only the
+    // first two (scoreonescriptspan.cc:60-96), so two rounds.
     const uint2 v2 = reinterpret_cast<const uint2*>(s.tote)[lane];
     const bool inuse = (gm >> lane) & 1;
     uint32_t cand[4] = {v2.x & 0xFFFF, v2.x >> 16, v2.y & 0xFFFF, v2.y >> 16};
-    int key3[3] = {-1, -1, -1};
-    uint32_t sc3[3] = {0, 0, 0};
+    int key3[2] = {-1, -1};
+    uint32_t sc3[2] = {0, 0};
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 2; ++r) {
       uint32_t best = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = lane * 4 + i;
-        const bool taken = key == key3[0] || key == key3[1];
+        const bool taken = key == key3[0];
         const uint32_t comp = (inuse && !taken) ? ((cand[i] + 1) << 8) | (uint32_t)(255 - key) : 0u;
         best = comp > best ? comp : best;
       }
