@@ -85,6 +85,14 @@ constexpr int kLdsText = LNG_TEXT;
 #ifndef LNG_PF
 #define LNG_PF 4
 #endif
+// Inlining of the two largest stages (A/B: a call keeps the caller's
+// registers free, inlining lets the slot / LDS accesses stay global / ds).
+#ifndef LNG_SR_INL
+#define LNG_SR_INL __device__ __forceinline__
+#endif
+#ifndef LNG_NS_INL
+#define LNG_NS_INL __device__ __forceinline__
+#endif
 #ifndef LNG_REPX
 #define LNG_REPX 1                       // experiments: 2 = read-ahead of two windows in rep_span_lds, 3 = no predictor
 #endif
@@ -318,9 +326,9 @@ __device__ __noinline__ uint64_t char_slow(DevSM script, DevSM scan, DevSM lower
 __device__ __forceinline__ void raw_load(const DocView& dv, int p, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
   const uintptr_t a = (uintptr_t)(dv.p + p) & ~(uintptr_t)3, end = (uintptr_t)(dv.p + dv.len);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(a);
-  d0 = a < end ? q[0] : 0u;
-  d1 = a + 4 < end ? q[1] : 0u;
-  d2 = a + 8 < end ? q[2] : 0u;
+  d0 = a < end ? gld(q) : 0u;              // (the document is always in global memory)
+  d1 = a + 4 < end ? gld(q + 1) : 0u;
+  d2 = a + 8 < end ? gld(q + 2) : 0u;
 }
 __device__ __forceinline__ void raw_bytes(const DocView& dv, int p, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t& lo,
                                           uint32_t& hi) {
@@ -369,8 +377,8 @@ __device__ __forceinline__ void cp_index(const DocView& dv, int p, uint32_t lo, 
 // The gathers themselves: e = entry i1, e2 = the low word (script) of entry i2.
 template <bool SN2>
 __device__ __forceinline__ void cp_gather(const DevTables& T, int i1, int i2, uint64_t& e, uint32_t& e2) {
-  e = T.cpt[i1];
-  e2 = SN2 ? reinterpret_cast<const uint32_t*>(T.cpt)[2 * (i2 >= 0 ? i2 : 0)] : 0u;
+  e = gld(T.cpt + (i1));
+  e2 = SN2 ? gld(reinterpret_cast<const uint32_t*>(T.cpt) + 2 * (i2 >= 0 ? i2 : 0)) : 0u;
 }
 // The class word of byte p from its bytes and gathered entries (cls_* above).
 template <bool SN2>
@@ -447,7 +455,7 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // letter-stop bitmap (one bit per byte) the span builder searches for span
 // starts.  False if the document does not tile into characters with local
 // scanner behaviour (then k_general redoes it).
-__device__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
+__device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
   cut = false;
@@ -509,7 +517,7 @@ __device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, ui
 // with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
-__device__ int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
+LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane) {
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
@@ -858,7 +866,7 @@ __device__ __forceinline__ bool predict_window_lds(uint16_t* tbl, uint64_t* ovf,
 // the window end are written at their dst positions (<= their source
 // positions, so in place is safe).  The next window's bytes are loaded while
 // the current one is processed.  hcarry carries from span to span.
-__device__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len, uint32_t& hcarry, bool careful,
+__device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len, uint32_t& hcarry, bool careful,
                             bool& ok, int lane) {
   const int nw = (len + 63) >> 6;
   int D = 0, WD = 0;                     // dst, word_dst (as offsets)
@@ -1186,7 +1194,7 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
 }
 
 // The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
-__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? t.adds[i] : 0ull; }
+__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? gld(t.adds + i) : 0ull; }
 
 // Base emissions of one base hit (LinearizeAll, scoreonescriptspan.cc:856-960):
 // one or two langprobs as tote adds, zero langprobs dropped.  ind bit 31
@@ -1612,7 +1620,7 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
 // (key, score) tote adds of a langprob, packed k1 | s1 << 8 | k2 << 16 |
 // s2 << 24 | k3 << 32 | s3 << 40 (bytes 5..7 of its kLgProbV2Tbl row).
 __device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
-  const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
+  const uint32_t e = gld(reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4));
   return (uint64_t)((lp >> 8) & 0xFF) | ((uint64_t)((e >> 8) & 0xFF) << 8) | ((uint64_t)((lp >> 16) & 0xFF) << 16) |
          ((uint64_t)((e >> 16) & 0xFF) << 24) | ((uint64_t)(lp >> 24) << 32) | ((uint64_t)(e >> 24) << 40);
 }
@@ -1626,8 +1634,38 @@ __device__ __forceinline__ uint64_t tote_adds(const DevTables& T, uint32_t lp) {
 __device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
   const int lang = from_per_script_number(T, ulscript, (uint8_t)k);
   const int esub = lang * 4 + lscript4(T, ulscript);
-  const int16_t ex = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : (int16_t)0;
+  const int16_t ex = (esub >= 0 && (uint32_t)esub < T.n_expected) ? gld(T.expected + (esub)) : (int16_t)0;
   return (uint64_t)(uint16_t)lang | ((uint64_t)close_set(T, lang) << 16) | ((uint64_t)(uint16_t)ex << 32);
+}
+
+// Chunk k's adds (score_round): t < seedn the seed, then its base, delta and
+// distinct emissions, then the four boosts (the last four distinct langprobs
+// so far).  Plain functions rather than lambdas: a captured reference loses
+// its address space, and the slot / LDS reads would become FLAT.
+__device__ __forceinline__ uint64_t chunk_add(const Slot& S, const Smem& s, uint64_t seed, int rs, int t, int k, int tot,
+                                              int bs, int nB, int ds, int nD, int xs, int nX, int xe) {
+  if (t >= tot) return 0ull;
+  int u = t;
+  const int seedn = k == 0 ? 1 : 0;
+  if (u < seedn) return seed;
+  if ((u -= seedn) < nB) return S.be_add[bs + u];
+  if ((u -= nB) < nD) return S.d_add[ds + u];
+  if ((u -= nD) < nX) return S.x_add[xs + u];
+  const int v = xe - kMaxBoosts + (u - nX);
+  return v < 0 ? s.ring[rs][v + kMaxBoosts] : gld(&S.x_add[v]);   // (gld: no LDS/global pointer select)
+}
+// Chunk plan of k: emission ranges and the number of adds.
+__device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
+                                          int& xs, int& nX, int& xe) {
+  bs = s.bst[k];
+  const int be = k == K - 1 ? eb : s.bst[k + 1];
+  ds = s.st[0][k];
+  xs = s.st[1][k];
+  xe = s.st[1][k + 1];
+  nB = be - bs;
+  nD = s.st[0][k + 1] - ds;
+  nX = xe - xs;
+  return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts;
 }
 
 // ------------------------------------- linearize + chunk + score (one round)
@@ -1641,7 +1679,7 @@ __device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
 // o <= theta_k = be_off[E_k - 2].  Every chunk is therefore one contiguous
 // range of each stream.
 template <bool D>
-__device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
+LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int lowest, int dummy_off, int lane, int feb = -1, int fed = 0, int fex = 0) {
   // feb >= 0: the emissions were made by quad_round / octa_round (feb base,
   // fed delta, fex distinct); else (CJK rounds) they are made here from the hits
@@ -1830,49 +1868,24 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
-  // chunk k's adds: t < seedn the seed, then its base, delta and distinct
-  // emissions, then the four boosts (the last four distinct langprobs so far)
-  auto fetch = [&](int t, int k, int tot, int bs, int nB, int ds, int nD, int xs, int nX, int xe) -> uint64_t {
-    if (t >= tot) return 0ull;
-    int u = t;
-    const int seedn = k == 0 ? 1 : 0;
-    if (u < seedn) return seed;
-    if ((u -= seedn) < nB) return S.be_add[bs + u];
-    if ((u -= nB) < nD) return S.d_add[ds + u];
-    if ((u -= nD) < nX) return S.x_add[xs + u];
-    const int v = xe - kMaxBoosts + (u - nX);
-    return v < 0 ? s.ring[rs][v + kMaxBoosts] : S.x_add[v];
-  };
-  // chunk plan of k: emission ranges and the number of adds
-  auto plan = [&](int k, int& bs, int& nB, int& ds, int& nD, int& xs, int& nX, int& xe) -> int {
-    bs = s.bst[k];
-    const int be = k == K - 1 ? eb : s.bst[k + 1];
-    ds = s.st[0][k];
-    xs = s.st[1][k];
-    xe = s.st[1][k + 1];
-    nB = be - bs;
-    nD = s.st[0][k + 1] - ds;
-    nX = xe - xs;
-    return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts;
-  };
   // the first 128 adds of chunk k + 1 are loaded while chunk k is scored
   int pbs, pnB, pds, pnD, pxs, pnX, pxe;
-  int ptot = plan(0, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-  uint64_t n0 = fetch(lane, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-  uint64_t n1 = fetch(lane + 64, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  int ptot = chunk_plan(s, K, eb, 0, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  uint64_t n0 = chunk_add(S, s, seed, rs, lane, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  uint64_t n1 = chunk_add(S, s, seed, rs, lane + 64, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
   for (int k = 0; k < K; ++k) {
     const int bs = pbs, nB = pnB, ds = pds, nD = pnD, xs = pxs, nX = pnX, xe = pxe, tot = ptot;
     const uint64_t a0 = n0, a1 = n1;
     if (k + 1 < K) {
-      ptot = plan(k + 1, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-      n0 = fetch(lane, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-      n1 = fetch(lane + 64, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      ptot = chunk_plan(s, K, eb, k + 1, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      n0 = chunk_add(S, s, seed, rs, lane, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      n1 = chunk_add(S, s, seed, rs, lane + 64, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
     }
     reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
     wsync();
     const int seedn = k == 0 ? 1 : 0;
     for (int t = lane; t < tot; t += 64) {
-      const uint64_t a = t < 128 ? (t < 64 ? a0 : a1) : fetch(t, k, tot, bs, nB, ds, nD, xs, nX, xe);
+      const uint64_t a = t < 128 ? (t < 64 ? a0 : a1) : chunk_add(S, s, seed, rs, t, k, tot, bs, nB, ds, nD, xs, nX, xe);
       const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
       // the low half sums the score (read with the reference's uint16 wrap), the
       // high half counts the adds: a group (the 4 keys of one lane) is in use
@@ -1926,7 +1939,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     hi = dummy_off;
     if (lane + 1 < K && s.lo[lane + 1] != kInf) hi = (int)s.lo[lane + 1];
     const uint64_t* kt = T.keytab + 256 * (uint32_t)ulscript;
-    const uint64_t i1 = kt[(uint8_t)ck1], i2 = kt[(uint8_t)ck2];
+    const uint64_t i1 = gld(kt + (uint8_t)ck1), i2 = gld(kt + (uint8_t)ck2);
     lang1 = (int)(i1 & 0xFFFF); lang2 = (int)(i2 & 0xFFFF);
     const int len = hi - lo;
     int actual = 0;
@@ -1965,7 +1978,7 @@ __device__ void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     uint64_t r4[4];
     for (int i = 0; i < 4; ++i) {
       const int u = ex - kMaxBoosts + i;
-      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : S.x_add[u];
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : gld(&S.x_add[u]);
     }
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
@@ -2051,7 +2064,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
 // Returns the number of passes, or -reason (kWhy*) to re-queue.
 enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
 template <bool D>
-__device__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
+__device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc) {
   const int unk = (int)T.unknown_lang;
   if (L == 0) {

@@ -68,12 +68,27 @@ struct DocView {
   __device__ __forceinline__ uint8_t at(int i) const { return (unsigned)i < (unsigned)len ? p[i] : 0; }
 };
 
+// Loads from the table set (and the k_long slot) through pointers the compiler
+// cannot prove global -- the pointers held in DevTables, a reference captured
+// by a lambda.  A plain dereference becomes a FLAT load, which also counts
+// against LGKM, so every later LDS or scalar wait would wait for the gather
+// too.  Only for memory that is always global (never a private or LDS copy).
+template <class V>
+__device__ __forceinline__ V gld(const V* p) {
+  return *(const __attribute__((address_space(1))) V*)p;
+}
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld4(const uint32_t* p) {      // one 16-byte load (p 16-byte aligned)
+  const u32x4_t v = gld(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // ---------------------------------------------------------- state machines
 __device__ __forceinline__ uint32_t sm16(const DevSM& sm, int64_t i) {
-  return (i < 0 || i >= (int64_t)sm.total) ? 0u : (uint32_t)sm.t16[i];
+  return (i < 0 || i >= (int64_t)sm.total) ? 0u : (uint32_t)gld(sm.t16 + i);
 }
 __device__ __forceinline__ int32_t sm8(const DevSM& sm, int64_t i) {
-  return (i < 0 || i >= (int64_t)sm.total) ? 0 : (int32_t)sm.t8[i];
+  return (i < 0 || i >= (int64_t)sm.total) ? 0 : (int32_t)gld(sm.t8 + i);
 }
 
 // GetUTF8LetterScriptNum -> UTF8GenericPropertyTwoByte
@@ -319,27 +334,27 @@ __device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* 
 // ------------------------------------------------------------ lang/script
 __device__ __forceinline__ int rtype_of(const DevTables& T, int s) {        // lang_script.cc:154-160
   if (s < 0 || (uint32_t)s >= T.n_scripts) s = 0;
-  return T.rtype[s];
+  return gld(T.rtype + (s));
 }
 __device__ __forceinline__ int default_language(const DevTables& T, int s) { // :314-318
   if (s < 0 || (uint32_t)s >= T.n_scripts) return (int)T.unknown_lang;
-  return T.deflang[s];
+  return gld(T.deflang + (s));
 }
 __device__ __forceinline__ uint32_t per_script_number_latin(const DevTables& T, int lang) { // :320-326
-  if (T.rtype[T.latin] == RTypeNone) return 1;
+  if (gld(T.rtype + (T.latin)) == RTypeNone) return 1;
   if (lang < 0 || (uint32_t)lang >= T.l2p_size) return 0;
-  return T.l2p[lang];
+  return gld(T.l2p + (lang));
 }
 __device__ __forceinline__ int from_per_script_number(const DevTables& T, int s, uint8_t ps) { // :328-341
   if (s < 0 || (uint32_t)s >= T.n_scripts) return (int)T.unknown_lang;
-  int rt = T.rtype[s];
-  if (rt == RTypeNone || rt == RTypeOne) return T.deflang[s];
-  if ((uint32_t)s == T.latin) return T.p2l_latn[ps];
-  return T.p2l_othr[ps];
+  int rt = gld(T.rtype + (s));
+  if (rt == RTypeNone || rt == RTypeOne) return gld(T.deflang + (s));
+  if ((uint32_t)s == T.latin) return gld(T.p2l_latn + (ps));
+  return gld(T.p2l_othr + (ps));
 }
 __device__ __forceinline__ int close_set(const DevTables& T, int lang) {      // :261-310
   if (lang < 0 || (uint32_t)lang >= T.n_langs) return 0;
-  return T.close_set[lang];
+  return gld(T.close_set + (lang));
 }
 __device__ __forceinline__ int lscript4(const DevTables& T, int s) {          // :552-557
   return (uint32_t)s == T.latin ? 0 : (uint32_t)s == T.cyrillic ? 1 : (uint32_t)s == T.arabic ? 2 : 3;
@@ -418,7 +433,7 @@ __device__ __forceinline__ uint64_t pair_hash(uint64_t a, uint64_t b) {   // cld
 // bucket gather, first of four slots whose masked key matches.
 __device__ __forceinline__ uint32_t lookup4(const DevTbl& t, uint32_t sub, uint32_t key) {
   if (t.n_buckets == 0) return 0;
-  const uint4 b = *reinterpret_cast<const uint4*>(t.b + 4 * (size_t)sub);
+  const uint4 b = gld4(t.b + 4 * (size_t)sub);
   if (((key ^ b.x) & t.key_mask) == 0) return b.x;
   if (((key ^ b.y) & t.key_mask) == 0) return b.y;
   if (((key ^ b.z) & t.key_mask) == 0) return b.z;
@@ -432,7 +447,7 @@ __device__ __forceinline__ uint32_t octa_lookup(const DevTbl& t, uint64_t h) {
   uint32_t sub = (uint32_t)((h + (h >> 12)) & (uint64_t)(t.size - 1));
   return lookup4(t, sub, (uint32_t)(h >> 4) & t.key_mask);
 }
-__device__ __forceinline__ uint32_t ind_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? t.ind[i] : 0u; }
+__device__ __forceinline__ uint32_t ind_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? gld(t.ind + i) : 0u; }
 
 // ------------------------------------------------------------------ totes
 struct Tote {                                                 // tote.h:33-61
@@ -1480,7 +1495,7 @@ __device__ ChunkSum chunk_summary(const DevTables& T, int ulscript, int lo, int 
   int actual = 0;
   if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
   int esub = lang1 * 4 + lscript4(T, ulscript);
-  int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+  int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? gld(T.expected + (esub)) : 0;
   ChunkSum cs;
   cs.offset = (uint16_t)lo;
   cs.chunk_start = (uint16_t)first_linear;
@@ -1517,9 +1532,9 @@ __device__ int get_lang_score(const DevTables& T, uint32_t lp, uint8_t pslang) {
 }
 __device__ uint8_t per_script_number(const DevTables& T, int ulscript, int lang) {  // lang_script.cc:320-326
   if (ulscript < 0 || (uint32_t)ulscript >= T.n_scripts) return 0;
-  if (T.rtype[ulscript] == RTypeNone) return 1;
+  if (gld(T.rtype + (ulscript)) == RTypeNone) return 1;
   if (lang < 0 || (uint32_t)lang >= T.l2p_size) return 0;
-  return T.l2p[lang];
+  return gld(T.l2p + (lang));
 }
 // BetterBoundary scoreonescriptspan.cc:671-720
 __device__ int better_boundary(const DevTables& T, const VecOut& vo, uint8_t ps0, uint8_t ps1, int lin0, int lin1,
@@ -1750,7 +1765,7 @@ __device__ void score_one_script_span(const DevTables& T, Ctx& cx, W& w, const S
 
 // ------------------------------------------------------ document level
 // RefineScoredClosePairs + MoveLang1ToLang2 compact_lang_det_impl.cc:1105-1203
-__device__ void refine_scored_close_pairs(const DevTables& T, DocTote& d, VecOut* vo = nullptr) {
+__device__ __forceinline__ void refine_scored_close_pairs(const DevTables& T, DocTote& d, VecOut* vo = nullptr) {
   for (int s = 0; s < 24; ++s) {
     int cs = close_set(T, d.key[s]);
     if (cs == 0) continue;
@@ -1768,7 +1783,7 @@ __device__ void refine_scored_close_pairs(const DevTables& T, DocTote& d, VecOut
   }
 }
 // RemoveUnreliableLanguages :997-1101 (score field receives newbytes, as there)
-__device__ void remove_unreliable_languages(const DevTables& T, DocTote& d) {
+__device__ __forceinline__ void remove_unreliable_languages(const DevTables& T, DocTote& d) {
   for (int s = 0; s < 24; ++s) {
     int lang = d.key[s];
     if (lang == kUnusedKey) continue;
@@ -1777,7 +1792,7 @@ __device__ void remove_unreliable_languages(const DevTables& T, DocTote& d) {
     int rp = reli / bytes;
     if (rp >= 41) continue;
     int alt = (int)T.unknown_lang;
-    if ((uint32_t)lang <= T.hawaiian && (uint32_t)lang < T.n_closest) alt = T.closest[lang];
+    if ((uint32_t)lang <= T.hawaiian && (uint32_t)lang < T.n_closest) alt = gld(T.closest + (lang));
     if (alt == (int)T.unknown_lang) continue;
     int as = d.find((uint16_t)alt);
     if (as < 0) continue;
@@ -1804,7 +1819,7 @@ __device__ void remove_unreliable_languages(const DevTables& T, DocTote& d) {
 struct Extract { int lang3[3], pct3[3], rp3[3], text_bytes; bool reliable; double ns3[3]; };
 
 // ExtractLangEtc :1276-1384 with GetNormalizedScore :1269-1273
-__device__ void extract_lang_etc(const DevTables& T, const DocTote& d, int total, Extract& x) {
+__device__ __forceinline__ void extract_lang_etc(const DevTables& T, const DocTote& d, int total, Extract& x) {
   const int unk = (int)T.unknown_lang;
   int bc[3] = {0, 0, 0};
   for (int i = 0; i < 3; ++i) { x.rp3[i] = 0; x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; }
@@ -1848,7 +1863,7 @@ template <class V>
 __device__ __forceinline__ V sel3(const V (&a)[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
 
 // CalcSummaryLang :1414-1522
-__device__ int calc_summary_lang(const DevTables& T, int total, const Extract& x, bool& rel) {
+__device__ __forceinline__ int calc_summary_lang(const DevTables& T, int total, const Extract& x, bool& rel) {
   const int unk = (int)T.unknown_lang, en = (int)T.english;
   int slot_count = 3;
   int active[3] = {0, 1, 2};

@@ -257,7 +257,7 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
             slow = 1;
           } else {
             need += n - 1;
-            const uint64_t e = T.cpt[cpt_index(c, b1, b2, n)];
+            const uint64_t e = gld(T.cpt + (cpt_index(c, b1, b2, n)));
             const int st = (int)((e >> 8) & 3);
             slow |= st == 3;
             s.sn[p] = (uint8_t)e;
@@ -966,7 +966,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     int cnt = 0;
     // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row
     auto add = [&](uint32_t lp) {
-      const uint32_t e = *reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4);
+      const uint32_t e = gld(reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4));
       const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
       if (k1) { atomicAdd(&s.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
       if (k2) { atomicAdd(&s.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
@@ -1034,7 +1034,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     int actual = 0;
     if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
     const int esub = lang1 * 4 + lscript4(T, ulscript);
-    const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? T.expected[esub] : 0;
+    const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? gld(T.expected + (esub)) : 0;
     const uint16_t bytes = (uint16_t)len, grams = (uint16_t)cgr;
     const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2;
     int rd = (uint8_t)reliability_delta(s1, s2, grams);
@@ -1108,7 +1108,7 @@ __device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
 // they could change exists -- otherwise they are no-ops there too.  Returns 1
 // with the result written, or 0 when the first pass is not good enough and the
 // Repeats pass must follow (never when `final`).
-__device__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
+__device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
                                int lane) {
   if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
     if (lane == 0) refine_scored_close_pairs(T, dt);
