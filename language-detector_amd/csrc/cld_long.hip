@@ -1247,10 +1247,20 @@ __device__ __forceinline__ bool word_lists(const uint8_t* text, int tb, int star
   return nws <= kListCap && nsp <= kListCap;
 }
 
-__device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uint16_t* out) {
+// The first four entries are also returned packed (r01: entries 0-1, r23:
+// entries 2-3, 16 bits each), so build_chain writes most words without a
+// second walk.
+__device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uint16_t* out, uint32_t& r01, uint32_t& r23) {
   int cnt = 0, src = s;
+  r01 = 0;
+  r23 = 0;
   for (;;) {
     if (out) out[cnt] = (uint16_t)src;
+    if (cnt < 4) {
+      const uint32_t v = (uint32_t)src << (16 * (cnt & 1));
+      if (cnt < 2) r01 |= v;
+      else r23 |= v;
+    }
     ++cnt;
     int e = src;
     e += adv_but_space(text[e]);
@@ -1274,11 +1284,20 @@ __device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S,
     int cnt = 0;
     const int s = (LNG_PF & 1) ? sn : (i < nws ? S.wst[i] : 0);
     if (LNG_PF & 1) sn = i + 64 < nws ? S.wst[i + 64] : 0;
-    if (i < nws) cnt = walk_word(text, s, tb, nullptr);
+    uint32_t r01 = 0, r23 = 0;
+    if (i < nws) cnt = walk_word(text, s, tb, nullptr, r01, r23);
     const int pre = excl_scan(cnt, lane);
     const int tot = rdl(pre + cnt, 63);
     if (nch + tot > kListCap) return -1;
-    if (i < nws) walk_word(text, s, tb, S.chain + nch + pre);
+    uint16_t* o = S.chain + nch + pre;
+    if (cnt > 4) {
+      walk_word(text, s, tb, o, r01, r23);         // long word: walk again
+    } else {
+      if (cnt > 0) o[0] = (uint16_t)r01;
+      if (cnt > 1) o[1] = (uint16_t)(r01 >> 16);
+      if (cnt > 2) o[2] = (uint16_t)r23;
+      if (cnt > 3) o[3] = (uint16_t)(r23 >> 16);
+    }
     nch += tot;
   }
   gsync();
