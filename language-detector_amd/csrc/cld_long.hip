@@ -81,7 +81,7 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 #endif
 constexpr int kLdsText = LNG_TEXT;
 // Read-ahead of the slot's streams (bit 1 word starts, 2 quad chain, 4 octa
-// word ends, 8 hit streams in score_round): overlap vs the registers it costs.
+// word ends): overlap vs the registers it costs (measured: only 4 pays).
 #ifndef LNG_PF
 #define LNG_PF 4
 #endif
@@ -116,13 +116,13 @@ struct Slot {
   uint16_t wst[kListCap];                // quad chain entry points (word starts)
   uint16_t wsp[kListCap];                // word-ending spaces (octa words)
   uint16_t chain[kListCap];              // quad chain of the span
-  uint16_t b_off[kHB];                   // hits: base (CJK rounds; quad rounds only for the debug dump)
+  uint16_t b_off[kHB];                   // base hits (debug dump only)
   uint32_t b_ind[kHB];
   uint16_t d_off[kHB];                   // delta / distinct emissions (offsets; adds below)
-  uint32_t d_ind[kHB];                   //   (CJK rounds: hits, compacted to emissions in place)
+  uint32_t d_ind[kHB];                   // delta / distinct hits (debug dump only)
   uint16_t x_off[kHB];
   uint32_t x_ind[kHB];
-  uint16_t d_hoff[kHB];                  // octa rounds' delta / distinct hit offsets (debug dump only)
+  uint16_t d_hoff[kHB];                  // delta / distinct hit offsets (debug dump only)
   uint16_t x_hoff[kHB];
   uint16_t be_off[kEB];
   uint64_t be_add[kEB];                  // tote adds per emission (tote_adds), base / delta / distinct
@@ -1565,10 +1565,16 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
 }
 
 // GetUniHits + GetBiHits (cldutil.cc:201-310) for one round from off.
+// As in quad_round / octa_round, the hits become emissions here (eb base,
+// edm delta, exm distinct); the hit lists are kept only for the debug dump.
+template <bool D>
 __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int off, int& nb, int& nd,
-                         int& nx, int lane) {
+                         int& nx, int& eb, int& edm, int& exm, int lane) {
   const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
   nb = 0;
+  eb = 0;
+  edm = 0;
+  exm = 0;
   int next = -1;
   uint32_t endmax = (uint32_t)start;
   for (int w0 = start; w0 < tb; w0 += 64) {
@@ -1585,12 +1591,28 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
       lastl = nth_bit(hm, kMaxScoringHits - nb - 1);
       hm &= mask_le(lastl);
     }
-    if ((hm >> lane) & 1) {
+    const bool kept = (hm >> lane) & 1;
+    if (D && kept) {
       const int k = nb + __popcll(hm & lanemask_lt(lane));
       S.b_off[k] = (uint16_t)(x + len);
       S.b_ind[k] = (uint32_t)prop;
     }
     nb += __popcll(hm);
+    {
+      uint64_t l1 = 0, l2 = 0;
+      if (kept) base_adds(T.compat, T.compat, (uint32_t)prop, l1, l2);
+      const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
+      const int o = eb + excl_scan(c, lane);
+      eb = rdl(o + c, 63);
+      if (l1 >> 63) {
+        S.be_off[o] = (uint16_t)(x + len);
+        S.be_add[o] = l1;
+      }
+      if (l2 >> 63) {
+        S.be_off[o + 1] = (uint16_t)(x + len);
+        S.be_add[o + 1] = l2;
+      }
+    }
     if (lastl < 64) {
       next = rdl(x + len, lastl);
       break;
@@ -1612,17 +1634,34 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
         xp = quad_lookup(T.distinctbi, bh);
       }
     }
+    const uint64_t adp = dp ? adds_at(T.deltabi, dp & ~T.deltabi.key_mask) : 0ull;
+    const uint64_t axp = xp ? adds_at(T.distinctbi, xp & ~T.distinctbi.key_mask) : 0ull;
     const int cd = dp != 0, cx = xp != 0;
     const int ed = excl_scan(cd, lane), ex = excl_scan(cx, lane);
     const uint64_t capm = __ballot(v && (nd + ed + cd >= kMaxScoringHits || nx + ex + cx >= kMaxScoringHits - 1));
     const int cut = capm ? __builtin_ctzll(capm) : 64;
-    if (lane <= cut) {
+    {
+      const bool in = lane <= cut;
+      const int md = in ? (int)(adp >> 63) : 0, mx = in ? (int)(axp >> 63) : 0;
+      const int od = edm + excl_scan(md, lane), ox = exm + excl_scan(mx, lane);
+      edm = rdl(od + md, 63);
+      exm = rdl(ox + mx, 63);
+      if (md) {
+        S.d_off[od] = (uint16_t)x;
+        S.d_add[od] = adp;
+      }
+      if (mx) {
+        S.x_off[ox] = (uint16_t)x;
+        S.x_add[ox] = axp;
+      }
+    }
+    if (D && lane <= cut) {
       if (dp) {
-        S.d_off[nd + ed] = (uint16_t)x;
+        S.d_hoff[nd + ed] = (uint16_t)x;
         S.d_ind[nd + ed] = dp & ~T.deltabi.key_mask;
       }
       if (xp) {
-        S.x_off[nx + ex] = (uint16_t)x;
+        S.x_hoff[nx + ex] = (uint16_t)x;
         S.x_ind[nx + ex] = xp & ~T.distinctbi.key_mask;
       }
     }
@@ -1699,114 +1738,14 @@ __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, i
 // range of each stream.
 template <bool D>
 LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
-                            int lowest, int dummy_off, int lane, int feb = -1, int fed = 0, int fex = 0) {
-  // feb >= 0: the emissions were made by quad_round / octa_round (feb base,
-  // fed delta, fex distinct); else (CJK rounds) they are made here from the hits
-  const bool fused = feb >= 0;
-  const int hb = fused ? 0 : nb, hd = fused ? 0 : nd, hx = fused ? 0 : nx;
-  const DevTbl& bo = cjk ? T.compat : T.quad;
-  const DevTbl& bo2 = cjk ? T.compat : T.quad2;
-  const DevTbl& dob = cjk ? T.deltabi : T.deltaocta;
-  const DevTbl& xob = cjk ? T.distinctbi : T.distinctocta;
+                            int lowest, int dummy_off, int lane, int eb, int ed, int ex) {
+  // The hit rounds (quad_round / octa_round / cjk_round) already turned their
+  // nb / nd / nx hits into eb base, ed delta and ex distinct emissions (tote
+  // adds, zero langprobs dropped) in be_* / d_* / x_*.
+  (void)nd;
+  (void)nx;
   const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
   long long t2 = (D && kProfSub && s.prof) ? (long long)clock64() : 0;
-
-  // base hits -> base emissions (1 or 2 langprobs, zeros dropped)
-  // (each stream is read one block ahead, so its load overlaps the current
-  // block's table gathers)
-  int eb = 0;
-  const bool pf = LNG_PF & 8;
-  int noff = pf && lane < hb ? S.b_off[lane] : 0;
-  uint32_t nind = pf && lane < hb ? S.b_ind[lane] : 0u;
-  for (int j0 = 0; j0 < hb; j0 += 64) {
-    const int j = j0 + lane;
-    uint64_t l1 = 0, l2 = 0;                // tote adds (bit 63: non-zero langprob)
-    int off = 0;
-    const int coff = pf ? noff : (j < hb ? S.b_off[j] : 0);
-    const uint32_t cind = pf ? nind : (j < hb ? S.b_ind[j] : 0u);
-    if (pf) {
-      noff = j + 64 < hb ? S.b_off[j + 64] : 0;
-      nind = j + 64 < hb ? S.b_ind[j + 64] : 0u;
-    }
-    if (j < hb) {
-      off = coff;
-      uint32_t ind = cind;
-      const DevTbl* lb = &bo;
-      if (ind & 0x80000000u) {
-        lb = &bo2;
-        ind &= ~0x80000000u;
-      }
-      if (ind < lb->size_one) {
-        l1 = adds_at(*lb, ind);
-      } else {
-        ind += ind - lb->size_one;
-        l1 = adds_at(*lb, ind);
-        l2 = adds_at(*lb, ind + 1);
-        if (!(l1 >> 63)) {
-          l1 = l2;
-          l2 = 0;
-        }
-      }
-    }
-    const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
-    const int o = eb + excl_scan(c, lane);
-    eb = rdl(o + c, 63);
-    if (l1 >> 63) {
-      S.be_off[o] = (uint16_t)off;
-      S.be_add[o] = l1;
-    }
-    if (l2 >> 63) {
-      S.be_off[o + 1] = (uint16_t)off;
-      S.be_add[o + 1] = l2;
-    }
-  }
-  if constexpr (D) mark_sub(s, lane, 0, t2);
-  // delta / distinct emissions, compacted in place (ind -> langprob)
-  int ed = 0, ex = 0;
-  uint32_t dni = pf && lane < hd ? S.d_ind[lane] : 0u;
-  uint16_t dno = pf && lane < hd ? S.d_off[lane] : (uint16_t)0;
-  for (int j0 = 0; j0 < hd; j0 += 64) {
-    const int j = j0 + lane;
-    const uint32_t ci = pf ? dni : (j < hd ? S.d_ind[j] : 0u);
-    const uint16_t off = pf ? dno : (j < hd ? S.d_off[j] : (uint16_t)0);
-    if (pf) {
-      dni = j + 64 < hd ? S.d_ind[j + 64] : 0u;
-      dno = j + 64 < hd ? S.d_off[j + 64] : (uint16_t)0;
-    }
-    const uint64_t a = j < hd ? adds_at(dob, ci) : 0ull;
-    const int nz = (int)(a >> 63);
-    const int o = ed + excl_scan(nz, lane);
-    ed = rdl(o + nz, 63);
-    if (nz) {
-      S.d_off[o] = off;
-      S.d_add[o] = a;
-    }
-  }
-  uint32_t xni = pf && lane < hx ? S.x_ind[lane] : 0u;
-  uint16_t xno = pf && lane < hx ? S.x_off[lane] : (uint16_t)0;
-  for (int j0 = 0; j0 < hx; j0 += 64) {
-    const int j = j0 + lane;
-    const uint32_t ci = pf ? xni : (j < hx ? S.x_ind[j] : 0u);
-    const uint16_t off = pf ? xno : (j < hx ? S.x_off[j] : (uint16_t)0);
-    if (pf) {
-      xni = j + 64 < hx ? S.x_ind[j + 64] : 0u;
-      xno = j + 64 < hx ? S.x_off[j + 64] : (uint16_t)0;
-    }
-    const uint64_t a = j < hx ? adds_at(xob, ci) : 0ull;
-    const int nz = (int)(a >> 63);
-    const int o = ex + excl_scan(nz, lane);
-    ex = rdl(o + nz, 63);
-    if (nz) {
-      S.x_off[o] = off;
-      S.x_add[o] = a;
-    }
-  }
-  if constexpr (D) mark_sub(s, lane, 1, t2);
-  if (fused) {
-    eb = feb;
-    ed = fed;
-    ex = fex;
-  }
   // chunk plan from the base-hit count (ChunkAll :978-1031)
   int K = 0;
   if (nb <= 0) {
@@ -2041,11 +1980,12 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
     while (off < tb) {
       int nb, nd, nx;
       if constexpr (D) trace(tr, lane, doc, 20, off);
-      const int next = cjk_round(T, text, tb, S, off, nb, nd, nx, lane);
+      int eb, edm, exm;
+      const int next = cjk_round<D>(T, text, tb, S, off, nb, nd, nx, eb, edm, exm, lane);
       if constexpr (D) trace(tr, lane, doc, 21, next);
-      if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, false, lane);
+      if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
       if constexpr (D) mark(s, lane, 6, t);
-      score_round<D>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane);
+      score_round<D>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane, eb, edm, exm);
       if constexpr (D) mark(s, lane, 7, t);
       off = next;
     }
