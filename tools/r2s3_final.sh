@@ -9,6 +9,7 @@ tail -3 $O/pytest_gpu.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 1
 cat $O/smoke.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > $O/trace_bench.json 2> $O/trace_bench.err || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_c2 -o c2 --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-sub --no-host > $O/trace_c2.json 2> $O/trace_c2.err || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_c3 -o c3 --output-format csv -- python3 bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-sub --no-host > $O/trace_c3.json 2> $O/trace_c3.err || exit 1
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 for c in c3 c4 c5; do
