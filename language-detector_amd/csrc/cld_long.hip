@@ -93,9 +93,6 @@ constexpr int kLdsText = LNG_TEXT;
 #ifndef LNG_NS_INL
 #define LNG_NS_INL __device__ __forceinline__
 #endif
-#ifndef LNG_REPX
-#define LNG_REPX 1                       // experiments: 2 = read-ahead of two windows in rep_span_lds, 3 = no predictor
-#endif
 
 // Per-wave working set in HBM (one per resident wavefront of the persistent grid).
 struct Slot {
@@ -872,19 +869,6 @@ __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_
   int D = 0, WD = 0;                     // dst, word_dst (as offsets)
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
   int carry = 0;
-#if LNG_REPX == 2
-  uint32_t n0 = text[lane], n1 = text[lane + 1], n2 = text[lane + 2];
-  uint32_t m0 = text[lane + 64], m1 = text[lane + 65], m2 = text[lane + 66];
-  for (int w = 0; w < nw; ++w) {
-    const int base = w << 6, x = base + lane;
-    const uint32_t b0 = n0, b1 = n1, b2 = n2;
-    n0 = m0; n1 = m1; n2 = m2;
-    if (w + 2 < nw) {
-      m0 = text[x + 128];
-      m1 = text[x + 129];
-      m2 = text[x + 130];
-    }
-#else
   uint32_t n0 = text[lane], n1 = text[lane + 1], n2 = text[lane + 2];
   for (int w = 0; w < nw; ++w) {
     const int base = w << 6, x = base + lane;
@@ -894,7 +878,6 @@ __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_
       n1 = text[x + 65];
       n2 = text[x + 66];
     }
-#endif
     const bool valid = x < len;
     // (well-formed text: the starts come from the bytes already in registers)
     const uint64_t st = careful ? char_starts(text, base, len, nullptr, carry, careful, lane)
@@ -911,12 +894,7 @@ __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_
       code = pred_code(b0, b1, b2, incr);
     }
     const uint64_t lm = __ballot(lead);
-#if LNG_REPX == 3
-    const bool pr = false;
-    hcarry = 0;
-#else
     const bool pr = lm ? predict_window_lds(tbl, ovf, lm, c, code, hcarry, lane) : false;
-#endif
     const int wl = lead ? incr : 0, gd = (lead && pr) ? incr : 0;
     const bool sp = lead && b0 == ' ';
     const uint64_t spm = __ballot(sp);
