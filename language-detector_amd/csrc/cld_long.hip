@@ -543,22 +543,24 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     raw_bytes(dv, x0, r0, r1, r2, lo, hi);
     int i1;
     cp_index(dv, x0, lo, hi, i1, i2);
-    cp_gather<true>(T, i1, i2, e, e2);
+    cp_gather<false>(T, i1, i2, e, e2);
     raw_load(dv, x0 + 64, r0, r1, r2);          // (guarded: nothing past the document is read)
   }
   for (int w = q >> 6;; ++w) {
     const int x = (w << 6) + lane;
     uint32_t lw = 0, cw = 0;
+    int cur_i2 = -1;                             // property index of the next character (cp_index)
     {
       uint32_t lo1, hi1, e2n;
       uint64_t en;
       int j1, j2;
       raw_bytes(dv, x + 64, r0, r1, r2, lo1, hi1);
       cp_index(dv, x + 64, lo1, hi1, j1, j2);
-      cp_gather<true>(T, j1, j2, en, e2n);
+      cp_gather<false>(T, j1, j2, en, e2n);
       raw_load(dv, x + 128, r0, r1, r2);
       int ignore2 = 0;
-      cw = cp_decode<true>(T, dv, x, lo, hi, e, e2, i2, lw, ignore2, ignore2, ignore2);
+      cw = cp_decode<false>(T, dv, x, lo, hi, e, e2, i2, lw, ignore2, ignore2, ignore2);
+      cur_i2 = i2;
       lo = lo1;
       hi = hi1;
       e = en;
@@ -579,7 +581,10 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         if (sc == common) {
           brk = true;
         } else {
-          const int sc2 = cls_sn2(cw);
+          // the next character's script, only for a letter of another script
+          // (rare inside a span): gathered here rather than for every byte
+          const int sc2 = cur_i2 >= 0 ? (int)(gld(reinterpret_cast<const uint32_t*>(T.cpt) + 2 * cur_i2) & 0xFF)
+                                      : script_num(T, dv, x + n);
           brk = sc2 != common && sc2 != ss;
         }
       }
