@@ -622,7 +622,9 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     if (act && (sep || hard_here)) lb[lpos + opre + olen] = ' ';
     if (act && chr && cutc) cutx = x;
     lpos += rdl(opre + tl, 63);
-    put += wsum(act ? raw + (hard_here ? 1 : 0) : 0);
+    // raw bytes of the lanes up to the stop (a prefix-sum read, not another
+    // reduction), plus the hard limit's ' '
+    put += rdl(pre + raw, stop < 64 ? stop : 63) + ((stop < 64 && ((Hm >> stop) & 1)) ? 1 : 0);
     if (lpos + 64 > kLB || put + 64 > kMaxScriptBuffer) {
       bad = 1;
       break;
