@@ -224,8 +224,8 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
     const int sh = (int)(ga & 3);
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(ga - (uintptr_t)sh);
     const int nw = (L + sh + 3) >> 2;                    // <= 65
-    const uint32_t w0 = lane < nw ? gw[lane] : 0u;
-    const uint32_t w64 = nw > 64 ? gw[64] : 0u;
+    const uint32_t w0 = lane < nw ? gld(gw + lane) : 0u;     // (gld: global, not FLAT, loads)
+    const uint32_t w64 = nw > 64 ? gld(gw + 64) : 0u;
     // lane + 1's word (DPP wave_shl:1); lane 63 keeps `old` = word 64
     const uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp((int)w64, (int)w0, kDppWaveShl1, 0xF, 0xF, false);
     const uint32_t v = sh == 0 ? w0 : __builtin_amdgcn_alignbyte(nxt, w0, (uint32_t)sh);
