@@ -34,7 +34,7 @@ def main():
         orc = Oracle()
     cfgs = [("c2", lambda: corpus.c2(1_000_000)), ("c3", lambda: corpus.c3(100_000)),
             ("c3_boiler5", lambda: corpus.c3(20_000, boiler_frac=0.05)), ("c4", lambda: corpus.c4(1_100_000)),
-            ("c5", lambda: corpus.c5(1_000_000))]
+            ("c5", lambda: corpus.c5(1_000_000)), ("html", lambda: corpus.html(100_000, seed=77))]
     only = set(args)
     for name, gen in cfgs:
         if only and name not in only:
@@ -43,9 +43,16 @@ def main():
         print("# %s: generating" % name, flush=True)
         buf, offs = gen()
         print("# %s: %d docs generated in %.1f s" % (name, len(offs) - 1, time.time() - t0), flush=True)
-        got = cld_amd.detect_batch(buf=buf, offsets=offs)
+        html = name == "html"                  # is_plain_text = false (ExtDetectLanguageSummary)
+        got = cld_amd.detect_batch_ex(buf=buf, offsets=offs, html=True) if html else \
+            cld_amd.detect_batch(buf=buf, offsets=offs)
         st = cld_amd.last_stats(0)
-        ref = orc.detect_batch(buf, offs, threads=16)
+        if html:
+            plain = np.zeros(len(offs) - 1, np.uint8)
+            ref = orc.detect_batch(buf, offs, plain=plain, threads=16) if use_ref else \
+                orc.detect_batch_ex(buf, offs, plain=plain, threads=16)
+        else:
+            ref = orc.detect_batch(buf, offs, threads=16)
         bad = np.zeros(len(got), dtype=bool)
         for f in FIELDS:
             bad |= (got[f].astype(np.float64) != ref[f].astype(np.float64)).reshape(len(got), -1).any(axis=1)
