@@ -16,6 +16,14 @@
 #include "cld_wave.hip"
 #include "cld_long.hip"
 
+#ifndef GEN_LANES_PER_WAVE
+// k_general / k_general_vec: documents per wavefront.  One per wave: the
+// sequential per-document code then never diverges between documents in a
+// wave (64 per wave ran every document's branches for all of them: HTML pages
+// 52K -> 185K docs/s).
+#define GEN_LANES_PER_WAVE 1
+#endif
+
 namespace cld {
 
 using ShortWork = Work<kShortSB, kShortLB, kShortHB, false>;
@@ -60,7 +68,13 @@ __global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp
                                                const uint8_t* __restrict__ special,
                                                const uint32_t* __restrict__ priors) {
   const DevTables& T = *Tp;
+#if GEN_LANES_PER_WAVE == 1
+  // one document per wavefront (lane 0): no divergence between documents
+  if (threadIdx.x != 0) return;
+  const int lane = blockIdx.x;
+#else
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+#endif
   GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
   const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // nothing re-queued (every C2 / C4 batch): leave before touching the shared
@@ -108,7 +122,12 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
                                                    cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
                                                    int32_t* __restrict__ n_chunks) {
   const DevTables& T = *Tp;
+#if GEN_LANES_PER_WAVE == 1
+  if (threadIdx.x != 0) return;
+  const int lane = blockIdx.x;
+#else
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+#endif
   VecWork& w = *reinterpret_cast<VecWork*>(arena + (uint64_t)lane * stride);
   for (;;) {
     const uint32_t k = atomicAdd(&counters[kCtrDequeue2], 1u);
@@ -414,7 +433,11 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
                                   const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+#if GEN_LANES_PER_WAVE == 1
+  dim3 grid(lanes), block(64);
+#else
   dim3 grid(lanes / 64), block(64);
+#endif
   hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
                      priors, pool, pool_off, n_chunks);
   return hipGetLastError();
@@ -455,7 +478,11 @@ hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const ui
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               const uint8_t* special, const uint32_t* priors, hipStream_t s) {
+#if GEN_LANES_PER_WAVE == 1
+  dim3 grid(lanes), block(64);                   // `lanes` documents in flight, one per wavefront
+#else
   dim3 grid(lanes / 64), block(64);
+#endif
   hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, d_T, buf, offs, list, out, arena, stride,
                      counters, ctr_count, ctr_deq, special, priors);
   return hipGetLastError();

@@ -512,7 +512,7 @@ int init_device(Device* d) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->id));
   d->stride = (cld_general_work_bytes() + 255) & ~(uint64_t)255;
-  int lanes = prop.multiProcessorCount * 64 * 2;
+  int lanes = prop.multiProcessorCount * 32;     // k_general documents in flight (one per wavefront)
   if (const char* e = getenv("CLD_GENERAL_LANES")) lanes = atoi(e);
   lanes = std::max(64, (lanes / 64) * 64);
   while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
