@@ -57,6 +57,22 @@ typedef struct cld_result {
  * (getonescriptspan.cc:150-541, 592-1027), lang= attributes in the first 8 KB
  * become hints (compact_lang_det_impl.cc:1596-1611). */
 #define CLD_FLAG_HTML 4u
+/* The reference's public result-affecting flags, with the reference's values
+ * (compact_lang_det.h:343-349), accepted in the `flags` word of every batch
+ * entry point and applied to every document of the batch:
+ *   CLD_FLAG_SCORE_AS_QUADS  kCLDFlagScoreAsQuads: scripts normally scored by
+ *                            their script alone (RTypeOne/None: Greek, Thai,
+ *                            ...) are quadgram-scored instead
+ *                            (scoreonescriptspan.cc:1318-1320)
+ *   CLD_FLAG_BEST_EFFORT     kCLDFlagBestEffort: no unreliable-language removal
+ *                            and no UNKNOWN summary for a small top percent
+ *                            (compact_lang_det_impl.cc:1998-2000, :1493)
+ * The reference's debug-output flags (kCLDFlagHtml, Cr, Verbose, Quiet, Echo:
+ * CLD_FLAG_DEBUG_MASK) only write diagnostics to stderr there; they are
+ * accepted and ignored. */
+#define CLD_FLAG_SCORE_AS_QUADS 0x0100u
+#define CLD_FLAG_BEST_EFFORT 0x4000u
+#define CLD_FLAG_DEBUG_MASK 0x3E00u
 
 /* ResultChunk (compact_lang_det.h:147-153): one piece of a document in one
  * language; offset/bytes index the document as given; lang1 is a Language
@@ -125,23 +141,24 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * CLD2::DetectLanguage(buffer, length, ...)).  `out` is caller-allocated
  * (n entries).  Host buffers; not retained after return.  Blocks until the
  * results are in `out`.  Documents are sharded across the initialised GPUs
- * by byte count; each shard streams through the GPU in chunks of <= 64 MB /
- * 512K documents (pinned staging, upload / kernels / download overlapped on
- * three streams).  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING (above).
- * Thread-safe. */
+ * by byte count; each shard streams through the GPU in chunks of <= 32 MB /
+ * 256K documents (pinned staging, upload / kernels / download overlapped on
+ * three streams).  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING and
+ * CLD_FLAG_SCORE_AS_QUADS / CLD_FLAG_BEST_EFFORT (above).  Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
                      cld_result* out, uint32_t flags);
 
-/* ExtDetectLanguageSummary (compact_lang_det.h:261-294 / impl.cc:1707) over a
- * batch: `hints` is NULL or one cld_hints per document; flags may add
- * CLD_FLAG_HTML (all documents are HTML) to the preparation flags.  Documents
- * that are HTML or carry a hint run the exact sequential kernel; results
- * are the same fields as cld_detect_batch.  Host buffers; blocks. */
+/* ExtDetectLanguageSummary (compact_lang_det.h:324-335 / impl.cc:1707) over a
+ * batch: `hints` is NULL or one cld_hints per document (CLDHints); flags is
+ * the reference's `flags` argument -- CLD_FLAG_SCORE_AS_QUADS,
+ * CLD_FLAG_BEST_EFFORT, the ignored debug flags -- plus CLD_FLAG_HTML for
+ * is_plain_text = false (all documents are HTML).  Results are the same
+ * fields as cld_detect_batch.  Host buffers; blocks. */
 int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
                         uint32_t flags, cld_result* out);
 
 /* ExtDetectLanguageSummary with a ResultChunkVector per document
- * (compact_lang_det.h:261-294): the same results as cld_detect_batch_ex plus
+ * (compact_lang_det.h:324-335): the same results as cld_detect_batch_ex plus
  * each document's chunk vector -- pieces of the document as given, in one
  * language each (SummaryBufferToVector / SharpenBoundaries / OffsetMap,
  * scoreonescriptspan.cc:389-548, 671-845; offsetmap.cc).  Vector mode changes
@@ -172,7 +189,8 @@ int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld
 int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets,
                             size_t n, cld_result* d_out, void* stream);
 
-/* cld_detect_batch_device with text preparation flags.  buf_bytes bounds
+/* cld_detect_batch_device with flags (preparation and CLD2 flags, as for
+ * cld_detect_batch).  buf_bytes bounds
  * d_offsets[n] (the prepared copy is staged in a device buffer of
  * buf_bytes + n bytes).  Asynchronous like cld_detect_batch_device. */
 int cld_detect_batch_device_ex(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,

@@ -23,6 +23,8 @@ SYNTH_TABLES = os.path.join(HERE, "data", "cld2_synth_q1.cldt")
 FLAG_STRIP_EXTRAS = 1      # include/cld_mi355x.h CLD_FLAG_STRIP_EXTRAS
 FLAG_CSTRING = 2           # include/cld_mi355x.h CLD_FLAG_CSTRING
 FLAG_HTML = 4              # include/cld_mi355x.h CLD_FLAG_HTML (cld_detect_batch_ex)
+FLAG_SCORE_AS_QUADS = 0x0100   # CLD_FLAG_SCORE_AS_QUADS = kCLDFlagScoreAsQuads (compact_lang_det.h:343)
+FLAG_BEST_EFFORT = 0x4000      # CLD_FLAG_BEST_EFFORT = kCLDFlagBestEffort (compact_lang_det.h:349)
 UNKNOWN_ENCODING = 23      # encodings.h UNKNOWN_ENCODING
 UNKNOWN_LANGUAGE = 26      # generated_language.h UNKNOWN_LANGUAGE
 
@@ -215,7 +217,8 @@ def pack(docs):
 
 def detect_batch(docs=None, buf=None, offsets=None, flags=0):
     """One DetectLanguageSummaryV2 per document; flags = FLAG_STRIP_EXTRAS | FLAG_CSTRING
-    prepares each text as POST / does before detecting (handlers.go:150-151)."""
+    prepares each text as POST / does before detecting (handlers.go:150-151);
+    FLAG_SCORE_AS_QUADS / FLAG_BEST_EFFORT are CLD2's own flags."""
     if docs is not None:
         buf, offsets = pack(docs)
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -231,10 +234,10 @@ def detect_batch(docs=None, buf=None, offsets=None, flags=0):
     return out
 
 
-def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False):
-    """ExtDetectLanguageSummary per document (compact_lang_det.h:261-294):
+def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False, flags=0):
+    """ExtDetectLanguageSummary per document (compact_lang_det.h:324-335):
     html=True scores every document as HTML (is_plain_text = false); hints is
-    None or one Hints per document."""
+    None or one Hints per document; flags: FLAG_SCORE_AS_QUADS / FLAG_BEST_EFFORT."""
     if docs is not None:
         buf, offsets = pack(docs)
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -250,13 +253,13 @@ def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False):
         harr = (Hints * n)(*hints)
     bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
     rc = lib().cld_detect_batch_ex(bptr, offsets.ctypes.data, n, ctypes.cast(harr, ctypes.c_void_p) if harr else None,
-                                   FLAG_HTML if html else 0, out.ctypes.data)
+                                   (FLAG_HTML if html else 0) | flags, out.ctypes.data)
     if rc != 0:
         raise CldError("cld_detect_batch_ex failed: %d" % rc)
     return out
 
 
-def detect_batch_vec(docs=None, buf=None, offsets=None, hints=None, html=False, chunk_cap=None):
+def detect_batch_vec(docs=None, buf=None, offsets=None, hints=None, html=False, chunk_cap=None, flags=0):
     """ExtDetectLanguageSummary with a ResultChunkVector per document:
     (results, chunks [CHUNK_DTYPE], chunk_offsets[n+1]); document i's vector is
     chunks[chunk_offsets[i]:chunk_offsets[i+1]]."""
@@ -280,7 +283,7 @@ def detect_batch_vec(docs=None, buf=None, offsets=None, hints=None, html=False, 
         chunks = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
         rc = lib().cld_detect_batch_vec(bptr, offsets.ctypes.data, n,
                                         ctypes.cast(harr, ctypes.c_void_p) if harr else None,
-                                        FLAG_HTML if html else 0, out.ctypes.data, chunks.ctypes.data, cap,
+                                        (FLAG_HTML if html else 0) | flags, out.ctypes.data, chunks.ctypes.data, cap,
                                         coffs.ctypes.data)
         if rc == 0:
             return out, chunks[:int(coffs[-1])], coffs

@@ -8,7 +8,9 @@ documents (unittest_data.h kTeststr_{zh_Hans,zh_Hant,ja_Hani,ko_Hani}).
   c2  n x U[100,180] B tweets, >= 10 Latin-script languages, 10% capitalised
       words, 5% digit/punctuation tokens                       
   c3  n x 16384 B pages: four ~4 KB paragraphs in Latin / Cyrillic / Arabic /
-      Devanagari languages in random order                      
+      Devanagari languages in random order; a stated fraction (mono_frac,
+      default 1/4) of pages is four paragraphs of ONE language instead, which
+      finishes in pass 1 -- the rest need the Repeats pass      
   c4  zh-Hans/zh-Hant/ja/ko documents: 10 of every 11 ~150 B, 1 in 11 ~4 KB
       (1.1M docs = 1M x 150 B + 100K x 4 KB)                     
   c5  lognormal lengths (median 140 B, cap 64 KB) mixing c2..c4
@@ -116,9 +118,17 @@ def c2(n, seed=SEEDS["c2"]):
 BOILERPLATE = b"home | news | contact | login | "
 
 
-def c3(n, seed=SEEDS["c3"], page=16384, boiler_frac=0.0):
+C3_MONO_FRAC = 0.25
+
+
+def c3(n, seed=SEEDS["c3"], page=16384, boiler_frac=0.0, mono_frac=C3_MONO_FRAC):
     """Four paragraphs per page, one per script (random order, random language
     of that script), each ~page/4 bytes; pages padded with spaces to `page`.
+    mono_frac: in that fraction of pages (seeded, drawn after everything else,
+    so the other pages do not change with it) all four paragraphs are one
+    language of one script: those pages are reliable and >= 70% one language
+    after pass 1 and finish there (compact_lang_det_impl.cc:1978-1991), the
+    four-script pages never are and take pass 2 (Repeats).
     boiler_frac: in that fraction of pages (seeded) the Latin paragraph opens
     with ~1 KB of repeated navigation boilerplate, which trips
     CheapSqueezeTriggerTest (compact_lang_det_impl.cc:952-971) and makes the
@@ -154,6 +164,23 @@ def c3(n, seed=SEEDS["c3"], page=16384, boiler_frac=0.0):
     if boiler_frac:
         boiler[rng.random(n) < boiler_frac] = True
         bp = np.frombuffer(BOILERPLATE * (1024 // len(BOILERPLATE) + 1), dtype=np.uint8)[:1024]
+    if mono_frac:
+        mrng = np.random.default_rng(seed ^ 0x6D6F6E6F)
+        mono = np.nonzero(mrng.random(n) < mono_frac)[0]
+        ms = mrng.integers(0, len(scripts), size=len(mono))
+        for si, sname in enumerate(scripts):
+            rows = mono[ms == si]
+            if not len(rows):
+                continue
+            t = tables[sname]
+            li = mrng.integers(0, len(t.langs), size=len(rows))
+            for k in range(4):
+                tg = mrng.integers(para - 256, para + 1, size=len(rows))
+                b, o = _assemble(mrng, t, li, tg, kmax=para // 3, punct_frac=0.02)
+                ol = o.astype(np.int64)
+                for j, r in enumerate(rows):
+                    pieces[r][k] = b[ol[j]:ol[j + 1]]
+            order[rows] = np.where(si == 0, 0, 1)          # (the boilerplate goes first on a Latin page)
     latin = np.argmax(order == 0, axis=1)              # slot of the Latin paragraph
     for r in range(n):
         ps = list(pieces[r])

@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __res
                                               uint32_t* __restrict__ requeue_list,
                                               uint32_t* __restrict__ counters,
                                               const uint8_t* __restrict__ special,
-                                              uint32_t* __restrict__ special_list, int special_ctr) {
+                                              uint32_t* __restrict__ special_list, int special_ctr,
+                                              uint32_t cflags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (special && special[i]) {
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __res
     ShortWork w;
     Status st{false};
     DocView d{buf + a, (int)len};
-    detect_doc(T, d, w, &out[i], st);
+    detect_doc(T, d, w, &out[i], st, true, nullptr, nullptr, cflags);
     rq = st.requeue;
   }
   if (rq) {
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp
                                                uint8_t* __restrict__ arena, uint64_t stride,
                                                uint32_t* __restrict__ counters, int ctr_count, int ctr_deq,
                                                const uint8_t* __restrict__ special,
-                                               const uint32_t* __restrict__ priors) {
+                                               const uint32_t* __restrict__ priors, uint32_t cflags) {
   const DevTables& T = *Tp;
 #if GEN_LANES_PER_WAVE == 1
   // one document per wavefront (lane 0): no divergence between documents
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp
     // ApplyHints priors (16 langprobs each, bit 1)
     const uint8_t sp = special ? special[i] : 0;
     int passes = detect_doc(T, d, w, &out[i], st, !(sp & kSpecialHtml),
-                            (sp & kSpecialPriors) ? priors + 16ull * i : nullptr);
+                            (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, cflags);
     if (passes >= 1 && passes <= 3) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
     else atomicAdd(&counters[kCtrError], 1u);
   }
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
                                                    const uint8_t* __restrict__ special,
                                                    const uint32_t* __restrict__ priors,
                                                    cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
-                                                   int32_t* __restrict__ n_chunks) {
+                                                   int32_t* __restrict__ n_chunks, uint32_t cflags) {
   const DevTables& T = *Tp;
 #if GEN_LANES_PER_WAVE == 1
   if (threadIdx.x != 0) return;
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
     DocView d{buf + a, (int)(b - a)};
     const uint8_t sp = special ? special[i] : 0;
     const int passes = detect_doc(T, d, w.g, &out[i], st, !(sp & kSpecialHtml),
-                                  (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, &vo);
+                                  (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, &vo, cflags);
     const bool bad = passes < 1 || passes > 3 || st.requeue || vo.over || vo.orig.over || vo.low.over;
     n_chunks[i] = bad ? -1 : vo.n;
     if (!bad) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
                                                    uint32_t* __restrict__ counters,
                                                    unsigned long long* __restrict__ prof,
                                                    const uint8_t* __restrict__ special,
-                                                   uint32_t* __restrict__ special_list, int special_ctr) {
+                                                   uint32_t* __restrict__ special_list, int special_ctr,
+                                                   uint32_t cflags) {
   __shared__ wave::Smem<CAP> smem[WPB];
   // wave index through readfirstlane: the document pointer, its length, the
   // result pointer and the LDS base are then scalars, not VGPRs live across
@@ -208,7 +210,8 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   bool rq = len > CAP;
   // stage cycles (CLD_PROFILE_STAGES=1) are sampled on one document in 64, so
   // the accounting atomics do not themselves become the bottleneck
-  if (!rq) rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr);
+  if (!rq) rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr,
+                                 cflags);
   if (rq && lane == 0) {
     uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
     requeue_list[k] = (uint32_t)i;
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   uint32_t* __restrict__ requeue2,
                                                   uint32_t* __restrict__ counters, uint32_t* trace,
                                                   uint32_t* dbg, uint32_t dbg_doc,
-                                                  unsigned long long* prof) {
+                                                  unsigned long long* prof, uint32_t cflags) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     }
     wave::wsync();
     if (exact && len <= (uint64_t)lng::kDocCap)
-      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i);
+      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags);
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (lane == 0) {
@@ -411,17 +414,17 @@ int cld_long_waves_per_simd() { return LNG_WPS; }
 hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
-                           unsigned long long* prof, hipStream_t s) {
+                           unsigned long long* prof, uint32_t cflags, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags);
   return hipGetLastError();
 }
 
@@ -431,7 +434,7 @@ size_t cld_vec_work_bytes() { return sizeof(cld::VecWork); }
 hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
-                                  const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
+                                  const uint64_t* pool_off, int32_t* n_chunks, uint32_t cflags, hipStream_t s) {
   if (n <= 0) return hipSuccess;
 #if GEN_LANES_PER_WAVE == 1
   dim3 grid(lanes), block(64);
@@ -439,7 +442,7 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
   dim3 grid(lanes / 64), block(64);
 #endif
   hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
-                     priors, pool, pool_off, n_chunks);
+                     priors, pool, pool_off, n_chunks, cflags);
   return hipGetLastError();
 }
 
@@ -455,36 +458,37 @@ size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
-                           int special_ctr, hipStream_t s) {
+                           int special_ctr, uint32_t cflags, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
-                     requeue_list, counters, prof, special, special_list, special_ctr);
+                     requeue_list, counters, prof, special, special_list, special_ctr, cflags);
   return hipGetLastError();
 }
 
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                            const uint8_t* special, uint32_t* special_list, int special_ctr, hipStream_t s) {
+                            const uint8_t* special, uint32_t* special_list, int special_ctr, uint32_t cflags,
+                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   dim3 grid((n + 255) / 256), block(256);
   hipLaunchKernelGGL(cld::k_short, grid, block, 0, s, *T, buf, offs, n, out, requeue_list, counters, special,
-                     special_list, special_ctr);
+                     special_list, special_ctr, cflags);
   return hipGetLastError();
 }
 
 hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              const uint8_t* special, const uint32_t* priors, hipStream_t s) {
+                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, hipStream_t s) {
 #if GEN_LANES_PER_WAVE == 1
   dim3 grid(lanes), block(64);                   // `lanes` documents in flight, one per wavefront
 #else
   dim3 grid(lanes / 64), block(64);
 #endif
   hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, d_T, buf, offs, list, out, arena, stride,
-                     counters, ctr_count, ctr_deq, special, priors);
+                     counters, ctr_count, ctr_deq, special, priors, cflags);
   return hipGetLastError();
 }
 }

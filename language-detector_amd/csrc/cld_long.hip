@@ -1951,8 +1951,9 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
 template <bool D>
 __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb,
-                                           int ulscript, int lane, uint32_t* tr, uint32_t doc) {
-  const int rt = rtype_of(T, ulscript);
+                                           int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags) {
+  int rt = rtype_of(T, ulscript);
+  if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
   if (rt == RTypeNone || rt == RTypeOne) {
     if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
     wsync();
@@ -2009,7 +2010,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
 enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
 template <bool D>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
-                      cld_result* __restrict__ out, uint32_t* tr, uint32_t doc) {
+                      cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags) {
   const int unk = (int)T.unknown_lang;
   if (L == 0) {
     if (lane == 0) {
@@ -2116,7 +2117,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc);
+        ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc, cflags);
       } else {
         const uint8_t* text = lb;
         if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
@@ -2132,7 +2133,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        ok = score_span<D>(T, S, s, text, tb, ul, lane, tr, doc);
+        ok = score_span<D>(T, S, s, text, tb, ul, lane, tr, doc, cflags);
       }
       if (!ok) return -kWhyCapacity;
       t = (D && s.prof) ? (long long)clock64() : 0;
@@ -2142,7 +2143,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
       sq = true;
       continue;
     }
-    if (wave::finish_document(T, s.dt, total, rep, out, lane)) return pass;
+    if (wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0)) return pass;
   }
   return 0;
 }

@@ -44,6 +44,9 @@ constexpr int kMaxSummaries = kMaxScoringHits / kChunksizeQuads;
 constexpr int kPredictionTableSize = 4096;
 constexpr int kCLDFlagFinish = 1, kCLDFlagSqueeze = 2, kCLDFlagRepeats = 4, kCLDFlagTop40 = 8,
               kCLDFlagShort = 16, kCLDFlagUseWords = 64;
+// The public result-affecting flags (compact_lang_det.h:343, :349), as the
+// caller passes them (CLD_FLAG_SCORE_AS_QUADS / CLD_FLAG_BEST_EFFORT)
+constexpr int kCLDFlagScoreAsQuads = 0x0100, kCLDFlagBestEffort = 0x4000;
 constexpr uint16_t kUnusedKey = 0xFFFF;
 enum { UNIHIT = 0, QUADHIT = 1, DELTAHIT = 2, DISTINCTHIT = 3 };
 enum { RTypeNone = 0, RTypeOne = 1, RTypeMany = 2, RTypeCJK = 3 };
@@ -1481,6 +1484,7 @@ struct Ctx {
   // latn[4] othr[4], then langprior_whack latn[4] othr[4]; null for none
   const uint32_t* priors;
   VecOut* vo;               // ResultChunkVector being built (k_general_vec), else null
+  int flags;                // the caller's public flags (kCLDFlagScoreAsQuads / kCLDFlagBestEffort)
 };
 
 // SetChunkSummary scoreonescriptspan.cc:60-96
@@ -1735,6 +1739,7 @@ __device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb,
 template <class W>
 __device__ void score_one_script_span(const DevTables& T, Ctx& cx, W& w, const Span& span, DocTote& dt, Status& st) {
   int rt = rtype_of(T, span.ulscript);
+  if ((cx.flags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // :1318-1320
   if (rt == RTypeNone || rt == RTypeOne) {
     int bytes = span.text_bytes;
     dt.add((uint16_t)default_language(T, span.ulscript), bytes, bytes, 100);
@@ -1862,8 +1867,9 @@ __device__ __forceinline__ bool is_efigs(const DevTables& T, int l) { return l =
 template <class V>
 __device__ __forceinline__ V sel3(const V (&a)[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
 
-// CalcSummaryLang :1414-1522
-__device__ __forceinline__ int calc_summary_lang(const DevTables& T, int total, const Extract& x, bool& rel) {
+// CalcSummaryLang :1414-1522 (best_effort: kCLDFlagBestEffort, :1493)
+__device__ __forceinline__ int calc_summary_lang(const DevTables& T, int total, const Extract& x, bool& rel,
+                                                 bool best_effort = false) {
   const int unk = (int)T.unknown_lang, en = (int)T.english;
   int slot_count = 3;
   int active[3] = {0, 1, 2};
@@ -1896,7 +1902,7 @@ __device__ __forceinline__ int calc_summary_lang(const DevTables& T, int total, 
   } else if (is_figs(T, l1) && !is_efigs(T, l0)) {
     ignore += p1; ret_pct = (p0 * 100) / (101 - ignore);
   }
-  if (ret_pct < 26) { summary = unk; rel = false; }
+  if (ret_pct < 26 && !best_effort) { summary = unk; rel = false; }
   if (ret_pct < 51) rel = false;
   if (100 - (x.pct3[0] + x.pct3[1] + x.pct3[2]) > 20) rel = false;
   if (slot_count == 0) { summary = unk; rel = false; }
@@ -1916,15 +1922,17 @@ __device__ void write_result(cld_result* r, const Extract& x, int summary, bool 
   *r = o;
 }
 
-// DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (flags 0, no
-// ResultChunkVector; HTML mode when !plain, the ApplyHints priors when given);
+// DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (HTML mode when
+// !plain, the ApplyHints priors when given, a ResultChunkVector when vo;
+// cflags: the caller's public flags, kCLDFlagScoreAsQuads / kCLDFlagBestEffort);
 // recursion unrolled into passes.  Returns the number of passes, or 0 with
 // st.requeue set.
 template <class W>
 __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result* out, Status& st,
-                          bool plain = true, const uint32_t* priors = nullptr, VecOut* vo = nullptr) {
+                          bool plain = true, const uint32_t* priors = nullptr, VecOut* vo = nullptr,
+                          uint32_t cflags = 0) {
   const int unk = (int)T.unknown_lang;
-  int flags = 0;
+  int flags = (int)(cflags & (kCLDFlagScoreAsQuads | kCLDFlagBestEffort));
   int passes = 0;
   Extract x;
   if (vo) vo->n = 0;
@@ -1943,6 +1951,7 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     cx.latn.n = 0; cx.othr.n = 0;
     cx.priors = priors;
     cx.vo = vo;
+    cx.flags = flags;
     if (vo) vo->n = 0;                       // resultchunkvector->clear() (:1730-1732)
     for (int k = 0; k < kMaxBoosts; ++k) { cx.latn.lp[k] = 0; cx.othr.lp[k] = 0; }
     int next = 0, remaining = d.len;
@@ -1987,11 +1996,11 @@ __device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result
     bool good = (flags & kCLDFlagFinish) || total <= 256 ||
                 (x.reliable && x.pct3[0] >= 70) || (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
     if (good) {
-      remove_unreliable_languages(T, dt);
+      if (!(flags & kCLDFlagBestEffort)) remove_unreliable_languages(T, dt);   // :1998-2000
       dt.sort3();
       extract_lang_etc(T, dt, total, x);
       bool rel;
-      int summary = calc_summary_lang(T, total, x, rel);
+      int summary = calc_summary_lang(T, total, x, rel, (flags & kCLDFlagBestEffort) != 0);
       write_result(out, x, summary, rel);
       if (vo && vo->n > 0) {                 // FinishResultVector(0, buffer_length) (:1688-1702)
         cld_chunk& a = vo->v[0];

@@ -17,7 +17,10 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <set>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -41,10 +44,20 @@ namespace {
   } while (0)
 
 // ------------------------------------------------------------ host tables
+// Language codes and names handed to callers stay valid for the life of the
+// process (the reference returns static strings, lang_script.cc:205-217):
+// they are interned once and never freed, even when the tables are swapped.
+const char* intern(const std::string& v) {
+  static std::mutex mu;
+  static std::set<std::string>* pool = new std::set<std::string>();
+  std::lock_guard<std::mutex> lk(mu);
+  return pool->insert(v).first->c_str();
+}
+
 struct HostTables {
   std::vector<uint8_t> blob;
   cldt_meta meta{};
-  std::vector<std::string> codes, names;
+  std::vector<const char*> codes, names;   // interned
   std::string version;
   DevTables offs{};   // pointer fields hold byte offsets into blob
   cld::HintView hints;   // host views for cld_hint_priors (null fields: the blob has no hint sections)
@@ -203,8 +216,10 @@ int parse_tables(HostTables* t, const std::string& label) {
   D.unknown_lang = M.unknown_language; D.english = M.english; D.tg_unknown = M.tg_unknown_language;
   D.french = M.french; D.italian = M.italian; D.german = M.german; D.spanish = M.spanish;
   D.hawaiian = M.hawaiian;
-  t->codes = strings(t->blob, CLDT_LANG_CODES);
-  t->names = strings(t->blob, CLDT_LANG_NAMES);
+  t->codes.clear();
+  t->names.clear();
+  for (const std::string& c : strings(t->blob, CLDT_LANG_CODES)) t->codes.push_back(intern(c));
+  for (const std::string& c : strings(t->blob, CLDT_LANG_NAMES)) t->names.push_back(intern(c));
   {  // optional HTML-mode sections: entity names (a sorted string table), their
      // code points, the cp1252 fix-up; all three or none
     uint64_t no = 0, ns = 0, vo = 0, vs = 0, co = 0, cs = 0;
@@ -261,8 +276,8 @@ int parse_tables(HostTables* t, const std::string& label) {
       h.unknown_language = t->meta.unknown_language;
       h.chinese = h.chinese_t = 0xFFFFFFFFu;
       for (size_t i = 0; i < t->codes.size(); ++i) {
-        if (t->codes[i] == "zh") h.chinese = (uint32_t)i;
-        if (t->codes[i] == "zh-Hant") h.chinese_t = (uint32_t)i;
+        if (strcmp(t->codes[i], "zh") == 0) h.chinese = (uint32_t)i;
+        if (strcmp(t->codes[i], "zh-Hant") == 0) h.chinese_t = (uint32_t)i;
       }
       if (!h.ok()) h = cld::HintView();
     }
@@ -395,6 +410,12 @@ struct Device {
 };
 
 std::mutex g_init_mu;
+// Table generation lock: every batch call holds it shared from its host-side
+// ApplyHints through its last kernel, a table swap (cld_load_data_*,
+// cld_unload_data) holds it exclusively.  So no call reads host tables that
+// are being replaced, and a call's priors and device tables come from the
+// same table set.  Order: g_init_mu, then g_swap_mu, then a device's mu.
+std::shared_mutex g_swap_mu;
 bool g_inited = false;
 int g_init_rc = CLD_ENODEV;
 HostTables g_tab;
@@ -553,6 +574,9 @@ int init_device(Device* d) {
 }
 
 constexpr uint32_t kPrepFlags = CLD_FLAG_STRIP_EXTRAS | CLD_FLAG_CSTRING;
+// the reference's public flags the kernels apply; its debug-output flags are accepted and ignored
+constexpr uint32_t kCldFlags = CLD_FLAG_SCORE_AS_QUADS | CLD_FLAG_BEST_EFFORT;
+constexpr uint32_t kPublicFlags = kCldFlags | CLD_FLAG_DEBUG_MASK;
 
 // Text preparation (handlers.go:150-151) on device d: documents [buf, offs) ->
 // prepared documents in d->d_sbuf / d->d_soffs.  cap_bytes bounds offs[n].
@@ -570,9 +594,10 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 // Enqueue the whole pipeline for n documents already on device d.  special /
 // priors (device, nullable): cld_detect_batch_ex's per-document routing bits
 // and ApplyHints langprobs (16 per document); such documents skip the wave and
-// long kernels and run whole in k_general.
+// long kernels and run whole in k_general.  cflags: CLD2's public flags (kCldFlags).
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
-            const uint8_t* special = nullptr, const uint32_t* priors = nullptr) {
+            const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0) {
+  cflags &= kCldFlags;
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (d->n_slots > 0 && d->long_order) {
@@ -593,10 +618,11 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
   if (d->front == 1)
-    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, special, sp_list, sp_ctr, s));
+    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, special, sp_list, sp_ctr,
+                            cflags, s));
   else
     HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
-                           sp_ctr, s));
+                           sp_ctr, cflags, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
@@ -606,14 +632,14 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
-                           d->d_prof ? d->d_prof + 8 : nullptr, s));
+                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, s));
+                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, s));
   } else {
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, s));
+                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, cflags, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -822,10 +848,10 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     const uint8_t* kbuf = h.d_in - base;
     if (flags & kPrepFlags) {
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
-      rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream);
+      rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream, nullptr, nullptr, flags);
     } else {
       rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream, special ? h.d_sp : nullptr,
-                   (special && priors) ? h.d_pri : nullptr);
+                   (special && priors) ? h.d_pri : nullptr, flags);
     }
     if (rc) break;
     HIP_OK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
@@ -882,7 +908,7 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
 // [0, n) to *chunks and their counts to *counts.
 int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out,
                   const uint8_t* special, const uint32_t* priors, std::vector<cld_chunk>* chunks,
-                  std::vector<int32_t>* counts) {
+                  std::vector<int32_t>* counts, uint32_t cflags) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   Device::Vec& V = d->vec;
@@ -926,7 +952,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     if (priors) HIP_OK(hipMemcpyAsync(V.pri, priors + 16 * a, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
     HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
-                                  special ? V.sp : nullptr, priors ? V.pri : nullptr, V.pool, V.pool_off, V.nch, s));
+                                  special ? V.sp : nullptr, priors ? V.pri : nullptr, V.pool, V.pool_off, V.nch,
+                                  cflags & kCldFlags, s));
     nch.resize(m);
     HIP_OK(hipMemcpyAsync(out + a, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -970,6 +997,7 @@ int host_tables(const char* tables_path) {
 // load keeps the tables in use and returns an error instead of leaving none.
 int load_dynamic(const uint8_t* data, size_t len, const std::string& label) {
   std::lock_guard<std::mutex> lk(g_init_mu);
+  std::unique_lock<std::shared_mutex> tl(g_swap_mu);   // no batch call is between its hints and its kernels
   int rc = host_tables(nullptr);
   if (rc) return rc;
   HostTables nt;
@@ -1033,9 +1061,27 @@ int cld_init(const char* tables_path, int n_devices) {
   }
   if (n_devices <= 0 || n_devices > count) n_devices = count;
   if (const char* e = getenv("CLD_MI355X_DEVICES")) n_devices = std::max(1, std::min(count, atoi(e)));
-  for (int i = 0; i < n_devices; ++i) {
+  std::vector<int> ids;
+  for (int i = 0; i < n_devices; ++i) ids.push_back(i);
+  // CLD_MI355X_DEVICE_MAP="0,0": one context per listed HIP ordinal, repeats
+  // allowed -- the multi-device fan-out of the batch entry points (one host
+  // thread per context, each with its own streams, tables and scratch) then
+  // runs on a one-GPU box too (tests/test_gpu_streams.py)
+  if (const char* e = getenv("CLD_MI355X_DEVICE_MAP")) {
+    ids.clear();
+    for (const char* p = e; *p;) {
+      char* end = nullptr;
+      const long v = strtol(p, &end, 10);
+      if (end == p || v < 0 || v >= count) return g_init_rc = CLD_EINVAL;
+      ids.push_back((int)v);
+      p = *end == ',' ? end + 1 : end;
+      if (*end && *end != ',') return g_init_rc = CLD_EINVAL;
+    }
+    if (ids.empty()) return g_init_rc = CLD_EINVAL;
+  }
+  for (int id : ids) {
     Device* d = new Device();
-    d->id = i;
+    d->id = id;
     if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
     g_devs.push_back(d);
   }
@@ -1116,6 +1162,7 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
 
 void cld_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_init_mu);
+  std::unique_lock<std::shared_mutex> tl(g_swap_mu);
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
@@ -1148,13 +1195,14 @@ void cld_shutdown(void) {
 }
 
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_result* out, uint32_t flags) {
-  if ((flags & ~kPrepFlags) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
+  if ((flags & ~(kPrepFlags | kPublicFlags)) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
   if (n > 0x7FFFFFFFu) return CLD_EINVAL;
   for (size_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return CLD_EINVAL;
   int rc = cld_init(nullptr, 0);
   if (rc) return rc;
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   const size_t ndev = g_devs.size();
   // Shard by byte count (+ a per-document weight) at document boundaries.
   std::vector<size_t> cut(ndev + 1, 0);
@@ -1178,6 +1226,7 @@ int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld
     std::lock_guard<std::mutex> lk(g_init_mu);
     if (int rc = host_tables(nullptr)) return rc;
   }
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   const cld::HintView& v = g_tab.hints;
   if (!v.ok()) return CLD_EINVAL;               // tables without the hint sections
   int16_t p[cld::kMaxPriors] = {};
@@ -1192,7 +1241,8 @@ int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld
 namespace {
 // ApplyHints per document on the host (a few table lookups, and for HTML a
 // scan of the first 8 KB), split over host threads: the routing bits and,
-// when any document has a prior, the 16 langprobs per document.
+// when any document has a prior, the 16 langprobs per document.  The caller
+// holds g_swap_mu (shared).
 int apply_hints(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints, bool html,
                 std::vector<uint8_t>* special, std::vector<uint32_t>* priors) {
   if (html && !g_tab.offs.ent_names) return CLD_EINVAL;     // tables without the HTML sections
@@ -1240,11 +1290,13 @@ extern "C" {
 
 int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
                         uint32_t flags, cld_result* out) {
-  if ((flags & ~CLD_FLAG_HTML) != 0) return CLD_EINVAL;
+  if ((flags & ~(CLD_FLAG_HTML | kPublicFlags)) != 0) return CLD_EINVAL;
   if (int rc = check_batch(buf, offsets, n, out)) return rc;
   if (n == 0) return CLD_OK;
   int rc = cld_init(nullptr, 0);
   if (rc) return rc;
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+  const uint32_t cf = flags & kCldFlags;
   std::vector<uint8_t> special;
   std::vector<uint32_t> priors;
   const bool html = (flags & CLD_FLAG_HTML) != 0;
@@ -1254,13 +1306,13 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
   const size_t ndev = g_devs.size();
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
-  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, 0, sp, pr);
+  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, cf, sp, pr);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
     th.emplace_back([&, k] {
-      rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], 0,
+      rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], cf,
                               sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr);
     });
   }
@@ -1272,12 +1324,13 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
 int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
                          uint32_t flags, cld_result* out, cld_chunk* chunks, size_t chunk_cap,
                          uint64_t* chunk_offsets) {
-  if ((flags & ~CLD_FLAG_HTML) != 0 || !chunk_offsets || (chunk_cap > 0 && !chunks)) return CLD_EINVAL;
+  if ((flags & ~(CLD_FLAG_HTML | kPublicFlags)) != 0 || !chunk_offsets || (chunk_cap > 0 && !chunks)) return CLD_EINVAL;
   if (int rc = check_batch(buf, offsets, n, out)) return rc;
   chunk_offsets[0] = 0;
   if (n == 0) return CLD_OK;
   int rc = cld_init(nullptr, 0);
   if (rc) return rc;
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   std::vector<uint8_t> special;
   std::vector<uint32_t> priors;
   const bool html = (flags & CLD_FLAG_HTML) != 0;
@@ -1295,7 +1348,8 @@ int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, 
     if (cut[k + 1] == cut[k]) continue;
     auto job = [&, k] {
       rcs[k] = run_vec_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k],
-                             sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr, &vs[k], &cs[k]);
+                             sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr, &vs[k], &cs[k],
+                             flags & kCldFlags);
     };
     if (ndev == 1) job(); else th.emplace_back(job);
   }
@@ -1318,6 +1372,7 @@ int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_
   if (rc) return rc;
   if (device < 0 || device >= (int)g_devs.size()) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   Device* d = g_devs[device];
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
@@ -1328,19 +1383,20 @@ int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_
 
 int cld_detect_batch_device_ex(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,
                                uint64_t buf_bytes, cld_result* d_out, uint32_t flags, void* stream) {
-  if ((flags & ~kPrepFlags) != 0) return CLD_EINVAL;
+  if ((flags & ~(kPrepFlags | kPublicFlags)) != 0) return CLD_EINVAL;
   int rc = cld_init(nullptr, 0);
   if (rc) return rc;
   if (device < 0 || device >= (int)g_devs.size() || n > 0x7FFFFFFFu) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   Device* d = g_devs[device];
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   if (d->ev_used >= 4096) d->ev_used = 0;
-  if (!(flags & kPrepFlags)) return enqueue(d, d_buf, d_offsets, n, d_out, s);
+  if (!(flags & kPrepFlags)) return enqueue(d, d_buf, d_offsets, n, d_out, s, nullptr, nullptr, flags);
   if ((rc = enqueue_prepare(d, d_buf, d_offsets, n, buf_bytes, flags, s))) return rc;
-  return enqueue(d, d->d_sbuf, d->d_soffs, n, d_out, s);
+  return enqueue(d, d->d_sbuf, d->d_soffs, n, d_out, s, nullptr, nullptr, flags);
 }
 
 int cld_prepare_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, uint32_t flags,
@@ -1390,20 +1446,25 @@ void cld_host_free(void* p) {
 }
 
 const char* cld_language_code(int lang) {
-  if (cld_init(nullptr, 0) != CLD_OK && g_tab.codes.empty()) return "un";
+  cld_init(nullptr, 0);
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+  if (g_tab.codes.empty()) return "un";
   if (lang < 0 || (size_t)lang >= g_tab.codes.size()) lang = (int)g_tab.meta.unknown_language;
-  return g_tab.codes[lang].c_str();
+  return (size_t)lang < g_tab.codes.size() ? g_tab.codes[lang] : "un";
 }
 
 const char* cld_language_name(int lang) {
-  if (cld_init(nullptr, 0) != CLD_OK && g_tab.names.empty()) return "Unknown";
+  cld_init(nullptr, 0);
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+  if (g_tab.names.empty()) return "Unknown";
   if (lang < 0 || (size_t)lang >= g_tab.names.size()) lang = (int)g_tab.meta.unknown_language;
-  return g_tab.names[lang].c_str();
+  return (size_t)lang < g_tab.names.size() ? g_tab.names[lang] : "Unknown";
 }
 
 const char* cld_version(void) {
   cld_init(nullptr, 0);
-  return g_tab.version.c_str();
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+  return intern(g_tab.version);
 }
 
 int cld_load_data_from_file(const char* path) {
@@ -1422,6 +1483,7 @@ int cld_load_data_from_raw_address(const void* raw, uint32_t length) {
 
 int cld_unload_data(void) {
   std::lock_guard<std::mutex> lk(g_init_mu);
+  std::unique_lock<std::shared_mutex> tl(g_swap_mu);
   if (!g_dynamic) return CLD_OK;
   HostTables nt;
   int rc = load_tables(g_base_path.c_str(), &nt);
@@ -1509,7 +1571,10 @@ const char* detect_language(const char* text) {
   }
   lk.unlock();
   int lang = p.res.summary_lang;
-  if (lang == (int)g_tab.meta.unknown_language) lang = (int)g_tab.meta.english;  // compact_lang_det.cc:91-93
+  {
+    std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+    if (lang == (int)g_tab.meta.unknown_language) lang = (int)g_tab.meta.english;  // compact_lang_det.cc:91-93
+  }
   return cld_language_code(lang);
 }
 

@@ -1108,8 +1108,10 @@ __device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
 // they could change exists -- otherwise they are no-ops there too.  Returns 1
 // with the result written, or 0 when the first pass is not good enough and the
 // Repeats pass must follow (never when `final`).
+// best_effort: kCLDFlagBestEffort (:1998-2000, :1493): no unreliable-language
+// removal and no UNKNOWN for a small return percent.
 __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
-                               int lane) {
+                               int lane, bool best_effort = false) {
   if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
     if (lane == 0) refine_scored_close_pairs(T, dt);
     wsync();
@@ -1126,7 +1128,7 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
   ok = rdl(ok, 0);
   if (ok) {
     bool unrel = false;
-    if (lane < 24) {
+    if (lane < 24 && !best_effort) {
       const int bytes = dt.value[lane];
       unrel = dt.key[lane] != kUnusedKey && bytes != 0 && dt.rel[lane] / bytes < 41;
     }
@@ -1138,7 +1140,7 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
     }
     if (lane == 0) {
       bool rel;
-      const int summary = calc_summary_lang(T, total, x, rel);
+      const int summary = calc_summary_lang(T, total, x, rel, best_effort);
       write_result(out, x, summary, rel);
     }
   }
@@ -1149,7 +1151,7 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
 // ------------------------------------------------------ the document
 template <int CAP>
 __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
-                       cld_result* __restrict__ out, unsigned long long* __restrict__ prof) {
+                       cld_result* __restrict__ out, unsigned long long* __restrict__ prof, uint32_t cflags) {
   // optional per-stage cycle accounting (CLD_PROFILE_STAGES=1): 0 load, 1 span,
   // 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level
   long long t_stage = prof ? (long long)clock64() : 0;
@@ -1184,7 +1186,8 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     tb = lower_span<CAP>(T, s, tb, lane);
     mark(2);
     if (tb < 0) return false;
-    const int rt = rtype_of(T, ulscript);
+    int rt = rtype_of(T, ulscript);
+    if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
     if (rt == RTypeNone || rt == RTypeOne) {
       if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
       wsync();
@@ -1209,7 +1212,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     }
     total += tb;
   }
-  const int ok = finish_document(T, s.dt, total, false, out, lane);
+  const int ok = finish_document(T, s.dt, total, false, out, lane, (cflags & kCLDFlagBestEffort) != 0);
   mark(6);
   return ok != 0;
 }

@@ -23,6 +23,7 @@ import json
 import cld_amd
 
 BODY_LIMIT_BYTES = 1048576     # main.go:32
+DRAIN_LIMIT = 64 << 20         # an oversized body's remainder is read and discarded up to this
 CONTENT_TYPE_OUT = "application/json; charset=utf-8"
 
 USAGE = {"result": {"id": "language-detector", "name": "language-detector",
@@ -128,8 +129,8 @@ class LanguageDetectorService:
         return status, _dump({"response": out})
 
 
-def serve(service, port=3000):
-    """Blocking HTTP server around `service.handle` (stdlib, threads)."""
+def make_server(service, port=3000, host=""):
+    """HTTP server around `service.handle` (stdlib, one thread per connection)."""
     from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
     class H(BaseHTTPRequestHandler):
@@ -137,13 +138,36 @@ def serve(service, port=3000):
             n = int(self.headers.get("Content-Length") or 0)
             # io.LimitReader (handlers.go:40): never read past the limit
             body = self.rfile.read(min(n, service.body_limit)) if n > 0 else b""
+            # the rest of an oversized body: discard it (up to DRAIN_LIMIT) so
+            # the reply is not lost to a reset when the socket closes with
+            # unread data, as net/http does; beyond that, close after replying
+            left = n - len(body)
+            close = False
+            while left > 0:
+                if n - service.body_limit > DRAIN_LIMIT:
+                    close = True
+                    break
+                got = self.rfile.read(min(left, 1 << 16))
+                if not got:
+                    break
+                left -= len(got)
             status, out = service.handle(method, self.path, self.headers.get("Content-Type", ""), body)
             self.send_response(status)
             if out or status != 200:
                 self.send_header("Content-Type", CONTENT_TYPE_OUT)
             self.send_header("Content-Length", str(len(out)))
+            if close:
+                self.send_header("Connection", "close")
+                self.close_connection = True
             self.end_headers()
             self.wfile.write(out)
+            if close:
+                import socket
+                self.wfile.flush()
+                try:
+                    self.connection.shutdown(socket.SHUT_WR)
+                except OSError:
+                    pass
 
         def do_GET(self):
             self._reply("GET")
@@ -154,4 +178,9 @@ def serve(service, port=3000):
         def log_message(self, *a):
             pass
 
-    ThreadingHTTPServer(("", port), H).serve_forever()
+    return ThreadingHTTPServer((host, port), H)
+
+
+def serve(service, port=3000):
+    """Blocking HTTP server around `service.handle`."""
+    make_server(service, port).serve_forever()

@@ -82,6 +82,8 @@ enum {
 #define kCLDFlagTop40 8
 #define kCLDFlagShort 16
 #define kCLDFlagUseWords 64
+/* compact_lang_det.h:343, :349 (the public result-affecting flags) */
+#define kCLDFlagScoreAsQuads 0x0100
 #define kCLDFlagBestEffort 0x4000
 /* cldutil.cc:43-44 */
 #define kMinGramCount 3
@@ -1274,6 +1276,7 @@ struct cldo_ctx {
   uint32_t priors[16];                         /* ApplyHints result: boost latn[4] othr[4], whack latn[4] othr[4] */
   rvec_t* vec;                                 /* ResultChunkVector being built, or NULL */
   offmap_t map_orig, map_low;                  /* the scanner's maps (vec mode) */
+  int cflags;                                  /* the caller's flags (ExtDetectLanguageSummary `flags`) */
 };
 
 static void tracef(struct cldo_ctx* c, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -1882,6 +1885,7 @@ static void hitbuf_init(hitbuf_t* hb) {        /* ScoringHitBuffer::init (.h:187
 /* ScoreOneScriptSpan :1302-1333 and its three cases :1132-1277 */
 static void score_one_script_span(struct cldo_ctx* c, ctx_t* cx, const span_t* span, doctote_t* dt) {
   int rt = rtype_of(span->ulscript);
+  if ((c->cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   /* :1318-1320 */
   if (c->trace) tracef(c, "span %s %d", script_code(span->ulscript), span->text_bytes);
   if (rt == RTypeNone || rt == RTypeOne) {
     int bytes = span->text_bytes;
@@ -2102,7 +2106,7 @@ static void trace_doctote(struct cldo_ctx* c, const doctote_t* d) {
  * unrolled into a pass loop with identical flag transitions. */
 static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cldo_result* r) {
   const int unk = (int)T.meta.unknown_language;
-  int flags = 0;
+  int flags = c->cflags & (kCLDFlagScoreAsQuads | kCLDFlagBestEffort);   /* the caller's flags (:1707) */
   r->passes = 0;
   for (;;) {
     r->passes++;
@@ -2170,7 +2174,7 @@ static int detect_summary_v2(struct cldo_ctx* c, const uint8_t* buf, int len, cl
     else if (rel && pct3[0] >= kGoodLang1Percent) good = 1;
     else if (rel && pct3[0] + pct3[1] >= kGoodLang1and2Percent) good = 1;
     if (good) {
-      remove_unreliable_languages(&dt);
+      if (!(flags & kCLDFlagBestEffort)) remove_unreliable_languages(&dt);   /* :1998-2000 */
       doctote_sort(&dt, 3);
       extract_lang_etc(&dt, total, rp3, lang3, pct3, ns3, &tb, &rel);
       int summary;
@@ -2217,6 +2221,7 @@ void cldo_ctx_free(cldo_ctx* c) {
 }
 void cldo_set_trace(cldo_ctx* c, cldo_trace_fn fn, void* arg) { c->trace = fn; c->trace_arg = arg; }
 void cldo_set_trace_text(cldo_ctx* c, int on) { c->trace_text = on; }
+void cldo_set_flags(cldo_ctx* c, int flags) { c->cflags = flags; }
 
 /* The document is copied into a buffer followed by 16 NUL bytes, matching
  * the NUL-terminated C string the reference wrapper receives. */
@@ -2274,7 +2279,7 @@ int cldo_meta(int which) {
 #include <pthread.h>
 typedef struct {
   const char* buf; const uint64_t* offs; int lo, hi; cldo_result* out;
-  const uint8_t* plain; const uint32_t* priors;
+  const uint8_t* plain; const uint32_t* priors; int flags;
 } job_t;
 int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
                          const uint32_t* priors, cldo_result* out, int threads);
@@ -2294,6 +2299,7 @@ int cldo_detect_ex(cldo_ctx* c, const char* text, int len, int is_plain_text, co
 static void* run_job(void* a) {
   job_t* j = (job_t*)a;
   cldo_ctx* c = cldo_ctx_new();
+  c->cflags = j->flags;
   for (int i = j->lo; i < j->hi; ++i)
     cldo_detect_ex(c, j->buf + j->offs[i], (int)(j->offs[i + 1] - j->offs[i]),
                    j->plain ? j->plain[i] : 1, j->priors ? j->priors + 16 * (size_t)i : NULL, &j->out[i]);
@@ -2305,6 +2311,10 @@ int cldo_detect_batch(const char* buf, const uint64_t* offsets, int n, cldo_resu
 }
 int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
                          const uint32_t* priors, cldo_result* out, int threads) {
+  return cldo_detect_batch_flags(buf, offsets, n, plain, priors, out, threads, 0);
+}
+int cldo_detect_batch_flags(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
+                            const uint32_t* priors, cldo_result* out, int threads, int flags) {
   if (!T.loaded) return -1;
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
@@ -2312,6 +2322,7 @@ int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const 
   job_t jobs[256];
   for (int t = 0; t < threads; ++t) {
     jobs[t].buf = buf; jobs[t].offs = offsets; jobs[t].out = out; jobs[t].plain = plain; jobs[t].priors = priors;
+    jobs[t].flags = flags;
     jobs[t].lo = (int)((int64_t)n * t / threads); jobs[t].hi = (int)((int64_t)n * (t + 1) / threads);
     pthread_create(&th[t], NULL, run_job, &jobs[t]);
   }

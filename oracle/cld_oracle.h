@@ -49,6 +49,11 @@ int cldo_detect_vec(cldo_ctx* c, const char* text, int len, int is_plain_text, c
                     cldo_result* r, cldo_rchunk* out, int cap);
 int cldo_detect_batch_ex(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
                          const uint32_t* priors, cldo_result* out, int threads);
+/* The caller's ExtDetectLanguageSummary flags (compact_lang_det.h:343-349):
+ * 0x0100 kCLDFlagScoreAsQuads, 0x4000 kCLDFlagBestEffort; others ignored. */
+void cldo_set_flags(cldo_ctx* c, int flags);
+int cldo_detect_batch_flags(const char* buf, const uint64_t* offsets, int n, const uint8_t* plain,
+                            const uint32_t* priors, cldo_result* out, int threads, int flags);
 /* handlers.go:150-151 text preparation: flags 1 = StripExtras, 2 = C-string cut.
  * out capacity: offsets[n]-offsets[0] + n bytes. */
 int cldo_prepare_batch(const char* buf, const uint64_t* offsets, int n, int flags, char* out,

@@ -107,25 +107,27 @@ class Oracle:
             raise RuntimeError("cldo_detect_batch rc=%d" % rc)
         return out
 
-    def detect_batch_ex(self, buf, offsets, plain=None, priors=None, threads=1):
+    def detect_batch_ex(self, buf, offsets, plain=None, priors=None, threads=1, flags=0):
         """is_plain_text per document (uint8, None = all plain) and the ApplyHints
-        langprobs (uint32 [n, 16], None = no hints)."""
+        langprobs (uint32 [n, 16], None = no hints); flags: the caller's
+        ExtDetectLanguageSummary flags (0x0100 ScoreAsQuads, 0x4000 BestEffort)."""
         buf = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = len(offsets) - 1
         out = np.zeros(n, dtype=RESULT_DTYPE)
         pl = None if plain is None else np.ascontiguousarray(plain, dtype=np.uint8)
         pr = None if priors is None else np.ascontiguousarray(priors, dtype=np.uint32).reshape(n, 16)
-        self.lib.cldo_detect_batch_ex.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] + [ctypes.c_void_p] * 3 + \
-            [ctypes.c_int]
-        rc = self.lib.cldo_detect_batch_ex(buf.ctypes.data, offsets.ctypes.data, n,
-                                           None if pl is None else pl.ctypes.data,
-                                           None if pr is None else pr.ctypes.data, out.ctypes.data, threads)
+        self.lib.cldo_detect_batch_flags.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] + [ctypes.c_void_p] * 3 + \
+            [ctypes.c_int, ctypes.c_int]
+        rc = self.lib.cldo_detect_batch_flags(buf.ctypes.data, offsets.ctypes.data, n,
+                                              None if pl is None else pl.ctypes.data,
+                                              None if pr is None else pr.ctypes.data, out.ctypes.data, threads,
+                                              int(flags))
         if rc != 0:
             raise RuntimeError("cldo_detect_batch_ex rc=%d" % rc)
         return out
 
-    def detect_vec(self, doc, plain=True, priors=None):
+    def detect_vec(self, doc, plain=True, priors=None, flags=0):
         """ExtDetectLanguageSummary with a ResultChunkVector -> (Result, chunks
         as a structured array offset/bytes/lang1)."""
         b = bytes(doc)
@@ -135,8 +137,11 @@ class Oracle:
         pr = None if priors is None else np.ascontiguousarray(priors, dtype=np.uint32)
         self.lib.cldo_detect_vec.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.POINTER(Result), ctypes.c_void_p, ctypes.c_int]
+        self.lib.cldo_set_flags.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        self.lib.cldo_set_flags(self.ctx, int(flags))
         n = self.lib.cldo_detect_vec(self.ctx, b, len(b), int(plain), None if pr is None else pr.ctypes.data,
                                      ctypes.byref(r), ch.ctypes.data, cap)
+        self.lib.cldo_set_flags(self.ctx, 0)
         if n < 0:
             raise RuntimeError("cldo_detect_vec rc=%d" % n)
         return r, ch[:n].copy()

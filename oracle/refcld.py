@@ -25,8 +25,38 @@ class Hints(ctypes.Structure):
                 ("encoding_hint", ctypes.c_int32), ("language_hint", ctypes.c_int32)]
 
 
+MANIFEST = os.path.join(HERE, "_ref", "librefcld2.manifest.json")
+
+
 def available():
     return os.path.exists(LIB) or os.path.isdir("/root/reference/cld2/internal")
+
+
+def verify_build():
+    """Raise unless oracle/_ref/librefcld2.so is present and was built from
+    this tree's recipe: its manifest (oracle/refcld/manifest.py, written at
+    link time) must name this library's sha256 and the current sha256 of
+    oracle/refcld/refcld.cc and oracle/refcld/Makefile.  Returns the manifest."""
+    import hashlib
+    import json
+
+    def sha(p):
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    if not os.path.exists(LIB):
+        raise RuntimeError("reference checker %s is not built (oracle/refcld/Makefile)" % LIB)
+    if not os.path.exists(MANIFEST):
+        raise RuntimeError("reference checker has no build manifest %s" % MANIFEST)
+    with open(MANIFEST) as f:
+        m = json.load(f)
+    if m["library"]["sha256"] != sha(LIB):
+        raise RuntimeError("librefcld2.so does not match its build manifest")
+    for rel, h in m["recipe"].items():
+        if sha(os.path.join(ROOT, rel)) != h:
+            raise RuntimeError("librefcld2.so was built from another %s than this tree's" % rel)
+    if len(m.get("reference_sources", {})) < 18:
+        raise RuntimeError("librefcld2.so manifest lists too few reference sources")
+    return m
 
 
 def build():
@@ -52,6 +82,8 @@ class RefCLD:
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.refcld_detect_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        lib.refcld_detect_batch_flags.argtypes = lib.refcld_detect_batch.argtypes + [ctypes.c_int]
+        lib.refcld_detect_flags.argtypes = lib.refcld_detect.argtypes + [ctypes.c_int]
         fd, path = tempfile.mkstemp(suffix=".cld2_data_file00")
         with os.fdopen(fd, "wb") as f:
             f.write(cld2_data_file.build(cldt.Blob.load(cldt_path)))
@@ -60,7 +92,8 @@ class RefCLD:
         if rc != 0:
             raise RuntimeError("reference loader rejected %s" % path)
 
-    def detect_batch(self, buf, offsets, plain=None, hints=None, threads=1):
+    def detect_batch(self, buf, offsets, plain=None, hints=None, threads=1, flags=0):
+        """flags: ExtDetectLanguageSummary's (0x0100 kCLDFlagScoreAsQuads, 0x4000 kCLDFlagBestEffort)."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = len(offsets) - 1
@@ -71,14 +104,14 @@ class RefCLD:
             harr = (Hints * n)(*[Hints(h.content_language_hint, h.tld_hint, h.encoding_hint, h.language_hint)
                                  for h in hints])
         bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
-        rc = self.lib.refcld_detect_batch(bptr, offsets.ctypes.data, n, None if pl is None else pl.ctypes.data,
-                                          ctypes.cast(harr, ctypes.c_void_p) if harr is not None else None,
-                                          out.ctypes.data, threads)
+        rc = self.lib.refcld_detect_batch_flags(bptr, offsets.ctypes.data, n, None if pl is None else pl.ctypes.data,
+                                                ctypes.cast(harr, ctypes.c_void_p) if harr is not None else None,
+                                                out.ctypes.data, threads, int(flags))
         if rc != 0:
             raise RuntimeError("refcld_detect_batch rc=%d" % rc)
         return out
 
-    def detect_vec(self, doc, plain=True, hints=None):
+    def detect_vec(self, doc, plain=True, hints=None, flags=0):
         """ExtDetectLanguageSummary with a ResultChunkVector -> (result, chunks)."""
         b = bytes(doc)
         r = np.zeros(1, dtype=RESULT_DTYPE)
@@ -87,8 +120,8 @@ class RefCLD:
         h = None
         if hints is not None:
             h = Hints(hints.content_language_hint, hints.tld_hint, hints.encoding_hint, hints.language_hint)
-        self.lib.refcld_detect(b, len(b), int(plain), ctypes.byref(h) if h is not None else None,
-                               r.ctypes.data, ch.ctypes.data, cap)
+        self.lib.refcld_detect_flags(b, len(b), int(plain), ctypes.byref(h) if h is not None else None,
+                                     r.ctypes.data, ch.ctypes.data, cap, int(flags))
         return r[0], ch[:int(r[0]["n_chunks"])].copy()
 
 

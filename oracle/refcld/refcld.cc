@@ -57,8 +57,9 @@ int refcld_load(const char* data_file) {
 
 // One document.  hints == NULL: DetectLanguage's empty hints (compact_lang_det.cc:66-71).
 // chunks != NULL: ExtDetectLanguageSummary with a ResultChunkVector, at most cap entries copied.
+// flags: ExtDetectLanguageSummary's `flags` (compact_lang_det.h:329, :343-349).
 static void detect_one(const char* text, int len, int plain, const refcld_hints* h, refcld_result* r,
-                       refcld_chunk* chunks, int cap, std::string* scratch) {
+                       refcld_chunk* chunks, int cap, std::string* scratch, int flags) {
   scratch->assign(text, (size_t)len);
   scratch->append(16, '\0');                    // NUL-terminated, as the wrapper hands it over
   CLDHints hints = {NULL, "", 23 /* UNKNOWN_ENCODING (encodings.h) */, UNKNOWN_LANGUAGE};
@@ -73,7 +74,7 @@ static void detect_one(const char* text, int len, int plain, const refcld_hints*
   double n3[3];
   bool rel = false;
   ResultChunkVector vec;
-  Language s = ExtDetectLanguageSummary(scratch->data(), len, plain != 0, &hints, 0, l3, p3, n3,
+  Language s = ExtDetectLanguageSummary(scratch->data(), len, plain != 0, &hints, flags, l3, p3, n3,
                                         chunks ? &vec : NULL, &tb, &rel);
   for (int i = 0; i < 3; ++i) { r->lang3[i] = l3[i]; r->percent3[i] = p3[i]; r->normalized3[i] = n3[i]; }
   r->text_bytes = tb;
@@ -89,17 +90,22 @@ static void detect_one(const char* text, int len, int plain, const refcld_hints*
     }
 }
 
-int refcld_detect(const char* text, int len, int plain, const refcld_hints* h, refcld_result* r,
-                  refcld_chunk* chunks, int cap) {
+int refcld_detect_flags(const char* text, int len, int plain, const refcld_hints* h, refcld_result* r,
+                        refcld_chunk* chunks, int cap, int flags) {
   if (!isDataLoaded()) return -1;
   std::string s;
-  detect_one(text, len, plain, h, r, chunks, cap, &s);
+  detect_one(text, len, plain, h, r, chunks, cap, &s, flags);
   return 0;
+}
+
+int refcld_detect(const char* text, int len, int plain, const refcld_hints* h, refcld_result* r,
+                  refcld_chunk* chunks, int cap) {
+  return refcld_detect_flags(text, len, plain, h, r, chunks, cap, 0);
 }
 
 typedef struct {
   const char* buf; const uint64_t* offs; int lo, hi;
-  const uint8_t* plain; const refcld_hints* hints; refcld_result* out;
+  const uint8_t* plain; const refcld_hints* hints; refcld_result* out; int flags;
 } job_t;
 
 static void* run(void* a) {
@@ -107,13 +113,14 @@ static void* run(void* a) {
   std::string s;
   for (int i = j->lo; i < j->hi; ++i)
     detect_one(j->buf + j->offs[i], (int)(j->offs[i + 1] - j->offs[i]), j->plain ? j->plain[i] : 1,
-               j->hints ? j->hints + i : NULL, &j->out[i], NULL, 0, &s);
+               j->hints ? j->hints + i : NULL, &j->out[i], NULL, 0, &s, j->flags);
   return NULL;
 }
 
-// n documents over `threads` pthreads; plain / hints per document or NULL.
-int refcld_detect_batch(const char* buf, const uint64_t* offs, int n, const uint8_t* plain,
-                        const refcld_hints* hints, refcld_result* out, int threads) {
+// n documents over `threads` pthreads; plain / hints per document or NULL;
+// flags as ExtDetectLanguageSummary's, for every document.
+int refcld_detect_batch_flags(const char* buf, const uint64_t* offs, int n, const uint8_t* plain,
+                              const refcld_hints* hints, refcld_result* out, int threads, int flags) {
   if (!isDataLoaded()) return -1;
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
@@ -121,11 +128,16 @@ int refcld_detect_batch(const char* buf, const uint64_t* offs, int n, const uint
   std::vector<job_t> jobs(threads);
   for (int t = 0; t < threads; ++t) {
     jobs[t] = job_t{buf, offs, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads), plain,
-                    hints, out};
+                    hints, out, flags};
     pthread_create(&th[t], NULL, run, &jobs[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
   return 0;
+}
+
+int refcld_detect_batch(const char* buf, const uint64_t* offs, int n, const uint8_t* plain,
+                        const refcld_hints* hints, refcld_result* out, int threads) {
+  return refcld_detect_batch_flags(buf, offs, n, plain, hints, out, threads, 0);
 }
 
 }  // extern "C"

@@ -2,7 +2,9 @@
 box: oracle/_ref/librefcld2.so is the reference's own sources built in its
 dynamic-data mode (oracle/refcld), and it travels with the tree like the
 product's library.  Tables: the same CLDT the GPU loads, written as a
-cld2_data_file00 and read by the reference's loader."""
+cld2_data_file00 and read by the reference's loader.  A missing checker, or
+one not built from this tree's oracle/refcld recipe, is a failure, not a skip
+(refcld.verify_build)."""
 import os
 
 import numpy as np
@@ -17,8 +19,7 @@ FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "nor
 @pytest.fixture(scope="module")
 def ref():
     import refcld
-    if not os.path.exists(refcld.LIB):
-        pytest.skip("oracle/_ref/librefcld2.so not built")
+    refcld.verify_build()
     return refcld.instance(os.environ["CLD_MI355X_TABLES"])
 
 
@@ -46,3 +47,32 @@ def test_gpu_equals_reference_html_hints(gpu, ref):
     hints = random_hints(gpu, 20000, 33)
     same(gpu.detect_batch_ex(buf=buf, offsets=offs, hints=hints), ref.detect_batch(buf, offs, hints=hints, threads=16),
          "c5 hints")
+
+
+@pytest.mark.parametrize("flags", [0x0100, 0x4000, 0x4100], ids=["score_as_quads", "best_effort", "both"])
+def test_gpu_equals_reference_with_flags(gpu, ref, golden, flags):
+    """CLD2's result-affecting flags (compact_lang_det.h:343-349) through every
+    batch entry point: the wave / long kernels (cld_detect_batch), the hinted
+    and HTML paths (cld_detect_batch_ex), each equal to the reference called
+    with the same flags; and the flags change results on these documents."""
+    from test_reference_pin import flag_docs
+    docs = flag_docs(golden)
+    b3, o3 = corpus.c3(300, seed=509)
+    docs += [bytes(b3[o3[i]:o3[i + 1]]) for i in range(300)]
+    buf, offs = gpu.pack(docs)
+    want = ref.detect_batch(buf, offs, threads=16, flags=flags)
+    got = gpu.detect_batch(buf=buf, offsets=offs, flags=flags)
+    same(got, want, "batch flags %#x" % flags)
+    same(gpu.detect_batch_ex(buf=buf, offsets=offs, flags=flags), want, "batch_ex flags %#x" % flags)
+    base = gpu.detect_batch(buf=buf, offsets=offs)
+    assert ((got["summary_lang"] != base["summary_lang"]) | (got["is_reliable"] != base["is_reliable"]) |
+            (got["lang3"] != base["lang3"]).any(axis=1)).sum() >= 10
+    from test_gpu_html_hints import random_hints
+    hb, ho = corpus.html(500, seed=510)
+    n = len(ho) - 1
+    same(gpu.detect_batch_ex(buf=hb, offsets=ho, html=True, flags=flags),
+         ref.detect_batch(hb, ho, plain=np.zeros(n, np.uint8), threads=16, flags=flags), "html flags %#x" % flags)
+    cb, co = corpus.c5(5000, seed=511)
+    hints = random_hints(gpu, 5000, 512)
+    same(gpu.detect_batch_ex(buf=cb, offsets=co, hints=hints, flags=flags),
+         ref.detect_batch(cb, co, hints=hints, threads=16, flags=flags), "hints flags %#x" % flags)

@@ -76,3 +76,53 @@ def test_two_streams_and_a_host_batch(gpu, oracle):
             h.hipFree(p)
     for s in streams:
         h.hipStreamDestroy(s)
+
+
+FAN_OUT = r'''
+import sys
+import numpy as np
+import cld_amd, corpus
+from oracle import Oracle
+from test_gpu_html_hints import priors_for, random_hints
+from test_gpu_parity import assert_same
+cld_amd.init()
+o = Oracle()
+b, off = corpus.c5(30000, seed=121)
+assert_same(cld_amd.detect_batch(buf=b, offsets=off), o.detect_batch(b, off, threads=16), "fan-out batch")
+docs = [cld_amd.last_stats(k).docs for k in (0, 1)]
+assert docs[0] > 0 and docs[1] > 0 and sum(docs) == 30000, docs
+hb, ho = corpus.html(600, seed=122)
+n = len(ho) - 1
+assert_same(cld_amd.detect_batch_ex(buf=hb, offsets=ho, html=True),
+            o.detect_batch_ex(hb, ho, plain=np.zeros(n, np.uint8), priors=priors_for(cld_amd, hb, ho, True, None),
+                              threads=16), "fan-out html")
+hints = random_hints(cld_amd, 30000, 123)
+assert_same(cld_amd.detect_batch_ex(buf=b, offsets=off, hints=hints),
+            o.detect_batch_ex(b, off, priors=priors_for(cld_amd, b, off, False, hints), threads=16), "fan-out hints")
+vb, vo = corpus.c5(800, seed=124)
+res, chunks, coffs = cld_amd.detect_batch_vec(buf=vb, offsets=vo)
+for i in range(len(vo) - 1):
+    r, ch = o.detect_vec(bytes(vb[vo[i]:vo[i + 1]]))
+    assert [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]] == \
+        [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in ch], i
+    assert int(res[i]["summary_lang"]) == r.summary_lang, i
+print("fan-out ok", docs)
+'''
+
+
+def test_multi_context_fan_out():
+    """The batch entry points' multi-device branch (one host thread per
+    context writing out + cut[k]; cld_runtime.cpp cld_detect_batch /
+    _ex / _vec) with GPU 0 registered twice (CLD_MI355X_DEVICE_MAP=0,0: two
+    contexts with their own streams, tables and scratch), in a child process
+    (the runtime's device set is fixed per process).  Both contexts must get
+    documents, and every result must equal the oracle's."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CLD_MI355X_DEVICE_MAP="0,0",
+               PYTHONPATH=os.pathsep.join(os.path.join(root, p) for p in ("language-detector_amd", "oracle", "tests")))
+    r = subprocess.run([sys.executable, "-c", FAN_OUT], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "fan-out ok" in r.stdout

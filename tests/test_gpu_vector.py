@@ -1,7 +1,6 @@
 """cld_detect_batch_vec (ResultChunkVector) on the GPU vs the oracle, chunk for
-chunk, and vs the reference CLD2 itself when oracle/_ref/librefcld2.so is
-present (it travels with the tree; the oracle's vector is pinned to the
-reference by tests/test_reference_pin.py either way)."""
+chunk, and vs the reference CLD2 itself (oracle/_ref/librefcld2.so travels
+with the tree; a missing or stale build fails the test, refcld.verify_build)."""
 import os
 
 import numpy as np
@@ -67,19 +66,20 @@ def test_vector_squeeze_html_hints(gpu, oracle):
 
 def test_vector_matches_reference_directly(gpu):
     """GPU vs the reference's own ExtDetectLanguageSummary vector (the
-    prebuilt checker library), where it is available."""
+    checker library built from oracle/refcld; it must be present and current).
+    Also with the reference's flags (kCLDFlagScoreAsQuads / kCLDFlagBestEffort)."""
     import refcld
-    if not os.path.exists(refcld.LIB):
-        pytest.skip("oracle/_ref/librefcld2.so not built")
+    refcld.verify_build()
     r = refcld.instance(os.environ["CLD_MI355X_TABLES"])
     buf, offs = corpus.c5(1500, seed=15)
-    got, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs)
-    gv = vecs(chunks, coffs)
-    for i in range(len(offs) - 1):
-        doc = bytes(buf[offs[i]:offs[i + 1]])
-        rb, cb = r.detect_vec(doc)
-        assert gv[i] == [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in cb], i
-        assert int(got[i]["summary_lang"]) == int(rb["summary_lang"])
+    for flags in (0, 0x0100, 0x4000):
+        got, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs, flags=flags)
+        gv = vecs(chunks, coffs)
+        for i in range(len(offs) - 1):
+            doc = bytes(buf[offs[i]:offs[i + 1]])
+            rb, cb = r.detect_vec(doc, flags=flags)
+            assert gv[i] == [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in cb], (flags, i)
+            assert int(got[i]["summary_lang"]) == int(rb["summary_lang"]), (flags, i)
 
 
 def test_vector_capacity_contract(gpu):

@@ -159,3 +159,59 @@ def test_result_chunk_vector_equals_reference(oracles):
             (rb["summary_lang"], list(rb["lang3"]), list(rb["percent3"]), rb["text_bytes"], list(rb["normalized3"]))
         multi += len(ca) > 1
     assert multi > 200
+
+
+FLAG_SETS = (0x0100, 0x4000, 0x4100)     # kCLDFlagScoreAsQuads, kCLDFlagBestEffort, both (compact_lang_det.h:343-349)
+
+
+def flag_docs(golden):
+    """Documents where the two flags matter: the reference's unit-test strings
+    (20 script-only languages: ScoreAsQuads sends them to the quadgram path)
+    and short mixed tweets (BestEffort keeps languages under 41% reliability
+    and small top percents)."""
+    docs = [bytes.fromhex(t["text_hex"]) for t in golden["test_pairs"]]
+    docs = [d for d in docs if defined(d)]
+    b, o = corpus.c2(3000, seed=505)
+    docs += [bytes(b[o[i]:o[i + 1]]) for i in range(3000)]
+    b, o = corpus.c5(3000, seed=506)
+    docs += [bytes(b[o[i]:o[i + 1]]) for i in range(3000)]
+    b, o = corpus.c4(1500, seed=507)
+    docs += [bytes(b[o[i]:o[i + 1]]) for i in range(1500)]
+    # a few words each of several languages: small percents
+    b, o = corpus.c2(400, seed=508)
+    for i in range(0, 400, 4):
+        docs.append(b" ".join(bytes(b[o[j]:o[j + 1]])[:24] for j in range(i, i + 4)))
+    return docs
+
+
+@needs_ref
+@pytest.mark.parametrize("flags", FLAG_SETS, ids=["score_as_quads", "best_effort", "both"])
+def test_oracle_equals_reference_with_flags(oracles, golden, flags):
+    """ExtDetectLanguageSummary's result-affecting `flags`: the oracle with the
+    flags = the reference called with them, on both quad tables; and the flag
+    visibly changes results on these documents (else the test proves nothing)."""
+    import cld_amd
+    docs = flag_docs(golden)
+    buf, offs = cld_amd.pack(docs)
+    for tables in (SYNTH, Q0):
+        o = _oracle(oracles, tables)
+        got = o.detect_batch_ex(buf, offs, threads=8, flags=flags)
+        same(got, ref(tables).detect_batch(buf, offs, threads=8, flags=flags), "flags %#x" % flags)
+        base = o.detect_batch_ex(buf, offs, threads=8)
+        changed = (got["summary_lang"] != base["summary_lang"]) | (got["lang3"] != base["lang3"]).any(axis=1) | \
+            (got["is_reliable"] != base["is_reliable"])
+        assert changed.sum() >= 10, "flags %#x changed only %d results" % (flags, changed.sum())
+
+
+@needs_ref
+def test_result_chunk_vector_with_flags_equals_reference(oracles, golden):
+    o = _oracle(oracles, SYNTH)
+    r = ref(SYNTH)
+    docs = flag_docs(golden)[:300]
+    for flags in FLAG_SETS:
+        for doc in docs:
+            ra, ca = o.detect_vec(doc, flags=flags)
+            rb, cb = r.detect_vec(doc, flags=flags)
+            assert _vec(ca) == _vec(cb), (flags, doc[:80])
+            assert (ra.summary_lang, list(ra.lang3), list(ra.percent3)) == \
+                (rb["summary_lang"], list(rb["lang3"]), list(rb["percent3"])), (flags, doc[:80])

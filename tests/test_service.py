@@ -111,6 +111,33 @@ def test_serve_reads_at_most_the_body_limit(main_test):
     assert got == [64]
 
 
+def test_serve_oversized_body_is_drained(main_test, monkeypatch):
+    """A body past the limit is read to its end and discarded (the reply is
+    not lost to a TCP reset, and the keep-alive connection stays usable, as
+    with Go's net/http); past DRAIN_LIMIT the server replies and closes."""
+    import http.client
+    import threading
+    import service as svc_mod
+    svc = LanguageDetectorService(dict(main_test["known_languages"]), detect_codes=stub_codes, body_limit=64)
+    srv = svc_mod.make_server(svc, 0, "127.0.0.1")
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    try:
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        body = b'{"request": [{"text": "hello"}]}' + b" " * 200000
+        for _ in range(2):                                   # same connection twice
+            c.request("POST", "/", body=body, headers={"Content-Type": "application/json"})
+            r = c.getresponse()
+            assert r.status in (200, 203) and b"iso6391code" in r.read()
+        monkeypatch.setattr(svc_mod, "DRAIN_LIMIT", 1000)
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        c.request("POST", "/", body=body, headers={"Content-Type": "application/json"})
+        r = c.getresponse()
+        assert r.status in (200, 203) and r.getheader("Connection") == "close" and b"iso6391code" in r.read()
+    finally:
+        srv.shutdown()
+
+
 def test_handler_edge_semantics(main_test):
     svc = LanguageDetectorService(dict(main_test["known_languages"]), detect_codes=stub_codes)
     ok = b'{"request": [{"text": "hi"}]}'
