@@ -45,14 +45,16 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
 hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
                                  const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
 size_t cld_short_work_bytes();
-// special (nullable): per-document kSpecial* bits; such documents are appended
-// to special_list under counters[special_ctr] instead of being scored.
+// special (nullable): per-document kSpecial* bits; HTML documents are appended
+// to special_list under counters[special_ctr] instead of being scored, hinted
+// ones (kSpecialPriors) are scored with their 16 ApplyHints langprobs
+// (priors + 16 * i; k_long reads the same two arrays).
 // cflags (every launcher): the caller's public CLD2 flags, CLD_FLAG_SCORE_AS_QUADS /
 // CLD_FLAG_BEST_EFFORT (compact_lang_det.h:343, :349), the same for every document.
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
-                           int special_ctr, uint32_t cflags, hipStream_t s);
+                           int special_ctr, uint32_t cflags, const uint32_t* priors, hipStream_t s);
 size_t cld_wave_smem_bytes();
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
@@ -86,6 +88,7 @@ hipError_t cld_launch_strip_write(const uint8_t* buf, const uint64_t* offs, int 
 hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
-                           unsigned long long* prof, uint32_t cflags, hipStream_t s);
+                           unsigned long long* prof, uint32_t cflags, const uint8_t* special,
+                           const uint32_t* priors, hipStream_t s);
 }
 #endif

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
                                                    unsigned long long* __restrict__ prof,
                                                    const uint8_t* __restrict__ special,
                                                    uint32_t* __restrict__ special_list, int special_ctr,
-                                                   uint32_t cflags) {
+                                                   uint32_t cflags, const uint32_t* __restrict__ priors) {
   __shared__ wave::Smem<CAP> smem[WPB];
   // wave index through readfirstlane: the document pointer, its length, the
   // result pointer and the LDS base are then scalars, not VGPRs live across
@@ -197,21 +197,24 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   const int per = ((n + WPB - 1) / WPB + 7) >> 3;          // blocks per XCD slice
   const int i = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * WPB + wv;
   if (i >= n) return;
-  // HTML / hinted documents go straight to k_general's list (cld_detect_batch_ex)
-  if (special && special[i]) {
+  // HTML documents go straight to k_general's list (cld_detect_batch_ex);
+  // hinted plain ones are scored here with their ApplyHints priors
+  const uint8_t sp = special ? special[i] : (uint8_t)0;
+  if (sp & kSpecialHtml) {
     if (lane == 0) {
       special_list[atomicAdd(&counters[special_ctr], 1u)] = (uint32_t)i;
       atomicAdd(&counters[kCtrSpecial], 1u);
     }
     return;
   }
+  const uint32_t* pri = (sp & kSpecialPriors) ? priors + 16ull * i : nullptr;
   const uint64_t a = offs[i], b = offs[i + 1];
   const int64_t len = (int64_t)(b - a);
   bool rq = len > CAP;
   // stage cycles (CLD_PROFILE_STAGES=1) are sampled on one document in 64, so
   // the accounting atomics do not themselves become the bottleneck
   if (!rq) rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr,
-                                 cflags);
+                                 cflags, pri);
   if (rq && lane == 0) {
     uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
     requeue_list[k] = (uint32_t)i;
@@ -239,7 +242,9 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   uint32_t* __restrict__ requeue2,
                                                   uint32_t* __restrict__ counters, uint32_t* trace,
                                                   uint32_t* dbg, uint32_t dbg_doc,
-                                                  unsigned long long* prof, uint32_t cflags) {
+                                                  unsigned long long* prof, uint32_t cflags,
+                                                  const uint8_t* __restrict__ special,
+                                                  const uint32_t* __restrict__ priors) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -270,7 +275,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     }
     wave::wsync();
     if (exact && len <= (uint64_t)lng::kDocCap)
-      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags);
+      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
+                                 (special && (special[i] & kSpecialPriors)) ? priors + 16ull * i : nullptr);
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (lane == 0) {
@@ -414,17 +420,18 @@ int cld_long_waves_per_simd() { return LNG_WPS; }
 hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
-                           unsigned long long* prof, uint32_t cflags, hipStream_t s) {
+                           unsigned long long* prof, uint32_t cflags, const uint8_t* special,
+                           const uint32_t* priors, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors);
   return hipGetLastError();
 }
 
@@ -458,12 +465,12 @@ size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
-                           int special_ctr, uint32_t cflags, hipStream_t s) {
+                           int special_ctr, uint32_t cflags, const uint32_t* priors, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
-                     requeue_list, counters, prof, special, special_list, special_ctr, cflags);
+                     requeue_list, counters, prof, special, special_list, special_ctr, cflags, priors);
   return hipGetLastError();
 }
 

@@ -145,12 +145,15 @@ struct alignas(16) Smem {
     uint16_t pred[kPredictionTableSize]; // Repeats predictor, 16-bit codes (pred_code)
   };
   uint64_t ring[2][4];                   // distinct boosts (as tote adds), latn / othr, oldest first
+  uint64_t pri_add[2][4];                // ApplyHints prior boosts (as tote adds), latn / othr (has_pri)
+  uint8_t pri_wk[2][4];                  // ApplyHints prior whacks: the key each zeroes, 0 = none
+  int has_pri;                           // the document carries priors (cld_detect_batch_ex hints)
   DocTote dt;
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
   uint32_t dbg_pos;
   unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
 };
-static_assert(sizeof(Smem) <= 8640, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
+static_assert(sizeof(Smem) <= 10240, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
 
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
 // 3 repeats, 4 word lists + quad chain, 5 quad hits, 6 octa/uni/bi hits,
@@ -1694,6 +1697,7 @@ __device__ __forceinline__ uint64_t chunk_add(const Slot& S, const Smem& s, uint
   if ((u -= seedn) < nB) return S.be_add[bs + u];
   if ((u -= nB) < nD) return S.d_add[ds + u];
   if ((u -= nD) < nX) return S.x_add[xs + u];
+  if (u - nX >= kMaxBoosts) return s.pri_add[rs][u - nX - kMaxBoosts];   // prior boosts (has_pri)
   const int v = xe - kMaxBoosts + (u - nX);
   return v < 0 ? s.ring[rs][v + kMaxBoosts] : gld(&S.x_add[v]);   // (gld: no LDS/global pointer select)
 }
@@ -1708,7 +1712,7 @@ __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, i
   nB = be - bs;
   nD = s.st[0][k + 1] - ds;
   nX = xe - xs;
-  return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts;
+  return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts + (s.has_pri ? kMaxBoosts : 0);
 }
 
 // ------------------------------------- linearize + chunk + score (one round)
@@ -1839,6 +1843,11 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     }
     const int score_count = nB + seedn;
     wsync();
+    if (s.has_pri) {                         // the prior whacks zero their key's score (ZeroPSLang :39-42)
+      const int wk = lane < 4 ? s.pri_wk[rs][lane] : 0;
+      if (wk) atomicAnd(&s.tote[wk], 0xFFFF0000u);
+      wsync();
+    }
     // top keys of the in-use groups: (uint16 score desc, key asc).  The
     // reference sorts three (CurrentTopThreeKeys) but SetChunkSummary reads
     // only the first two (scoreonescriptspan.cc:60-96), so two rounds.
@@ -2010,8 +2019,17 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
 enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
 template <bool D>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
-                      cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags) {
+                      cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
+                      const uint32_t* __restrict__ pri) {
   const int unk = (int)T.unknown_lang;
+  // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
+  if (lane == 0) s.has_pri = pri != nullptr;
+  if (lane < 16) {
+    const uint32_t lp = pri ? gld(pri + lane) : 0u;
+    if (lane < 8) s.pri_add[lane >> 2][lane & 3] = lp ? tote_adds(T, lp) : 0ull;
+    else s.pri_wk[(lane - 8) >> 2][lane & 3] = (uint8_t)((lp >> 8) & 0xFF);
+  }
+  wsync();
   if (L == 0) {
     if (lane == 0) {
       Extract x;

@@ -593,8 +593,9 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 
 // Enqueue the whole pipeline for n documents already on device d.  special /
 // priors (device, nullable): cld_detect_batch_ex's per-document routing bits
-// and ApplyHints langprobs (16 per document); such documents skip the wave and
-// long kernels and run whole in k_general.  cflags: CLD2's public flags (kCldFlags).
+// and ApplyHints langprobs (16 per document); HTML documents skip the wave and
+// long kernels and run whole in k_general, hinted plain ones take the wave /
+// long kernels with their priors.  cflags: CLD2's public flags (kCldFlags).
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
             const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0) {
   cflags &= kCldFlags;
@@ -622,7 +623,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
                             cflags, s));
   else
     HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
-                           sp_ctr, cflags, s));
+                           sp_ctr, cflags, priors, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
@@ -632,7 +633,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
-                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, s));
+                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, s));

@@ -139,8 +139,8 @@ struct Cfg {
   // Packed tote (kToteNoCarry): a key's 16-bit half can neither wrap nor
   // carry into its neighbour when every add is <= kMaxLgProbScore (the host
   // checks the table at load) and a chunk holds at most NE + ND + NX + 1
-  // emissions plus 4 boosts.
-  static_assert((NE + ND + NX + 5) * kMaxLgProbScore < 65536, "tote headroom");
+  // emissions plus 4 distinct boosts and 4 prior boosts.
+  static_assert((NE + ND + NX + 9) * kMaxLgProbScore < 65536, "tote headroom");
 };
 
 template <int CAP>
@@ -848,7 +848,7 @@ __device__ int cjk_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, in
 // base, index); chunk k closes after base-type emission E_k.
 template <int CAP>
 __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool cjk, int nb, int nd, int nx,
-                            int dummy_off, int& ring_sel, int lane) {
+                            int dummy_off, int& ring_sel, int lane, const uint32_t* __restrict__ pri) {
   using C = Cfg<CAP>;
   const DevTbl& bo = cjk ? T.compat : T.quad;
   const DevTbl& bo2 = cjk ? T.compat : T.quad2;
@@ -981,15 +981,29 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     for (int t = lane; t < ex; t += 64)
       if (s.x_ch[t] <= k) { ++xin; if (s.x_ch[t] == k) add(s.x_ind[t]); }
     xc = wsum(xin);
-    // boosts: the last four distinct langprobs up to the end of this chunk
+    // ScoreBoosts (scoreonescriptspan.cc:125-152): the last four distinct
+    // langprobs up to the end of this chunk and, for a hinted document, the
+    // four ApplyHints prior boosts of this script class (cld_detect_batch_ex:
+    // 16 langprobs per document, boost latn[4] othr[4], whack latn[4] othr[4])
     if (lane < 4) {
       const int u = xc + lane;
       const uint32_t lp = u < 4 ? s.ring[rs][u] : s.x_ind[u - 4];
+      if (lp > 0) add(lp);
+    } else if (pri && lane < 8) {
+      const uint32_t lp = gld(pri + 4 * rs + (lane - 4));
       if (lp > 0) add(lp);
     }
     gm = wor64(gm);
     const int score_count = wsum(cnt);
     wsync();
+    if (pri) {                           // then the whacks zero their top key's score (ZeroPSLang :39-42)
+      const uint32_t wh = lane < 4 ? gld(pri + 8 + 4 * rs + lane) : 0u;
+      if (wh > 0) {
+        const uint32_t k1 = (wh >> 8) & 0xFF;
+        atomicAnd(&s.tote[k1 >> 1], ~(0xFFFFu << ((k1 & 1) * 16)));
+      }
+      wsync();
+    }
     // top keys of the in-use groups: (score desc, key asc).  The reference
     // sorts three (CurrentTopThreeKeys) but SetChunkSummary reads only the
     // first two (scoreonescriptspan.cc:60-96), so two rounds.
@@ -1151,7 +1165,8 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
 // ------------------------------------------------------ the document
 template <int CAP>
 __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
-                       cld_result* __restrict__ out, unsigned long long* __restrict__ prof, uint32_t cflags) {
+                       cld_result* __restrict__ out, unsigned long long* __restrict__ prof, uint32_t cflags,
+                       const uint32_t* __restrict__ pri) {
   // optional per-stage cycle accounting (CLD_PROFILE_STAGES=1): 0 load, 1 span,
   // 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level
   long long t_stage = prof ? (long long)clock64() : 0;
@@ -1207,7 +1222,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       }
       if (endo < tb) return false;     // a second round would be needed (never for short documents)
       int rsel;
-      if (1 < tb && !score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane)) return false;
+      if (1 < tb && !score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane, pri)) return false;
       mark(5);
     }
     total += tb;
