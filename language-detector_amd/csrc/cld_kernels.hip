@@ -197,28 +197,56 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   const int per = ((n + WPB - 1) / WPB + 7) >> 3;          // blocks per XCD slice
   const int i = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * WPB + wv;
   if (i >= n) return;
-  // HTML documents go straight to k_general's list (cld_detect_batch_ex);
-  // hinted plain ones are scored here with their ApplyHints priors
+  // k_route has already listed the HTML documents (for k_general) and those
+  // longer than CAP (for k_long); hinted plain ones are scored here with their
+  // ApplyHints priors
   const uint8_t sp = special ? special[i] : (uint8_t)0;
-  if (sp & kSpecialHtml) {
-    if (lane == 0) {
-      special_list[atomicAdd(&counters[special_ctr], 1u)] = (uint32_t)i;
-      atomicAdd(&counters[kCtrSpecial], 1u);
-    }
-    return;
-  }
+  if (sp & kSpecialHtml) return;
   const uint32_t* pri = (sp & kSpecialPriors) ? priors + 16ull * i : nullptr;
   const uint64_t a = offs[i], b = offs[i + 1];
   const int64_t len = (int64_t)(b - a);
-  bool rq = len > CAP;
+  if (len > CAP) return;
   // stage cycles (CLD_PROFILE_STAGES=1) are sampled on one document in 64, so
   // the accounting atomics do not themselves become the bottleneck
-  if (!rq) rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr,
-                                 cflags, pri);
-  if (rq && lane == 0) {
+  const bool rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr,
+                                     cflags, pri);
+  if (rq && lane == 0) {                       // rare (state-machine or capacity cases)
     uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
     requeue_list[k] = (uint32_t)i;
   }
+}
+
+// Appends `val` of every lane with `pred` to list under *ctr with one atomic
+// per wavefront (all 64 lanes call it).
+__device__ __forceinline__ void wave_append(bool pred, uint32_t* ctr, uint32_t* list, uint32_t val, uint32_t* ctr2) {
+  const uint64_t m = __ballot(pred);
+  if (!m) return;
+  const int leader = __builtin_ctzll(m), lane = (int)(threadIdx.x & 63);
+  uint32_t base = 0;
+  if (lane == leader) {
+    base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    if (ctr2) atomicAdd(ctr2, (uint32_t)__popcll(m));
+  }
+  base = (uint32_t)__shfl((int)base, leader, 64);
+  if (pred) list[base + __popcll(m & wave::lanemask_lt(lane))] = val;
+}
+
+// Routing before k_wave, one thread per document: HTML documents to
+// k_general's list, documents longer than k_wave's CAP to k_long's, each with
+// one atomic per wavefront instead of one per document (a batch of 100K pages
+// used to queue every page through the same counter from k_wave).
+__global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs, int n,
+                                              const uint8_t* __restrict__ special, int cap,
+                                              uint32_t* __restrict__ counters, uint32_t* __restrict__ requeue_list,
+                                              uint32_t* __restrict__ special_list, int special_ctr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool html = false, lng = false;
+  if (i < n) {
+    html = special && (special[i] & kSpecialHtml);
+    lng = !html && offs[i + 1] - offs[i] > (uint64_t)cap;
+  }
+  wave_append(html, &counters[special_ctr], special_list, (uint32_t)i, &counters[kCtrSpecial]);
+  wave_append(lng, &counters[kCtrRequeue], requeue_list, (uint32_t)i, nullptr);
 }
 
 // One wavefront per long document, persistent: each wave owns slot
@@ -332,10 +360,24 @@ __global__ __launch_bounds__(256) void k_len_scatter(const uint32_t* __restrict_
     for (int b = 0; b < kLenBuckets; ++b) { base[b] = s; s += hist[b]; }
   }
   __syncthreads();
+  // block-aggregated: positions inside the block from LDS counters, one
+  // global atomic per (block, bucket) present -- a batch whose documents all
+  // share a bucket (C3's pages) used to serialise on one cursor
+  __shared__ uint32_t lcnt[kLenBuckets], lbase[kLenBuckets];
   const uint32_t total = counters[kCtrRequeue];
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
-    const uint32_t b = key[k];
-    sorted[base[b] + atomicAdd(&cursor[b], 1u)] = list[k];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < total; k0 += stride) {
+    if (threadIdx.x < kLenBuckets) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t k = k0 + threadIdx.x;
+    const uint32_t b = k < total ? key[k] : 0u;
+    const uint32_t pos = k < total ? atomicAdd(&lcnt[b], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < kLenBuckets && lcnt[threadIdx.x])
+      lbase[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], lcnt[threadIdx.x]);
+    __syncthreads();
+    if (k < total) sorted[base[b] + lbase[b] + pos] = list[k];
+    __syncthreads();
   }
 }
 
@@ -467,6 +509,8 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
                            int special_ctr, uint32_t cflags, const uint32_t* priors, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cld::k_route, dim3((n + 255) / 256), dim3(256), 0, s, offs, n, special, kWaveCap, counters,
+                     requeue_list, special_list, special_ctr);
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
