@@ -168,7 +168,10 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
  * chunk_offsets[n+1] receives document i's chunks as
  * chunks[chunk_offsets[i] .. chunk_offsets[i+1]).  If chunk_cap is too small
  * the call returns CLD_ENOMEM with out and chunk_offsets complete and chunks
- * holding the first chunk_cap entries.  Every document runs the sequential
+ * holding the first chunk_cap entries.  A document whose vector outgrows its
+ * working region is redone alone with 8x the room; should that fail too, it
+ * gets an empty vector and the call returns CLD_EIO with every other
+ * document's result and vector complete.  Every document runs the sequential
  * kernel (not a high-throughput path, as in the reference). */
 int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
                          uint32_t flags, cld_result* out, cld_chunk* chunks, size_t chunk_cap,

@@ -85,6 +85,16 @@ constexpr int kLdsText = LNG_TEXT;
 #ifndef LNG_PF
 #define LNG_PF 4
 #endif
+// Timing experiment only (wrong results): -DLNG_EXP_NOADDS compiles out the
+// emission tote-add streams (stores in the hit rounds, loads in score_round)
+// so an A/B run prices them.
+#ifdef LNG_EXP_NOADDS
+#define LNG_ADD_ST(dst, v) ((void)(v))
+#define LNG_ADD_LD(src) (0x0101ull)
+#else
+#define LNG_ADD_ST(dst, v) ((dst) = (v))
+#define LNG_ADD_LD(src) (src)
+#endif
 // Inlining of the two largest stages (A/B: a call keeps the caller's
 // registers free, inlining lets the slot / LDS accesses stay global / ds).
 #ifndef LNG_SR_INL
@@ -234,6 +244,41 @@ __device__ __forceinline__ void gsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// LDS window over a lowered span for the hit stages (score_span): s.text
+// holds span bytes [w0, w1).  A span longer than the LDS text buffer stays in
+// the slot (g); every block of those stages first makes its byte range
+// resident (win_text) and reads the text through the biased LDS pointer it
+// returns, so the chain walk, the gram hashes and the word scans read LDS at
+// any span length (a window reload is a few 16-byte loads per lane, once per
+// ~6 KB of text per stage).  g null: the whole span is in s.text already.
+struct Win {
+  const uint8_t* g;
+  int w0, w1;
+  int len;                                     // bytes of the span buffer that may be copied
+};
+// (Smem is defined above; the window copy writes s.text.)
+template <class SM>
+__device__ __forceinline__ const uint8_t* win_text(Win& w, SM& s, int lo, int hi, bool& ok, int lane) {
+  hi = hi < w.len ? hi : w.len;
+  lo = lo > 0 ? lo : 0;
+  if (lo < w.w0 || hi > w.w1) {
+    const int a = (lo - 32 > 0 ? lo - 32 : 0) & ~15;
+    if (!w.g || hi > a + (int)sizeof(s.text) - 15) {   // (a block wider than the buffer: k_general takes it)
+      ok = false;
+      return s.text - w.w0;
+    }
+    const int b = min(w.len, a + (int)sizeof(s.text) - 15);
+    const int n16 = (b - a + 15) >> 4;
+    wsync();                                     // every lane is done with the previous window
+    for (int i = lane; i < n16; i += 64)
+      reinterpret_cast<uint4*>(s.text)[i] = gld4(reinterpret_cast<const uint32_t*>(w.g + a) + 4 * i);
+    wsync();
+    w.w0 = a;
+    w.w1 = a + 16 * n16;
+  }
+  return s.text - w.w0;
 }
 
 // First set bit at or after `from` in a bitmask over positions [0, L); L if none.
@@ -1212,10 +1257,13 @@ __device__ __forceinline__ void base_adds(const DevTbl& t1, const DevTbl& t2, ui
 // at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
 // else mid (+1 on a vowel).  It never jumps over a space, so it enters every
 // word at its first byte and a word's entries depend on that word alone.
-__device__ __forceinline__ bool word_lists(const uint8_t* text, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+__device__ __forceinline__ bool word_lists(Win& win, Smem& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
   nws = 0;
   nsp = 0;
+  bool ok = true;
   for (int w0 = start; w0 <= tb; w0 += 64) {
+    const uint8_t* text = win_text(win, s, w0 - 1, w0 + 65, ok, lane);
+    if (!ok) return false;
     const int x = w0 + lane;
     const bool isws = x < tb && (x == start || text[x - 1] == ' ');
     const bool issp = x <= tb && text[x] == ' ';
@@ -1264,10 +1312,14 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
   return cnt;
 }
 
-__device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S, int nws, int lane) {
+__device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, int nws, int lane) {
   int nch = 0;
   int sn = (LNG_PF & 1) && lane < nws ? S.wst[lane] : 0;       // word starts one block ahead
   for (int i0 = 0; i0 < nws; i0 += 64) {
+    // the block's words: from its first start to the next block's first (a walk stops at its word's space)
+    bool ok = true;
+    const uint8_t* text = win_text(win, sm, ufl(S.wst[i0]), (i0 + 64 < nws ? ufl(S.wst[i0 + 64]) : tb) + 24, ok, lane);
+    if (!ok) return -1;
     const int i = i0 + lane;
     int cnt = 0;
     const int s = (LNG_PF & 1) ? sn : (i < nws ? S.wst[i] : 0);
@@ -1299,13 +1351,16 @@ __device__ __forceinline__ int build_chain(const uint8_t* text, int tb, Slot& S,
 // kept only for the debug dump (D).  Returns the round end (the reference's
 // `next`); c0 advances.
 template <bool D>
-__device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int nch, int& c0, int& nb,
-                          int& eb, int lane) {
+__device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int nch, int& c0, int& nb,
+                          int& eb, bool& ok, int lane) {
   nb = 0;
   eb = 0;
   uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
   int pn = (LNG_PF & 2) && c0 + lane < nch ? S.chain[c0 + lane] : 0;   // chain entries one block ahead
   for (int i0 = c0; i0 < nch; i0 += 64) {
+    // the block's chain entries: each reads its quad (<= 4 chars) and one byte either side
+    const uint8_t* text = win_text(win, sm, ufl(S.chain[i0]) - 1, ufl(S.chain[min(i0 + 63, nch - 1)]) + 24, ok, lane);
+    if (!ok) return tb;
     const int i = i0 + lane;
     bool hit = false;
     uint32_t hv = 0, ind = 0;
@@ -1385,11 +1440,11 @@ __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* tex
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)p;
-        S.be_add[o] = l1;
+        LNG_ADD_ST(S.be_add[o], l1);
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)p;
-        S.be_add[o + 1] = l2;
+        LNG_ADD_ST(S.be_add[o + 1], l2);
       }
     }
     if (lastl < 64) {
@@ -1412,11 +1467,12 @@ __device__ __forceinline__ int quad_round(const DevTables& T, const uint8_t* tex
 // distinct with non-zero langprobs, in hit order); the hit lists are kept
 // only for the debug dump (D).
 template <bool D>
-__device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* text, Slot& S, int nsp, int& j0, int off, int next,
-                           int& nd, int& nx, int& edm, int& exm, int lane) {
+__device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& sm, Slot& S, int nsp, int& j0, int off, int next,
+                           int& nd, int& nx, int& edm, int& exm, bool& ok, int lane) {
   edm = 0;
   exm = 0;
-  const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
+  const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
+  if (!ok) return;
   const int lim = next + 1;
   nd = 0;
   nx = 0;
@@ -1426,6 +1482,10 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
   int en = (LNG_PF & 4) && j0 + lane < nsp ? S.wsp[j0 + lane] : 0x7FFFFFFF;
   int c1 = start - 1, c2 = start - 1;    // wsp[jb - 1], wsp[jb - 2] as "start - 1" before jfirst
   for (int jb = j0;; jb += 64) {
+    // the block's words end at spaces below lim: text from the space before the first on
+    const uint8_t* text =
+        jb < nsp ? win_text(win, sm, c1, min((int)ufl(S.wsp[min(jb + 63, nsp - 1)]), lim) + 8, ok, lane) : sm.text;
+    if (!ok) return;
     const int j = jb + lane;
     const int ej = (LNG_PF & 4) ? en : (j < nsp ? S.wsp[j] : 0x7FFFFFFF);
     if (LNG_PF & 4) en = j + 64 < nsp ? S.wsp[j + 64] : 0x7FFFFFFF;
@@ -1506,16 +1566,16 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
       edm = rdl(od + md, 63);
       if (in && (apx >> 63)) {
         S.x_off[ox] = (uint16_t)pws;
-        S.x_add[ox] = apx;
+        LNG_ADD_ST(S.x_add[ox], apx);
         ++ox;
       }
       if (in && (axp >> 63)) {
         S.x_off[ox] = (uint16_t)a;
-        S.x_add[ox] = axp;
+        LNG_ADD_ST(S.x_add[ox], axp);
       }
       if (in && (adp >> 63)) {
         S.d_off[od] = (uint16_t)a;
-        S.d_add[od] = adp;
+        LNG_ADD_ST(S.d_add[od], adp);
       }
     }
     if (D && lane <= cut) {
@@ -1556,9 +1616,10 @@ __device__ __forceinline__ void octa_round(const DevTables& T, const uint8_t* te
 // As in quad_round / octa_round, the hits become emissions here (eb base,
 // edm delta, exm distinct); the hit lists are kept only for the debug dump.
 template <bool D>
-__device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text, int tb, Slot& S, int off, int& nb, int& nd,
-                         int& nx, int& eb, int& edm, int& exm, int lane) {
-  const int start = off + (ufl(text[off]) == ' ' ? 1 : 0);
+__device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int off, int& nb, int& nd,
+                         int& nx, int& eb, int& edm, int& exm, bool& ok, int lane) {
+  const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
+  if (!ok) return tb;
   nb = 0;
   eb = 0;
   edm = 0;
@@ -1566,6 +1627,8 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
   int next = -1;
   uint32_t endmax = (uint32_t)start;
   for (int w0 = start; w0 < tb; w0 += 64) {
+    const uint8_t* text = win_text(win, sm, w0, w0 + 64 + 8, ok, lane);
+    if (!ok) return tb;
     const int x = w0 + lane;
     int prop = 0, len = 0;
     if (x < tb && (text[x] & 0xC0) != 0x80) {
@@ -1594,11 +1657,11 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)(x + len);
-        S.be_add[o] = l1;
+        LNG_ADD_ST(S.be_add[o], l1);
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)(x + len);
-        S.be_add[o + 1] = l2;
+        LNG_ADD_ST(S.be_add[o + 1], l2);
       }
     }
     if (lastl < 64) {
@@ -1610,6 +1673,8 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
   nd = 0;
   nx = 0;
   for (int w0 = off; w0 < next; w0 += 64) {
+    const uint8_t* text = win_text(win, sm, w0, w0 + 64 + 12, ok, lane);
+    if (!ok) return tb;
     const int x = w0 + lane;
     uint32_t dp = 0, xp = 0;
     const bool v = x < next && (text[x] & 0xC0) != 0x80;
@@ -1636,11 +1701,11 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, const uint8_t* text
       exm = rdl(ox + mx, 63);
       if (md) {
         S.d_off[od] = (uint16_t)x;
-        S.d_add[od] = adp;
+        LNG_ADD_ST(S.d_add[od], adp);
       }
       if (mx) {
         S.x_off[ox] = (uint16_t)x;
-        S.x_add[ox] = axp;
+        LNG_ADD_ST(S.x_add[ox], axp);
       }
     }
     if (D && lane <= cut) {
@@ -1694,12 +1759,12 @@ __device__ __forceinline__ uint64_t chunk_add(const Slot& S, const Smem& s, uint
   int u = t;
   const int seedn = k == 0 ? 1 : 0;
   if (u < seedn) return seed;
-  if ((u -= seedn) < nB) return S.be_add[bs + u];
-  if ((u -= nB) < nD) return S.d_add[ds + u];
-  if ((u -= nD) < nX) return S.x_add[xs + u];
+  if ((u -= seedn) < nB) return LNG_ADD_LD(S.be_add[bs + u]);
+  if ((u -= nB) < nD) return LNG_ADD_LD(S.d_add[ds + u]);
+  if ((u -= nD) < nX) return LNG_ADD_LD(S.x_add[xs + u]);
   if (u - nX >= kMaxBoosts) return s.pri_add[rs][u - nX - kMaxBoosts];   // prior boosts (has_pri)
   const int v = xe - kMaxBoosts + (u - nX);
-  return v < 0 ? s.ring[rs][v + kMaxBoosts] : gld(&S.x_add[v]);   // (gld: no LDS/global pointer select)
+  return v < 0 ? s.ring[rs][v + kMaxBoosts] : LNG_ADD_LD(gld(&S.x_add[v]));   // (gld: no LDS/global pointer select)
 }
 // Chunk plan of k: emission ranges and the number of adds.
 __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
@@ -1930,7 +1995,7 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     uint64_t r4[4];
     for (int i = 0; i < 4; ++i) {
       const int u = ex - kMaxBoosts + i;
-      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : gld(&S.x_add[u]);
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : LNG_ADD_LD(gld(&S.x_add[u]));
     }
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
@@ -1959,7 +2024,7 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
 template <bool D>
-__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, const uint8_t* text, int tb,
+__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, Win& win, int tb,
                                            int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags) {
   int rt = rtype_of(T, ulscript);
   if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
@@ -1976,7 +2041,9 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
       int nb, nd, nx;
       if constexpr (D) trace(tr, lane, doc, 20, off);
       int eb, edm, exm;
-      const int next = cjk_round<D>(T, text, tb, S, off, nb, nd, nx, eb, edm, exm, lane);
+      bool ok = true;
+      const int next = cjk_round<D>(T, win, s, tb, S, off, nb, nd, nx, eb, edm, exm, ok, lane);
+      if (!ok) return false;
       if constexpr (D) trace(tr, lane, doc, 21, next);
       if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
       if constexpr (D) mark(s, lane, 6, t);
@@ -1986,11 +2053,12 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
     }
     return true;
   }
-  const int start = 1 + (ufl(text[1]) == ' ' ? 1 : 0);
+  bool ok = true;
+  const int start = 1 + (ufl(win_text(win, s, 0, 2, ok, lane)[1]) == ' ' ? 1 : 0);
   int nws, nsp;
-  if (!word_lists(text, tb, start, S, nws, nsp, lane)) return false;
+  if (!ok || !word_lists(win, s, tb, start, S, nws, nsp, lane)) return false;
   if constexpr (D) trace(tr, lane, doc, 10, nws);
-  const int nch = build_chain(text, tb, S, nws, lane);
+  const int nch = build_chain(win, s, tb, S, nws, lane);
   if (nch < 0) return false;
   if constexpr (D) trace(tr, lane, doc, 11, nch);
   if constexpr (D) mark(s, lane, 4, t);
@@ -1999,10 +2067,12 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
     int nb, nd, nx;
     if constexpr (D) trace(tr, lane, doc, 12, off);
     int eb, edm, exm;
-    const int next = quad_round<D>(T, text, tb, S, nch, c0, nb, eb, lane);
+    const int next = quad_round<D>(T, win, s, tb, S, nch, c0, nb, eb, ok, lane);
+    if (!ok) return false;
     if constexpr (D) trace(tr, lane, doc, 13, next);
     if constexpr (D) mark(s, lane, 5, t);
-    octa_round<D>(T, text, S, nsp, j0, off, next, nd, nx, edm, exm, lane);
+    octa_round<D>(T, win, s, S, nsp, j0, off, next, nd, nx, edm, exm, ok, lane);
+    if (!ok) return false;
     if constexpr (D) trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
     if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
     if constexpr (D) mark(s, lane, 6, t);
@@ -2135,7 +2205,8 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        ok = score_span<D>(T, S, s, s.text, tb, ul, lane, tr, doc, cflags);
+        Win win{nullptr, 0, 16 * n16, 16 * n16};                          // the whole span is in s.text
+        ok = score_span<D>(T, S, s, win, tb, ul, lane, tr, doc, cflags);
       } else {
         const uint8_t* text = lb;
         if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
@@ -2151,7 +2222,8 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        ok = score_span<D>(T, S, s, text, tb, ul, lane, tr, doc, cflags);
+        Win win{text, 0, 0, (tb + 48 + 15) & ~15};                       // windows of it go to s.text
+        ok = score_span<D>(T, S, s, win, tb, ul, lane, tr, doc, cflags);
       }
       if (!ok) return -kWhyCapacity;
       t = (D && s.prof) ? (long long)clock64() : 0;

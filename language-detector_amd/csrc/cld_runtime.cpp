@@ -775,13 +775,58 @@ void par_copy(void* dst, const void* src, size_t n) {
 // caller wrote them and the kernels get `d_in - offs[first]` as their buffer
 // base, so no rebasing pass runs anywhere.  Chunk k's staging overlaps chunk
 // k-1's kernels; its upload overlaps them too.
+// Large pageable batches: the caller's buffers are page-locked for the call
+// (hipHostRegister) instead of staged chunk by chunk through pinned copies,
+// above CLD_HOST_REGISTER_MB of document text (default 64; 0 = never).
+uint64_t register_min_bytes() {
+  static const uint64_t v = [] {
+    uint64_t mb = 64;
+    if (const char* e = getenv("CLD_HOST_REGISTER_MB")) mb = strtoull(e, nullptr, 10);
+    return mb ? mb << 20 : ~0ull;
+  }();
+  return v;
+}
+
+// Page-locks [p, p + bytes) for the life of the object when it is not pinned already.
+struct HostReg {
+  void* p = nullptr;
+  bool on = false;
+  bool take(const void* q, size_t bytes) {
+    if (!bytes) return false;
+    if (hipHostRegister(const_cast<void*>(q), bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    p = const_cast<void*>(q);
+    on = true;
+    return true;
+  }
+  void release() {
+    if (on) (void)hipHostUnregister(p);
+    on = false;
+  }
+  HostReg() = default;
+  HostReg(const HostReg&) = delete;
+  HostReg& operator=(const HostReg&) = delete;
+  ~HostReg() { release(); }
+};
+
 int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
                    const uint8_t* special = nullptr, const uint32_t* priors = nullptr) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
-  const bool in_pinned = host_pinned(buf + offs[0]) && host_pinned(offs);
-  const bool out_pinned = host_pinned(out);
+  bool in_pinned = host_pinned(buf + offs[0]) && host_pinned(offs);
+  bool out_pinned = host_pinned(out);
+  // (declared before any DMA is enqueued: unregistered only after the drain below)
+  HostReg reg_buf, reg_offs, reg_out;
+  if (offs[n] - offs[0] >= register_min_bytes()) {
+    if (!in_pinned) {
+      in_pinned = reg_buf.take(buf + offs[0], offs[n] - offs[0]) && reg_offs.take(offs, (n + 1) * sizeof(uint64_t));
+      if (!in_pinned) reg_buf.release();
+    }
+    if (!out_pinned) out_pinned = reg_out.take(out, n * sizeof(cld_result));
+  }
   // chunk plan
   std::vector<size_t> cut{0};
   while (cut.back() < n) {
@@ -926,60 +971,114 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   }
   const size_t kSub = 256 * 1024;
   const uint64_t kSubBytes = 32ull << 20;
-  size_t a = 0;
+  // test hook: CLD_VEC_POOL_SMALL=1 makes first-pass pool regions too small so
+  // the retry below runs (tests/test_gpu_vector.py)
+  static const bool small_pool = getenv("CLD_VEC_POOL_SMALL") && atoi(getenv("CLD_VEC_POOL_SMALL")) > 0;
+  // One sub-batch: documents [o[0], o[m]) of b (o: offsets into b), document
+  // i building its vector in a pool region of len + len/4 + 8 chunks (big: 8 len
+  // + 256); results to res, vector sizes to nch (-1: the document overflowed
+  // its pool region or an offset map), the vectors to ch in document order.
   std::vector<uint64_t> pool_off, pos;
-  std::vector<int32_t> nch;
-  while (a < n) {
-    size_t m = 1;                                       // at least one document, then up to the limits
-    while (a + m < n && m < kSub && offs[a + m + 1] - offs[a] <= kSubBytes) ++m;
-    const uint64_t base = offs[a], bytes = offs[a + m] - base;
+  auto sub = [&](const uint8_t* b, const uint64_t* o, size_t m, cld_result* res, const uint8_t* sp,
+                 const uint32_t* pr, bool big, std::vector<int32_t>& nch, std::vector<cld_chunk>& ch) -> int {
+    const uint64_t base = o[0], bytes = o[m] - base;
     pool_off.assign(m + 1, 0);
     for (size_t i = 0; i < m; ++i) {
-      const uint64_t len = offs[a + i + 1] - offs[a + i];
-      pool_off[i + 1] = pool_off[i] + len + len / 4 + 8;
+      const uint64_t len = o[i + 1] - o[i];
+      pool_off[i + 1] = pool_off[i] + (big ? 8 * len + 256 : small_pool ? 1 : len + len / 4 + 8);
     }
     if (grow(&V.in, &V.in_cap, std::max<size_t>(bytes, 1)) || grow(&V.offs, &V.offs_cap, m + 1) ||
         grow(&V.out, &V.out_cap, m) || grow(&V.pool, &V.pool_cap, pool_off[m]) ||
         grow(&V.pool_off, &V.pool_off_cap, m + 1) || grow(&V.nch, &V.nch_cap, m) || grow(&V.pos, &V.pos_cap, m))
       return CLD_ENOMEM;
-    if (special && grow(&V.sp, &V.sp_cap, m)) return CLD_ENOMEM;
-    if (priors && grow(&V.pri, &V.pri_cap, 16 * m)) return CLD_ENOMEM;
+    if (sp && grow(&V.sp, &V.sp_cap, m)) return CLD_ENOMEM;
+    if (pr && grow(&V.pri, &V.pri_cap, 16 * m)) return CLD_ENOMEM;
     hipStream_t s = d->stream;
     HIP_OK(hipStreamWaitEvent(s, d->done, 0));
-    if (bytes) HIP_OK(hipMemcpyAsync(V.in, buf + base, bytes, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(V.offs, offs + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    if (bytes) HIP_OK(hipMemcpyAsync(V.in, b + base, bytes, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(V.offs, o, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemcpyAsync(V.pool_off, pool_off.data(), (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    if (special) HIP_OK(hipMemcpyAsync(V.sp, special + a, m, hipMemcpyHostToDevice, s));
-    if (priors) HIP_OK(hipMemcpyAsync(V.pri, priors + 16 * a, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (sp) HIP_OK(hipMemcpyAsync(V.sp, sp, m, hipMemcpyHostToDevice, s));
+    if (pr) HIP_OK(hipMemcpyAsync(V.pri, pr, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
     HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
-                                  special ? V.sp : nullptr, priors ? V.pri : nullptr, V.pool, V.pool_off, V.nch,
+                                  sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off, V.nch,
                                   cflags & kCldFlags, s));
     nch.resize(m);
-    HIP_OK(hipMemcpyAsync(out + a, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(res, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     pos.assign(m, 0);
     uint64_t total = 0;
-    bool err = false;
     for (size_t i = 0; i < m; ++i) {
       pos[i] = total;
-      if (nch[i] < 0) err = true;
-      else total += (uint64_t)nch[i];
+      if (nch[i] > 0) total += (uint64_t)nch[i];
     }
-    if (err) { HIP_OK(hipEventRecord(d->done, s)); return CLD_EIO; }
     if (grow(&V.compact, &V.compact_cap, std::max<uint64_t>(total, 1))) return CLD_ENOMEM;
     HIP_OK(hipMemcpyAsync(V.pos, pos.data(), m * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    HIP_OK(cld_launch_vec_gather(V.pool, V.pool_off, V.nch, V.pos, (int)m, V.compact, s));
-    const size_t at = chunks->size();
-    chunks->resize(at + total);
-    if (total) HIP_OK(hipMemcpyAsync(chunks->data() + at, V.compact, total * sizeof(cld_chunk), hipMemcpyDeviceToHost, s));
+    HIP_OK(cld_launch_vec_gather(V.pool, V.pool_off, V.nch, V.pos, (int)m, V.compact, s));   // (-1: no chunks)
+    ch.resize(total);
+    if (total) HIP_OK(hipMemcpyAsync(ch.data(), V.compact, total * sizeof(cld_chunk), hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(d->done, s));
     HIP_OK(hipStreamSynchronize(s));
+    return CLD_OK;
+  };
+  size_t a = 0;
+  bool failed = false;
+  while (a < n) {
+    size_t m = 1;                                       // at least one document, then up to the limits
+    while (a + m < n && m < kSub && offs[a + m + 1] - offs[a] <= kSubBytes) ++m;
+    std::vector<int32_t> nch;
+    std::vector<cld_chunk> ch;
+    if (int rc = sub(buf, offs + a, m, out + a, special ? special + a : nullptr, priors ? priors + 16 * a : nullptr,
+                     false, nch, ch))
+      return rc;
+    // A document whose vector did not fit runs again, alone with the others
+    // that did not, with 8x the pool region; the rest of the batch is kept.
+    std::vector<size_t> bad;
+    for (size_t i = 0; i < m; ++i)
+      if (nch[i] < 0) bad.push_back(i);
+    if (!bad.empty()) {
+      std::vector<uint8_t> rb, rsp;
+      std::vector<uint64_t> ro{0};
+      std::vector<uint32_t> rpr;
+      for (size_t i : bad) {
+        rb.insert(rb.end(), buf + offs[a + i], buf + offs[a + i + 1]);
+        ro.push_back(rb.size());
+        if (special) rsp.push_back(special[a + i]);
+        if (priors) rpr.insert(rpr.end(), priors + 16 * (a + i), priors + 16 * (a + i + 1));
+      }
+      std::vector<cld_result> rres(bad.size());
+      std::vector<int32_t> nch2;
+      std::vector<cld_chunk> ch2;
+      if (int rc = sub(rb.empty() ? buf : rb.data(), ro.data(), bad.size(), rres.data(),
+                       special ? rsp.data() : nullptr, priors ? rpr.data() : nullptr, true, nch2, ch2))
+        return rc;
+      std::vector<cld_chunk> merged;
+      merged.reserve(ch.size() + ch2.size());
+      size_t c1 = 0, c2 = 0, j = 0;
+      for (size_t i = 0; i < m; ++i) {
+        if (j < bad.size() && bad[j] == i) {
+          out[a + i] = rres[j];
+          const int32_t k = nch2[j];
+          if (k < 0) failed = true;                   // no vector: an empty one, and CLD_EIO
+          const size_t kk = k > 0 ? (size_t)k : 0;
+          merged.insert(merged.end(), ch2.begin() + c2, ch2.begin() + c2 + kk);
+          c2 += kk;
+          nch[i] = (int32_t)kk;
+          ++j;
+        } else {
+          merged.insert(merged.end(), ch.begin() + c1, ch.begin() + c1 + nch[i]);
+          c1 += (size_t)nch[i];
+        }
+      }
+      ch.swap(merged);
+    }
+    chunks->insert(chunks->end(), ch.begin(), ch.end());
     counts->insert(counts->end(), nch.begin(), nch.end());
     a += m;
   }
-  return CLD_OK;
+  return failed ? CLD_EIO : CLD_OK;
 }
 
 // ------------------------------------------------ detect_language batching
@@ -1355,7 +1454,11 @@ int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, 
     if (ndev == 1) job(); else th.emplace_back(job);
   }
   for (auto& t : th) t.join();
-  for (int r : rcs) if (r) return r;
+  int partial = CLD_OK;                 // CLD_EIO: some document got no vector; all others are complete
+  for (int r : rcs) {
+    if (r == CLD_EIO) partial = CLD_EIO;
+    else if (r) return r;
+  }
   size_t i = 0;
   uint64_t total = 0;
   for (size_t k = 0; k < ndev; ++k) {
@@ -1364,7 +1467,7 @@ int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, 
     if (at < chunk_cap)
       memcpy(chunks + at, vs[k].data(), std::min<uint64_t>(vs[k].size(), chunk_cap - at) * sizeof(cld_chunk));
   }
-  return total > chunk_cap ? CLD_ENOMEM : CLD_OK;
+  return total > chunk_cap ? CLD_ENOMEM : partial;
 }
 
 int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,

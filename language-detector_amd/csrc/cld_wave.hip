@@ -156,9 +156,9 @@ struct Smem {
       uint32_t b_ind[C::NB];
       uint16_t b_off[C::NB];
     };
-    struct {                          //   chunk of each delta/distinct emission, written after
-      uint8_t d_ch[C::ND];            //   the base hits are expanded (scoring only)
-      uint8_t x_ch[C::NX];
+    struct {                          //   chunk plan, written after the base hits are expanded:
+      int32_t theta[C::MAXCH];        //   chunk k takes delta/distinct emissions at offset <= theta_k
+      uint16_t st[3][C::MAXCH + 1];   //   first base / delta / distinct emission of chunk k
     };
   };
   union alignas(16) {                 // scoring reads only hit offsets, never the span text:
@@ -169,10 +169,9 @@ struct Smem {
     uint16_t nx[CAP];                 // load: p + ScanToLetterOrSpecial(p, L - p)
     uint16_t nxq[C::LB];              // quad hits: next quad start for a quad starting at p
     uint16_t wsp[C::NB + 1];          // octa hits: word-ending spaces
-    struct {                          // scoring: base emissions (offset, langprob, chunk), linear order
+    struct {                          // scoring: base emissions (offset, langprob), linear order
       uint32_t be_lp[C::NE];
       uint16_t be_off[C::NE + 1];
-      uint8_t be_ch[C::NE];
     } e;
   } a;
   uint16_t d_off[C::ND]; uint32_t d_ind[C::ND];   // delta hits; compacted in place to emissions
@@ -922,79 +921,114 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     }
     if (lane == 0) s.E[K - 1] = 0xFFFF;   // the last chunk takes everything that is left
   }
-  // lo[k] = first (lowest) offset in chunk k; chunk 0 opens with the seed at `lowest` = 1
-  for (int k = lane; k < K; k += 64) s.lo[k] = k == 0 ? 1u : 0xFFFFFFFFu;
   wsync();
-  // base emission t has base number t+2 (the seed is #1): chunk = min k with num <= E_k
-  for (int t = lane; t < eb; t += 64) {
-    const int num = t + 2;
-    int k = 0;
-    while (num > s.E[k]) ++k;
-    s.a.e.be_ch[t] = (uint8_t)k;
-    atomicMin(&s.lo[k], (uint32_t)s.a.e.be_off[t]);
-  }
-  // delta/distinct at offset o after m base emissions (m = 1 + #base emissions with offset < o):
-  // chunk = min k with m < E_k
-  for (int t = lane; t < ed + ex; t += 64) {
-    const bool isd = t < ed;
-    const int idx = isd ? t : t - ed;
-    const uint32_t o = isd ? s.d_off[idx] : s.x_off[idx];
-    int lo_i = 0, hi_i = eb;
-    while (lo_i < hi_i) {
-      int mid = (lo_i + hi_i) >> 1;
-      if ((uint32_t)s.a.e.be_off[mid] < o) lo_i = mid + 1; else hi_i = mid;
+  // Every chunk is one contiguous range of each stream (k_long's score_round):
+  // base emission t has base number t+2 (the seed is #1), so chunk k holds base
+  // emissions [E_{k-1} - 1, E_k - 1); a delta / distinct emission at offset o
+  // follows 1 + #(base emissions with offset < o) base entries and lands in the
+  // first chunk with that count < E_k, i.e. with o <= theta_k = be_off[E_k - 2].
+  if (lane <= K) {                                     // K <= MAXCH < 64
+    const int k = lane;
+    if (k < K) {
+      int th = 0x7FFFFFFF;
+      if (k < K - 1) {
+        const int idx = (int)s.E[k] - 2;
+        th = idx < 0 ? -1 : (idx < eb ? (int)s.a.e.be_off[idx] : 0x7FFFFFFF);
+      }
+      s.theta[k] = th;
+      s.st[0][k] = (uint16_t)(k == 0 ? 0 : min(max((int)s.E[k - 1] - 1, 0), eb));
+    } else {
+      s.st[0][K] = (uint16_t)eb;
     }
-    const int m = 1 + lo_i;
-    int k = 0;
-    while (m >= s.E[k]) ++k;
-    if (isd) s.d_ch[idx] = (uint8_t)k; else s.x_ch[idx] = (uint8_t)k;
-    atomicMin(&s.lo[k], o);
+    s.st[1][k] = (uint16_t)ed;
+    s.st[2][k] = (uint16_t)ex;
   }
   wsync();
+  for (int pass = 0; pass < 2; ++pass) {               // first delta / distinct emission of each chunk
+    const int n = pass == 0 ? ed : ex;
+    int pch = -1;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      int ch = K - 1;
+      if (i < n) {
+        const int o = pass == 0 ? s.d_off[i] : s.x_off[i];
+        int lo_c = 0, hi_c = K - 1;
+        while (lo_c < hi_c) {
+          const int mid = (lo_c + hi_c) >> 1;
+          if (o <= s.theta[mid]) hi_c = mid;
+          else lo_c = mid + 1;
+        }
+        ch = lo_c;
+      }
+      const int prev = (int)wshr1((uint32_t)ch, (uint32_t)pch);   // lane - 1's chunk
+      if (i < n)
+        for (int k = prev + 1; k <= ch; ++k) s.st[1 + pass][k] = (uint16_t)i;
+      pch = rdl(ch, 63);
+    }
+  }
+  wsync();
+  // lo[k] = first (lowest) offset in chunk k; chunk 0 opens with the seed at `lowest` = 1
+  if (lane < K) {
+    const int k = lane;
+    uint32_t m = k == 0 ? 1u : 0xFFFFFFFFu;
+    const int bs = s.st[0][k], be = s.st[0][k + 1], ds = s.st[1][k], de = s.st[1][k + 1];
+    const int xs = s.st[2][k], xe = s.st[2][k + 1];
+    if (bs < be) m = min(m, (uint32_t)s.a.e.be_off[bs]);
+    if (ds < de) m = min(m, (uint32_t)s.d_off[ds]);
+    if (xs < xe) m = min(m, (uint32_t)s.x_off[xs]);
+    s.lo[k] = m;
+  }
   // linear order starts with the seed at `lowest` (= 1 for the only round)
   const uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   ring_sel = rs;
-  // X emissions with chunk <= k, for the boosts (X is in linear order)
-  int xc = 0;
+  const int nboost = pri ? 2 * kMaxBoosts : kMaxBoosts;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
+  wsync();
   for (int k = 0; k < K; ++k) {
-    // zero the tote
+    const int seedn = k == 0 ? 1 : 0;
+    const int bs = s.st[0][k], nB = s.st[0][k + 1] - bs, ds = s.st[1][k], nD = s.st[1][k + 1] - ds;
+    const int xs = s.st[2][k], xe = s.st[2][k + 1], nX = xe - xs;
+    const int tot = seedn + nB + nD + nX + nboost;
+    // chunk k's langprob t: the seed, its base, delta and distinct emissions,
+    // then ScoreBoosts (scoreonescriptspan.cc:125-152): the last four distinct
+    // langprobs up to the end of the chunk and, for a hinted document, the four
+    // ApplyHints prior boosts of this script class (cld_detect_batch_ex: 16
+    // langprobs per document, boost latn[4] othr[4], whack latn[4] othr[4])
+    auto chunk_lp = [&](int t) -> uint32_t {
+      if (t >= tot) return 0u;
+      int u = t;
+      if (u < seedn) return seed;
+      if ((u -= seedn) < nB) return s.a.e.be_lp[bs + u];
+      if ((u -= nB) < nD) return s.d_ind[ds + u];
+      if ((u -= nD) < nX) return s.x_ind[xs + u];
+      if ((u -= nX) < kMaxBoosts) {
+        const int v = xe - kMaxBoosts + u;
+        return v < 0 ? s.ring[rs][v + kMaxBoosts] : s.x_ind[v];
+      }
+      return gld(pri + 4 * rs + (u - kMaxBoosts));
+    };
+    // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row,
+    // gathered before the tote is cleared so the L2 round trip overlaps it
+    uint32_t lp = chunk_lp(lane);
+    uint32_t e = lp ? gld(reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4)) : 0u;
     reinterpret_cast<uint2*>(s.tote)[lane] = make_uint2(0, 0);
     wsync();
     uint64_t gm = 0;
-    int cnt = 0;
-    // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row
-    auto add = [&](uint32_t lp) {
-      const uint32_t e = gld(reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4));
-      const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
-      if (k1) { atomicAdd(&s.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
-      if (k2) { atomicAdd(&s.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
-      if (k3) { atomicAdd(&s.tote[k3 >> 1], (e >> 24) << ((k3 & 1) * 16)); gm |= 1ull << (k3 >> 2); }
-    };
-    if (k == 0 && lane == 0) { add(seed); ++cnt; }
-    for (int t = lane; t < eb; t += 64)
-      if (s.a.e.be_ch[t] == k) { add(s.a.e.be_lp[t]); ++cnt; }
-    for (int t = lane; t < ed; t += 64)
-      if (s.d_ch[t] == k) add(s.d_ind[t]);
-    int xin = 0;
-    for (int t = lane; t < ex; t += 64)
-      if (s.x_ch[t] <= k) { ++xin; if (s.x_ch[t] == k) add(s.x_ind[t]); }
-    xc = wsum(xin);
-    // ScoreBoosts (scoreonescriptspan.cc:125-152): the last four distinct
-    // langprobs up to the end of this chunk and, for a hinted document, the
-    // four ApplyHints prior boosts of this script class (cld_detect_batch_ex:
-    // 16 langprobs per document, boost latn[4] othr[4], whack latn[4] othr[4])
-    if (lane < 4) {
-      const int u = xc + lane;
-      const uint32_t lp = u < 4 ? s.ring[rs][u] : s.x_ind[u - 4];
-      if (lp > 0) add(lp);
-    } else if (pri && lane < 8) {
-      const uint32_t lp = gld(pri + 4 * rs + (lane - 4));
-      if (lp > 0) add(lp);
+    for (int t = lane;;) {
+      if (lp) {
+        const uint32_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
+        if (k1) { atomicAdd(&s.tote[k1 >> 1], ((e >> 8) & 0xFF) << ((k1 & 1) * 16)); gm |= 1ull << (k1 >> 2); }
+        if (k2) { atomicAdd(&s.tote[k2 >> 1], ((e >> 16) & 0xFF) << ((k2 & 1) * 16)); gm |= 1ull << (k2 >> 2); }
+        if (k3) { atomicAdd(&s.tote[k3 >> 1], (e >> 24) << ((k3 & 1) * 16)); gm |= 1ull << (k3 >> 2); }
+      }
+      t += 64;
+      if (t - lane >= tot) break;                      // (uniform)
+      lp = chunk_lp(t);
+      e = lp ? gld(reinterpret_cast<const uint32_t*>(T.lgprob + 8 * (lp & 0xFF) + 4)) : 0u;
     }
     gm = wor64(gm);
-    const int score_count = wsum(cnt);
+    const int score_count = nB + seedn;
     wsync();
     if (pri) {                           // then the whacks zero their top key's score (ZeroPSLang :39-42)
       const uint32_t wh = lane < 4 ? gld(pri + 8 + 4 * rs + lane) : 0u;

@@ -94,3 +94,32 @@ def test_vector_capacity_contract(gpu):
                                         small.ctypes.data, 3, co.ctypes.data)
     assert rc == -12 and int(co[-1]) == len(chunks)       # CLD_ENOMEM with the needed size
     assert np.array_equal(co, coffs)
+
+
+def test_vector_overflow_retry_keeps_the_batch():
+    """A document whose chunk vector outgrows its pool region is redone alone
+    with a larger one; the batch is not failed (CLD_VEC_POOL_SMALL shrinks the
+    first-pass regions to one chunk, so every multi-chunk document takes the
+    retry).  Child
+    process: the variable is read once per process."""
+    import subprocess
+    import sys
+    code = r'''
+import cld_amd, corpus
+from oracle import Oracle
+cld_amd.init()
+o = Oracle()
+b, off = corpus.c5(800, seed=17)
+res, chunks, coffs = cld_amd.detect_batch_vec(buf=b, offsets=off)
+for i in range(len(off) - 1):
+    r, ch = o.detect_vec(bytes(b[off[i]:off[i + 1]]))
+    assert [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]] == \
+        [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in ch], i
+    assert int(res[i]["summary_lang"]) == r.summary_lang, i
+assert sum(int(coffs[i + 1] - coffs[i]) > 1 for i in range(len(off) - 1)) > 50   # these took the retry
+print("retry ok")
+'''
+    env = dict(os.environ, CLD_VEC_POOL_SMALL="1",
+               PYTHONPATH=os.pathsep.join(os.path.join(ROOT, p) for p in ("language-detector_amd", "oracle", "tests")))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "retry ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
