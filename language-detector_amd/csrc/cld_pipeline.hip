@@ -446,6 +446,32 @@ __device__ __forceinline__ uint32_t lookup4(const DevTbl& t, uint32_t sub, uint3
 __device__ __forceinline__ uint32_t quad_lookup(const DevTbl& t, uint32_t h) {
   return lookup4(t, (h + (h >> 12)) & (t.size - 1), h & t.key_mask);
 }
+// GetQuadHits' probe (cldutil.cc:356-363): QuadHashV3Lookup4 on the first
+// quadgram table, then on the second one only on a miss.  Both buckets are
+// gathered at once -- the second load need not wait for the first answer --
+// so a miss costs one L2 round trip, not two.  ind: the indirect subscript,
+// bit 31 set for the second table.  Returns the matching keyvalue or 0.
+__device__ __forceinline__ uint32_t quad_probe(const DevTbl& q1, const DevTbl& q2, uint32_t h, uint32_t& ind) {
+  const bool two = q2.size != 0 && q2.n_buckets != 0;
+  const uint4 b1 = q1.n_buckets ? gld4(q1.b + 4 * (size_t)((h + (h >> 12)) & (q1.size - 1))) : make_uint4(0, 0, 0, 0);
+  const uint4 b2 = two ? gld4(q2.b + 4 * (size_t)((h + (h >> 12)) & (q2.size - 1))) : make_uint4(0, 0, 0, 0);
+  auto match = [](uint4 b, uint32_t key, uint32_t mask) -> uint32_t {
+    if (((key ^ b.x) & mask) == 0) return b.x;
+    if (((key ^ b.y) & mask) == 0) return b.y;
+    if (((key ^ b.z) & mask) == 0) return b.z;
+    if (((key ^ b.w) & mask) == 0) return b.w;
+    return 0u;
+  };
+  uint32_t probs = q1.n_buckets ? match(b1, h & q1.key_mask, q1.key_mask) : 0u;
+  ind = 0;
+  if (probs == 0 && q2.size != 0) {
+    probs = two ? match(b2, h & q2.key_mask, q2.key_mask) : 0u;
+    if (probs) ind = (probs & ~q2.key_mask) | 0x80000000u;
+  } else if (probs) {
+    ind = probs & ~q1.key_mask;
+  }
+  return probs;
+}
 __device__ __forceinline__ uint32_t octa_lookup(const DevTbl& t, uint64_t h) {
   uint32_t sub = (uint32_t)((h + (h >> 12)) & (uint64_t)(t.size - 1));
   return lookup4(t, sub, (uint32_t)(h >> 4) & t.key_mask);

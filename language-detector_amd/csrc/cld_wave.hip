@@ -242,9 +242,13 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
   // else takes the state-machine path below, unchanged.
   {
     int slow = 0, conts = 0, need = 0;
+    // every window's property gathers are issued before any is used: one L2
+    // round trip for the document instead of one per 64-byte window
+    int idx[C::NM];
+#pragma unroll
     for (int w = 0; w < C::NM; ++w) {
       const int p = w * 64 + lane;
-      bool ls = false;
+      idx[w] = -1;
       if (p < L) {
         const uint32_t c = s.doc[p];
         if ((c & 0xC0) == 0x80) {
@@ -256,13 +260,24 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
             slow = 1;
           } else {
             need += n - 1;
-            const uint64_t e = gld(T.cpt + (cpt_index(c, b1, b2, n)));
-            const int st = (int)((e >> 8) & 3);
-            slow |= st == 3;
-            s.sn[p] = (uint8_t)e;
-            ls = st == 1 && (e & 0xFF) != 0;
+            idx[w] = cpt_index(c, b1, b2, n);
           }
         }
+      }
+    }
+    uint64_t ev[C::NM];
+#pragma unroll
+    for (int w = 0; w < C::NM; ++w) ev[w] = idx[w] >= 0 ? gld(T.cpt + idx[w]) : 0ull;
+#pragma unroll
+    for (int w = 0; w < C::NM; ++w) {
+      const int p = w * 64 + lane;
+      bool ls = false;
+      if (idx[w] >= 0) {
+        const uint64_t e = ev[w];
+        const int st = (int)((e >> 8) & 3);
+        slow |= st == 3;
+        s.sn[p] = (uint8_t)e;
+        ls = st == 1 && (e & 0xFF) != 0;
       }
       const uint64_t m = __ballot(ls);
       if (lane == 0) s.lsm[w] = m;
@@ -599,14 +614,8 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
       e += adv_but_space(text[e]); e += adv_but_space(text[e]);
       e += adv_but_space(text[e]); e += adv_but_space(text[e]);
       uint32_t hv = quad_hash_v2(text + p, e - p);
-      uint32_t probs = quad_lookup(T.quad, hv);
       uint32_t ind = 0;
-      if (probs == 0 && T.quad2.size != 0) {
-        probs = quad_lookup(T.quad2, hv);
-        if (probs) ind = (probs & ~T.quad2.key_mask) | 0x80000000u;
-      } else if (probs) {
-        ind = probs & ~T.quad.key_mask;
-      }
+      const uint32_t probs = quad_probe(T.quad, T.quad2, hv, ind);
       h[r] = hv;
       pr[r] = ind;
       hit[r] = probs != 0;

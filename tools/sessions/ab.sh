@@ -7,6 +7,6 @@ for v in ${VARIANTS:-build}; do
   for c in ${CONFIGS:-c3}; do
     CLD_MI355X_LIB=$PWD/language-detector_amd/$v/libcld_mi355x.so timeout -k 10 300 \
       python bench.py --config $c --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-sub --no-host ${EXTRA:-} > $O/$v.$c.log 2>&1 || { tail -20 $O/$v.$c.log; exit 1; }
-    echo $v $c; tail -1 $O/$v.$c.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print(d['value'], k['wave_ms'], k['long_ms'], k['general_ms'], k['last_batch']['general_docs'], d['passes_hist'])"
+    echo $v $c; tail -1 $O/$v.$c.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print(d['value'], k['wave_ms'], k['long_ms'], k['general_ms'], k['last_batch']['general_docs'], d['passes_hist'], k['last_batch']['long_requeue_reasons'])"
   done
 done
