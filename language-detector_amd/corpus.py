@@ -118,7 +118,7 @@ def c2(n, seed=SEEDS["c2"]):
 BOILERPLATE = b"home | news | contact | login | "
 
 
-C3_MONO_FRAC = 0.25
+C3_MONO_FRAC = float(os.environ.get("CLD_C3_MONO_FRAC", "0.25"))   # (override: experiments only)
 
 
 def c3(n, seed=SEEDS["c3"], page=16384, boiler_frac=0.0, mono_frac=C3_MONO_FRAC):

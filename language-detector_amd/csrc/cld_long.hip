@@ -76,8 +76,15 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 // LDS: the chain walk, the gram hashes and the word scans then read the text
 // at LDS latency instead of through the per-wave HBM slot.  Longer spans run
 // the same code on the slot copy.
+#ifndef LNG_INC
+#define LNG_INC 0
+#endif
 #ifndef LNG_TEXT
+#if LNG_INC
 #define LNG_TEXT 3584                    // the text window; with the emission rings it fills the LDS a wave has
+#else
+#define LNG_TEXT 6128                    // fills the 8 KB the scoring state shares with the Repeats predictor
+#endif
 #endif
 constexpr int kLdsText = LNG_TEXT;
 // Quad spans are scored chunk by chunk as their emissions appear (score_quad):
@@ -87,9 +94,6 @@ constexpr int kLdsText = LNG_TEXT;
 // score_round).  Measured round 3 on MI355X: LNG_INC=1 is bit-exact but slower
 // (C3 0.97M vs 1.16M docs/s, C5 15.9M vs 17.8M; 416 B/lane scratch vs 304),
 // so it stays an A/B variant (make variant V=inc VFLAGS=-DLNG_INC=1).
-#ifndef LNG_INC
-#define LNG_INC 0
-#endif
 constexpr int kPB = 256, kPD = 128, kPX = 256;    // ring capacities (powers of two)
 constexpr int kRingSlack = 8;                      // consumed entries whose offsets may still be read
 // Read-ahead of the slot's streams (bit 1 word starts, 2 quad chain, 4 octa
@@ -166,12 +170,14 @@ struct alignas(16) Smem {
           uint16_t bst[kMaxCh + 1];
           uint16_t st[2][kMaxCh + 1];    // first delta [0] / distinct [1] emission of chunk k
         };
+#if LNG_INC
         struct {                         // chunk-at-a-time scoring (score_quad: quad spans)
           uint16_t pb_off[kPB], pd_off[kPD], px_off[kPX];   // emission offsets, by emission number mod ring
           uint32_t pb_idx[kPB], pd_idx[kPD], px_idx[kPX];   // their tote adds: T.compat.adds[idx]
           uint16_t Eq[kMaxCh];           // the round's chunk plan, once its hit count is final
           uint64_t xlast[4];             // the last distinct adds of an add pass (boost ring update)
         };
+#endif
       };
     };
     uint16_t pred[kPredictionTableSize]; // Repeats predictor, 16-bit codes (pred_code)
@@ -2019,6 +2025,7 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   if constexpr (D) mark_sub(s, lane, 4, t2);
 }
 
+#if LNG_INC
 // ------------------------------------------ quad spans: chunks scored as they fill
 // ScoreQuadScriptSpan's rounds (scoreonescriptspan.cc:1231-1277: GetQuadHits,
 // GetOctaHits, LinearizeAll, ChunkAll, ScoreAllHits) without materialising a
@@ -2624,6 +2631,8 @@ __device__ __forceinline__ bool score_quad(const DevTables& T, Slot& S, Smem& s,
   }
   return true;
 }
+
+#endif  // LNG_INC
 
 __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, bool octa, int lane) {
   if (!s.dbg) return;

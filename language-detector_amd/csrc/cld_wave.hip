@@ -1119,90 +1119,171 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   return true;
 }
 
+// The document level below keeps DocTote slot `lane` (lanes 0-23) in
+// registers: the per-slot arithmetic (close sets, divisions) runs across lanes
+// at once, the control (which slot merges, which pass) on wave-uniform scalars
+// read back with readlane, so no branch on it costs an exec-mask round trip.
+struct SlotRegs {
+  uint32_t key;
+  int val, sc, rl;
+};
+__device__ __forceinline__ SlotRegs load_slots(const DocTote& dt, int lane) {
+  const bool in = lane < 24;
+  const int j = in ? lane : 0;
+  SlotRegs r;
+  r.key = in ? dt.key[j] : kUnusedKey;
+  r.val = in ? dt.value[j] : -1;
+  r.sc = in ? dt.score[j] : 0;
+  r.rl = in ? dt.rel[j] : 0;
+  return r;
+}
+__device__ __forceinline__ void store_slots(DocTote& dt, const SlotRegs& r, int lane) {
+  if (lane < 24) {
+    dt.key[lane] = (uint16_t)r.key;
+    dt.value[lane] = r.val;
+    dt.score[lane] = r.sc;
+    dt.rel[lane] = r.rl;
+  }
+}
+
 // DocTote::Sort(3) (tote.cc:221-250) across lanes 0-23, one lane per slot.
 // Pass s of the reference's partial bubble sort swaps slot s with every later
 // slot whose value beats the current holder (strictly): the holders are the
 // running-maximum records r1 < ... < rm of slots s+1..23.  Afterwards slot s
 // has rm's entry, r1 has s's, and rj has r(j-1)'s; nothing else moves.
 // Unused slots count as value -1 (the reference sets that as it scans).
-__device__ __forceinline__ void sort3_wave(DocTote& dt, int lane) {
+__device__ __forceinline__ void sort3_regs(SlotRegs& r, int lane) {
   const bool in = lane < 24;
-  uint32_t key = in ? dt.key[lane] : kUnusedKey;
-  int val = in ? dt.value[lane] : -1, sc = in ? dt.score[lane] : 0, rl = in ? dt.rel[lane] : 0;
-  if (key == kUnusedKey) val = -1;
+  if (r.key == kUnusedKey) r.val = -1;
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
     // exclusive running max of slots p..lane-1 (values biased to unsigned)
-    const uint32_t m = dpp_scan_incl((in && lane >= p) ? (uint32_t)val ^ 0x80000000u : 0u, 0u, OpMax());
+    const uint32_t m = dpp_scan_incl((in && lane >= p) ? (uint32_t)r.val ^ 0x80000000u : 0u, 0u, OpMax());
     const int ex = (int)(wshr1(m, 0u) ^ 0x80000000u);
-    const uint64_t R = __ballot(in && lane > p && val > ex);
+    const uint64_t R = __ballot(in && lane > p && r.val > ex);
     if (R) {
-      int src = lane;
-      if (lane == p) src = 63 - __builtin_clzll(R);
-      else if ((R >> lane) & 1) {
-        const uint64_t below = R & lanemask_lt(lane);
-        src = below ? 63 - __builtin_clzll(below) : p;
-      }
-      key = (uint32_t)__shfl((int)key, src, 64);
-      val = __shfl(val, src, 64);
-      sc = __shfl(sc, src, 64);
-      rl = __shfl(rl, src, 64);
+      const uint64_t below = R & lanemask_lt(lane);
+      const int src = lane == p ? 63 - __builtin_clzll(R)
+                    : ((R >> lane) & 1) ? (below ? 63 - __builtin_clzll(below) : p) : lane;
+      r.key = (uint32_t)__shfl((int)r.key, src, 64);
+      r.val = __shfl(r.val, src, 64);
+      r.sc = __shfl(r.sc, src, 64);
+      r.rl = __shfl(r.rl, src, 64);
     }
   }
-  if (in) {
-    dt.key[lane] = (uint16_t)key;
-    dt.value[lane] = val;
-    dt.score[lane] = sc;
-    dt.rel[lane] = rl;
-  }
-  if (lane == 0) dt.sorted = 1;
-  wsync();
 }
 
-// Document level (compact_lang_det_impl.cc:1997-2065).  Lanes 0-23 hold the
-// DocTote slots: the partial sort runs across them, and the close-pair and
-// unreliable-language passes run (on lane 0, as written) only when a slot
-// they could change exists -- otherwise they are no-ops there too.  Returns 1
-// with the result written, or 0 when the first pass is not good enough and the
-// Repeats pass must follow (never when `final`).
-// best_effort: kCLDFlagBestEffort (:1998-2000, :1493): no unreliable-language
-// removal and no UNKNOWN for a small return percent.
+// RefineScoredClosePairs (compact_lang_det_impl.cc:1105-1147): slot s, in
+// order, merges into the first later slot of its close set.  The close sets
+// are gathered for all slots at once; the slots that have one (a handful at
+// most) are visited in order on scalars.
+__device__ __forceinline__ void refine_close_pairs_regs(const DevTables& T, SlotRegs& r, int lane) {
+  int cs = lane < 24 ? close_set(T, (int)r.key) : 0;
+  uint64_t todo = __ballot(cs != 0);
+  while (todo) {
+    const int s = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int css = rdl(cs, s);
+    if (css == 0) continue;                                    // emptied by an earlier merge
+    const uint64_t mm = __ballot(lane > s && cs == css);
+    if (!mm) continue;
+    const int s2 = __builtin_ctzll(mm);
+    const bool s_from = rdl(r.val, s) < rdl(r.val, s2);        // the smaller moves into the larger
+    const int from = s_from ? s : s2, to = s_from ? s2 : s;
+    const int fv = rdl(r.val, from), fs = rdl(r.sc, from), fr = rdl(r.rl, from);
+    if (lane == to) { r.val += fv; r.sc += fs; r.rl += fr; }
+    if (lane == from) { r.key = kUnusedKey; r.sc = 0; r.rl = 0; cs = 0; }   // (value stays, as there)
+  }
+}
+
+// ExtractLangEtc (compact_lang_det_impl.cc:1276-1384): slots 0-2 in lanes
+// 0-2, their divisions in parallel; the results as wave-uniform scalars
+// (normalized score of slot `lane` in ns).
+struct DocSum {
+  int lang[3], pct[3];
+  int text_bytes;
+  bool reliable;
+};
+__device__ __forceinline__ DocSum extract_regs(const DevTables& T, const SlotRegs& r, int total, int lane, double& ns) {
+  const int unk = (int)T.unknown_lang;
+  const bool valid = lane < 3 && r.key != kUnusedKey && (int)r.key != unk;
+  const int bc = valid ? r.val : 0;
+  const int rp = valid ? r.rl / (bc ? bc : 1) : 0;
+  ns = (valid && bc > 0) ? (double)((int32_t)((uint32_t)r.sc << 10) / (bc > 0 ? bc : 1)) : 0.0;
+  const int b0 = rdl(bc, 0), b1 = rdl(bc, 1), b2 = rdl(bc, 2);
+  const int t12 = b0 + b1, t123 = t12 + b2;
+  const int tot = total < t123 ? t123 : total;
+  const int div = tot > 1 ? tot : 1;
+  const int cum = lane == 0 ? b0 : lane == 1 ? t12 : t123;
+  const int pc = (cum * 100) / div;
+  int q0 = rdl(pc, 0), q1 = rdl(pc, 1), q2 = rdl(pc, 2);
+  q2 -= q1;
+  q1 -= q0;
+  if (q1 < q2) { ++q1; --q2; }
+  if (q0 < q1) { ++q0; --q1; }
+  const int lg = valid ? (int)r.key : unk;
+  DocSum d;
+  d.lang[0] = rdl(lg, 0); d.lang[1] = rdl(lg, 1); d.lang[2] = rdl(lg, 2);
+  d.pct[0] = q0; d.pct[1] = q1; d.pct[2] = q2;
+  d.text_bytes = tot;
+  d.reliable = rdl(valid ? 1 : 0, 0) && rdl(rp, 0) >= 41;
+  if (100 - (q0 + q1 + q2) > 20) d.reliable = false;
+  return d;
+}
+
+__device__ __forceinline__ double rdl_f64(double v, int l) {
+  return __longlong_as_double((long long)rdl64((uint64_t)__double_as_longlong(v), l));
+}
+
+// Document level (compact_lang_det_impl.cc:1997-2065).  Returns 1 with the
+// result written, or 0 when the first pass is not good enough and the Repeats
+// pass must follow (never when `final`).  best_effort: kCLDFlagBestEffort
+// (:1998-2000, :1493): no unreliable-language removal and no UNKNOWN for a
+// small return percent.
 __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
                                int lane, bool best_effort = false) {
-  if (__ballot(lane < 24 && close_set(T, dt.key[lane < 24 ? lane : 0]) != 0)) {
-    if (lane == 0) refine_scored_close_pairs(T, dt);
-    wsync();
-  }
-  sort3_wave(dt, lane);
-  int ok = 1;
-  Extract x;
-  if (lane == 0) {
-    extract_lang_etc(T, dt, total, x);
-    const bool good = final || total <= 256 || (x.reliable && x.pct3[0] >= 70) ||
-                      (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
-    if (!good) ok = 0;
-  }
-  ok = rdl(ok, 0);
-  if (ok) {
-    bool unrel = false;
-    if (lane < 24 && !best_effort) {
-      const int bytes = dt.value[lane];
-      unrel = dt.key[lane] != kUnusedKey && bytes != 0 && dt.rel[lane] / bytes < 41;
-    }
+  SlotRegs r = load_slots(dt, lane);
+  refine_close_pairs_regs(T, r, lane);
+  sort3_regs(r, lane);
+  double ns;
+  DocSum x = extract_regs(T, r, total, lane, ns);
+  const bool good = final || total <= 256 || (x.reliable && x.pct[0] >= 70) ||
+                    (x.reliable && x.pct[0] + x.pct[1] >= 93);
+  if (!good) return 0;
+  if (!best_effort) {
+    // RemoveUnreliableLanguages (:997-1101) only when some slot is unreliable
+    const bool unrel = lane < 24 && r.key != kUnusedKey && r.val != 0 && r.rl / (r.val ? r.val : 1) < 41;
     if (__ballot(unrel)) {
+      store_slots(dt, r, lane);
+      if (lane == 0) dt.sorted = 1;                            // (DocTote::Find then scans linearly)
+      wsync();
       if (lane == 0) remove_unreliable_languages(T, dt);
       wsync();
-      sort3_wave(dt, lane);
-      if (lane == 0) extract_lang_etc(T, dt, total, x);
-    }
-    if (lane == 0) {
-      bool rel;
-      const int summary = calc_summary_lang(T, total, x, rel, best_effort);
-      write_result(out, x, summary, rel);
+      r = load_slots(dt, lane);
+      sort3_regs(r, lane);
+      x = extract_regs(T, r, total, lane, ns);
     }
   }
-  wsync();
-  return ok;
+  // CalcSummaryLang (:1414-1522) on the scalars
+  Extract e;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { e.lang3[i] = x.lang[i]; e.pct3[i] = x.pct[i]; e.rp3[i] = 0; e.ns3[i] = 0.0; }
+  e.text_bytes = x.text_bytes;
+  e.reliable = x.reliable;
+  bool rel;
+  const int summary = calc_summary_lang(T, total, e, rel, best_effort);
+  const double n0 = rdl_f64(ns, 0), n1 = rdl_f64(ns, 1), n2 = rdl_f64(ns, 2);
+  if (lane == 0) {
+    cld_result o;
+    o.lang3[0] = (uint16_t)x.lang[0]; o.lang3[1] = (uint16_t)x.lang[1]; o.lang3[2] = (uint16_t)x.lang[2];
+    o.summary_lang = (uint16_t)summary;
+    o.percent3[0] = (int8_t)x.pct[0]; o.percent3[1] = (int8_t)x.pct[1]; o.percent3[2] = (int8_t)x.pct[2];
+    o.is_reliable = rel ? 1 : 0;
+    o.text_bytes = x.text_bytes;
+    o.normalized3[0] = n0; o.normalized3[1] = n1; o.normalized3[2] = n2;
+    *out = o;
+  }
+  return 1;
 }
 
 // ------------------------------------------------------ the document
@@ -1220,6 +1301,13 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       t_stage = t;
     }
   };
+  // -DWAVE_STOP=k (instruction-count A/B only, wrong results): the document
+  // ends after stage k of its first span, so PMC differences price each stage
+#ifdef WAVE_STOP
+#define WAVE_STOP_AT(k) if (WAVE_STOP == (k)) return true
+#else
+#define WAVE_STOP_AT(k) (void)0
+#endif
   const int unk = (int)T.unknown_lang;
   if (L == 0) {
     if (lane == 0) {
@@ -1232,6 +1320,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
   }
   if (!load_document<CAP>(T, g, L, s, lane)) return false;
   mark(0);
+    WAVE_STOP_AT(0);
   if (lane == 0) s.dt.init();
   if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
   wsync();
@@ -1240,9 +1329,11 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     int ulscript = 0;
     int tb = next_span<CAP>(T, s, L, next, ulscript, lane);
     mark(1);
+    WAVE_STOP_AT(1);
     if (tb == 0) break;
     tb = lower_span<CAP>(T, s, tb, lane);
     mark(2);
+    WAVE_STOP_AT(2);
     if (tb < 0) return false;
     int rt = rtype_of(T, ulscript);
     if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
@@ -1259,14 +1350,17 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       } else {
         endo = quad_hits<CAP>(T, s, tb, nb, lane);
         mark(3);
+        WAVE_STOP_AT(3);
         if (endo < 0) return false;
         if (!octa_hits<CAP>(T, s, endo, nd, nx, lane)) return false;
         mark(4);
+        WAVE_STOP_AT(4);
       }
       if (endo < tb) return false;     // a second round would be needed (never for short documents)
       int rsel;
       if (1 < tb && !score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane, pri)) return false;
       mark(5);
+      WAVE_STOP_AT(5);
     }
     total += tb;
   }
