@@ -32,6 +32,15 @@
 namespace cld {
 namespace wave {
 
+// -DWAVE_STOP=k (instruction-count A/B only, wrong results): the wave ends
+// (s_endpgm) at stop point k of its document's first span, so PMC differences
+// between variants price each stage (tools/sessions/r3c_stages.sh).
+#ifdef WAVE_STOP
+#define WAVE_STOP_AT(k) if (WAVE_STOP == (k)) __builtin_amdgcn_endpgm()
+#else
+#define WAVE_STOP_AT(k) (void)0
+#endif
+
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t uflu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t ufl64(uint64_t v) {
@@ -130,6 +139,7 @@ struct Cfg {
   static constexpr int LB = (SB * 3) / 2 + 64;      // lowered span (max per-char growth 1.5x) + hash read pad
   static constexpr int NR = 2;                      // registers of 64 entries: quad chain, words
   static constexpr int NB = NR * 64;                // base hits / quad chain / words
+  static constexpr int QM = ((LB + 63) / 64) * 2;   // u32 words of chain marks (whole u64 windows)
   static constexpr int NE = 160;                    // base emissions (<= 2 langprobs per hit; overflow requeues)
   static constexpr int ND = 96;
   static constexpr int NX = 160;
@@ -152,6 +162,11 @@ struct Smem {
   uint64_t brk[C::NM];                // letters that end a run for the current span script
   union alignas(16) {                 // one span's life: raw text -> base hits -> chunk ids
     uint8_t sbuf[C::SB];              //   span text (raw); dead once lowered
+    struct {                          //   quad chain (quad_hits, before its base hits are written)
+      uint32_t qmark[C::QM];          //   chain entries as bits over lowered-text positions
+      uint16_t qws[C::NB];            //   word starts
+      uint16_t qchn[C::NB];           //   chain entries, in order
+    };
     struct {                          //   base hits before expansion (hit streams -> scoring)
       uint32_t b_ind[C::NB];
       uint16_t b_off[C::NB];
@@ -543,63 +558,70 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   if (text[start] == ' ') ++start;
   // The chain never jumps over a space: it enters every word at its first
   // byte, and a word's entries depend on that word alone (k_long's
-  // build_chain).  One lane walks one word; a prefix sum places the entries.
-  uint16_t* wst = s.a.nxq;               // word starts
-  uint16_t* chn = s.a.nxq + C::NB;       // chain entries, in order
+  // build_chain).  First, for every text position at once, GetQuadHits'
+  // step from there (cldutil.cc:340-400): the quad [p, p4) of four characters
+  // (stopping at a space), the next chain position and whether the word's
+  // chain ends at p -- packed as (p4 - p) | (next - p) << 5 | end << 10 --
+  // and the word starts.  Then one lane walks one word on those steps, one
+  // LDS read per entry, marking its entries as bits over text positions: in
+  // text order the marks are the chain.
+  uint16_t* nfo = s.a.nxq;
   int nws = 0;
   for (int w0 = start; w0 < limit; w0 += 64) {
-    const int x = w0 + lane;
-    const bool isws = x < limit && (x == start || text[x - 1] == ' ');
+    const int p = w0 + lane;
+    const bool in = p < limit;
+    const int pc = in ? p : start;
+    const int a1 = pc + adv_but_space(text[pc]);
+    const int a2 = a1 + adv_but_space(text[a1]);
+    const uint32_t c2 = text[a2];
+    const int a3 = a2 + adv_but_space((uint8_t)c2);
+    const int a4 = a3 + adv_but_space(text[a3]);
+    const int nx = a2 + adv_space_vowel((uint8_t)c2);
+    const bool fin = text[a4] == ' ' || a2 >= limit || nx >= limit;
+    if (in) nfo[p] = (uint16_t)((a4 - p) | ((nx - p) << 5) | (fin ? 0x400 : 0));
+    const bool isws = in && (p == start || text[p - 1] == ' ');
     const uint64_t m = __ballot(isws);
     if (isws) {
       const int k = nws + __popcll(m & lanemask_lt(lane));
-      if (k < C::NB) wst[k] = (uint16_t)x;
+      if (k < C::NB) s.qws[k] = (uint16_t)p;
     }
     nws += __popcll(m);
   }
   if (nws > C::NB) return -1;
+  if (lane < C::QM) s.qmark[lane] = 0u;
   wsync();
-  int n = 0;
+  WAVE_STOP_AT(31);
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) {
+    if (r * 64 >= nws) break;
     const int i = r * 64 + lane;
-    int cnt = 0, w = 0;
     if (i < nws) {
-      w = wst[i];
-      int src = w;
+      int p = s.qws[i];
       for (;;) {
-        ++cnt;
-        int e = src;
-        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-        const int mid = e;
-        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-        if (text[e] == ' ' || mid >= limit) break;
-        src = mid + adv_space_vowel(text[mid]);
-        if (src >= limit) break;
+        atomicOr(&s.qmark[p >> 5], 1u << (p & 31));
+        const uint32_t f = nfo[p];
+        if (f & 0x400) break;
+        p += (f >> 5) & 31;
       }
     }
-    const int pre = n + excl_scan(cnt, lane);
-    const int tot = rdl(pre + cnt, 63);
-    if (tot > C::NB) return -1;
-    if (cnt) {
-      int src = w, k = pre;
-      for (;;) {
-        chn[k++] = (uint16_t)src;
-        int e = src;
-        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-        const int mid = e;
-        e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-        if (text[e] == ' ' || mid >= limit) break;
-        src = mid + adv_space_vowel(text[mid]);
-        if (src >= limit) break;
-      }
-    }
-    n = tot;
   }
   wsync();
+  int n = 0;
+  for (int w = start >> 6; w * 64 < limit; ++w) {
+    const uint64_t m = ufl64(*reinterpret_cast<const uint64_t*>(&s.qmark[2 * w]));
+    if ((m >> lane) & 1) {
+      const int k = n + __popcll(m & lanemask_lt(lane));
+      if (k < C::NB) s.qchn[k] = (uint16_t)(w * 64 + lane);
+    }
+    n += __popcll(m);
+  }
+  if (n > C::NB) return -1;
+  wsync();
+  WAVE_STOP_AT(32);
   int cp[C::NR];
 #pragma unroll
-  for (int r = 0; r < C::NR; ++r) cp[r] = chn[r * 64 + lane];
+  for (int r = 0; r < C::NR; ++r) cp[r] = s.qchn[r * 64 + lane];
+  wsync();                               // (the base hits below overwrite the chain lists)
   const int end = n == 0 ? start : limit;
   // hashes and probes per chain entry
   uint32_t h[C::NR], pr[C::NR];
@@ -610,10 +632,7 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
     h[r] = 0; pr[r] = 0; hit[r] = false;
     if (i < n) {
       const int p = cp[r];
-      int e = p;
-      e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-      e += adv_but_space(text[e]); e += adv_but_space(text[e]);
-      uint32_t hv = quad_hash_v2(text + p, e - p);
+      uint32_t hv = quad_hash_v2(text + p, (int)(nfo[p] & 31));
       uint32_t ind = 0;
       const uint32_t probs = quad_probe(T.quad, T.quad2, hv, ind);
       h[r] = hv;
@@ -621,6 +640,7 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
       hit[r] = probs != 0;
     }
   }
+  WAVE_STOP_AT(33);
   // repeat filter: drop a hit equal to either of the last two kept hits.
   // Assume every hit is kept: then a hit's two predecessors are the previous
   // hit lanes; from the first hit that equals one of them, resolve in order.
@@ -677,6 +697,26 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   return end;
 }
 
+// OctaHash40 (cldutil_shared.cc:234-354) of n <= 8 bytes already in two
+// little-endian dwords (lo = bytes 0-3, hi = 4-7), with the same 64-bit sums.
+__device__ __forceinline__ uint64_t octa_hash40_le8(uint32_t lo, uint32_t hi, int n, bool sp_before, bool sp_after) {
+  const uint64_t pre = (sp_before ? 0x00004444ull : 0ull) | (sp_after ? 0x44440000ull : 0ull);
+  const uint32_t m = kWordMask0[n & 3];
+  uint64_t w0 = (uint64_t)(n <= 4 ? (lo & m) : lo);
+  uint64_t sum = w0;
+  w0 ^= w0 >> 3;
+  if (n > 4) {
+    uint64_t w1 = (uint64_t)(hi & m);
+    sum += w1;
+    w1 ^= w1 << 4;
+    w0 += w1;
+  }
+  sum += sum >> 17;
+  sum += sum >> 9;
+  sum = (sum & 0xFF) << 32;
+  return (w0 ^ pre) + sum;
+}
+
 // GetOctaHits (cldutil.cc:416-533): one lane per space-terminated word.
 template <int CAP>
 __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int& nd, int& nx, int lane) {
@@ -708,6 +748,8 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
     if (i < nw) {
       const int a = i == 0 ? start : s.a.wsp[i - 1] + 1;
       const int e = s.a.wsp[i];
+      ws[r] = a;
+      pws[r] = i <= 1 ? start : s.a.wsp[i - 2] + 1;
       int we = a, q = a, cc = 0;
       while (q < e) {
         ++cc;
@@ -715,8 +757,6 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
         if (cc <= 8) we = q;
         else break;
       }
-      ws[r] = a;
-      pws[r] = i <= 1 ? start : s.a.wsp[i - 2] + 1;
       wh[r] = octa_hash40(text + a, we - a);
     }
   }
@@ -849,6 +889,38 @@ __device__ int cjk_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, in
   return next;
 }
 
+// DocTote::Add (tote.cc:127-175) with the wave: lanes 0-23 read their slot's
+// key, the reference's probe order (slot k&15, its partner ^8, then (k&7)+16;
+// a free one in the same order; else the smallest value) is resolved on
+// ballots and scalars, and lane 0 writes the one slot that changes.
+__device__ __forceinline__ void dt_add_wave(DocTote& dt, int k, int bytes, int sc, int r, int lane) {
+  const int s0 = k & 15, s1 = s0 ^ 8, s2 = (k & 7) + 16;
+  const uint32_t key = lane < 24 ? dt.key[lane < 24 ? lane : 0] : (uint32_t)kUnusedKey;
+  const uint64_t cand = (1ull << s0) | (1ull << s1) | (1ull << s2);
+  const uint64_t same = __ballot(key == (uint32_t)k) & cand;
+  const uint64_t fr = __ballot(key == (uint32_t)kUnusedKey) & cand;
+  const uint64_t m = same ? same : fr;
+  int a;
+  if (m) {
+    a = ((m >> s0) & 1) ? s0 : ((m >> s1) & 1) ? s1 : s2;
+  } else {
+    const int v0 = dt.value[s0], v1 = dt.value[s1], v2 = dt.value[s2];
+    a = s0;
+    int va = v0;
+    if (v1 < va) { a = s1; va = v1; }
+    if (v2 < va) a = s2;
+  }
+  if (lane == 0) {
+    ++dt.incr_count;
+    if (same) {
+      dt.value[a] += bytes; dt.score[a] += sc; dt.rel[a] += r * bytes;
+    } else {
+      dt.key[a] = (uint16_t)k; dt.value[a] = bytes; dt.score[a] = sc; dt.rel[a] = r * bytes;
+    }
+  }
+  wsync();
+}
+
 // ------------------------------------- stage 4: linearize + chunk + score
 // LinearizeAll/ChunkAll/ScoreAllHits (scoreonescriptspan.cc:856-1031, 208-302)
 // without materialising linear[]: every emitted langprob gets its chunk from
@@ -912,6 +984,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     if (lp) { s.x_off[o] = off; s.x_ind[o] = lp; }
     ex = rdl(o + (lp != 0), 63);
   }
+  WAVE_STOP_AT(51);
   // chunk plan from the base-hit count (ChunkAll :978-1031)
   int K = 0;
   if (nb <= 0) {
@@ -936,6 +1009,16 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   // emissions [E_{k-1} - 1, E_k - 1); a delta / distinct emission at offset o
   // follows 1 + #(base emissions with offset < o) base entries and lands in the
   // first chunk with that count < E_k, i.e. with o <= theta_k = be_off[E_k - 2].
+  if (K == 1) {
+    // one chunk (most short spans): it takes every stream whole and opens with
+    // the seed at offset 1 (hit offsets are >= 1), so no chunk search is needed
+    if (lane < 7) {
+      const int v = lane == 0 ? 0x7FFFFFFF : lane == 2 ? eb : lane == 4 ? ed : lane == 6 ? ex : 0;
+      if (lane == 0) s.theta[0] = v;
+      else s.st[(lane - 1) >> 1][(lane - 1) & 1] = (uint16_t)v;
+    }
+    if (lane == 0) s.lo[0] = 1u;
+  } else {
   if (lane <= K) {                                     // K <= MAXCH < 64
     const int k = lane;
     if (k < K) {
@@ -987,6 +1070,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     if (xs < xe) m = min(m, (uint32_t)s.x_off[xs]);
     s.lo[k] = m;
   }
+  }
   // linear order starts with the seed at `lowest` (= 1 for the only round)
   const uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
@@ -994,6 +1078,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   const int nboost = pri ? 2 * kMaxBoosts : kMaxBoosts;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
   wsync();
+  WAVE_STOP_AT(52);
   for (int k = 0; k < K; ++k) {
     const int seedn = k == 0 ? 1 : 0;
     const int bs = s.st[0][k], nB = s.st[0][k + 1] - bs, ds = s.st[1][k], nD = s.st[1][k + 1] - ds;
@@ -1004,18 +1089,18 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     // langprobs up to the end of the chunk and, for a hinted document, the four
     // ApplyHints prior boosts of this script class (cld_detect_batch_ex: 16
     // langprobs per document, boost latn[4] othr[4], whack latn[4] othr[4])
+    // (every candidate is read, with a clamped index, and one select chain
+    // picks: no branch per stream)
     auto chunk_lp = [&](int t) -> uint32_t {
-      if (t >= tot) return 0u;
-      int u = t;
-      if (u < seedn) return seed;
-      if ((u -= seedn) < nB) return s.a.e.be_lp[bs + u];
-      if ((u -= nB) < nD) return s.d_ind[ds + u];
-      if ((u -= nD) < nX) return s.x_ind[xs + u];
-      if ((u -= nX) < kMaxBoosts) {
-        const int v = xe - kMaxBoosts + u;
-        return v < 0 ? s.ring[rs][v + kMaxBoosts] : s.x_ind[v];
-      }
-      return gld(pri + 4 * rs + (u - kMaxBoosts));
+      const int u0 = t - seedn, u1 = u0 - nB, u2 = u1 - nD, u3 = u2 - nX, u4 = u3 - kMaxBoosts;
+      const uint32_t vb = s.a.e.be_lp[min(max(bs + u0, 0), C::NE - 1)];
+      const uint32_t vd = s.d_ind[min(max(ds + u1, 0), C::ND - 1)];
+      const int v = xe - kMaxBoosts + u3;                  // boost u3: the v-th distinct emission
+      const uint32_t vx = s.x_ind[min(max(u3 < 0 ? xs + u2 : v, 0), C::NX - 1)];
+      const uint32_t vr = s.ring[rs][min(max(v + kMaxBoosts, 0), kMaxBoosts - 1)];
+      const uint32_t vp = pri ? gld(pri + 4 * rs + min(max(u4, 0), kMaxBoosts - 1)) : 0u;
+      const uint32_t r = u0 < 0 ? seed : u1 < 0 ? vb : u2 < 0 ? vd : u3 < 0 ? vx : u4 < 0 ? (v < 0 ? vr : vx) : vp;
+      return t < tot ? r : 0u;
     };
     // ProcessProbV2Tote (cldutil.cc:128-138): bytes 5..7 of the kLgProbV2Tbl row,
     // gathered before the tote is cleared so the L2 round trip overlaps it
@@ -1077,6 +1162,7 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     }
     wsync();
   }
+  WAVE_STOP_AT(53);
   // SetChunkSummary (scoreonescriptspan.cc:60-96) for every chunk at once, one
   // lane per chunk; the DocTote adds then run in chunk order on lane 0
   int sum_lang = 0, sum_bytes = 0, sum_rel = 0;
@@ -1102,9 +1188,10 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     cs1 = s1;
   }
   const int nsum = K < kMaxSummaries ? K : kMaxSummaries;
+  WAVE_STOP_AT(54);
   for (int k = 0; k < nsum; ++k) {
     const int l1 = rdl(sum_lang, k), by = rdl(sum_bytes, k), sc = rdl(cs1, k), rl = rdl(sum_rel, k);
-    if (lane == 0) s.dt.add((uint16_t)l1, by, sc, rl);
+    dt_add_wave(s.dt, l1, by, sc, rl, lane);
   }
   // the ring keeps the last four distinct langprobs
   if (lane == 0) {
@@ -1243,13 +1330,16 @@ __device__ __forceinline__ double rdl_f64(double v, int l) {
 __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
                                int lane, bool best_effort = false) {
   SlotRegs r = load_slots(dt, lane);
+  WAVE_STOP_AT(61);
   refine_close_pairs_regs(T, r, lane);
   sort3_regs(r, lane);
   double ns;
+  WAVE_STOP_AT(62);
   DocSum x = extract_regs(T, r, total, lane, ns);
   const bool good = final || total <= 256 || (x.reliable && x.pct[0] >= 70) ||
                     (x.reliable && x.pct[0] + x.pct[1] >= 93);
   if (!good) return 0;
+  WAVE_STOP_AT(63);
   if (!best_effort) {
     // RemoveUnreliableLanguages (:997-1101) only when some slot is unreliable
     const bool unrel = lane < 24 && r.key != kUnusedKey && r.val != 0 && r.rl / (r.val ? r.val : 1) < 41;
@@ -1301,13 +1391,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       t_stage = t;
     }
   };
-  // -DWAVE_STOP=k (instruction-count A/B only, wrong results): the document
-  // ends after stage k of its first span, so PMC differences price each stage
-#ifdef WAVE_STOP
-#define WAVE_STOP_AT(k) if (WAVE_STOP == (k)) return true
-#else
-#define WAVE_STOP_AT(k) (void)0
-#endif
+
   const int unk = (int)T.unknown_lang;
   if (L == 0) {
     if (lane == 0) {
