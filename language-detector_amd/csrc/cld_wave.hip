@@ -544,6 +544,28 @@ __device__ int lower_span(const DevTables& T, Smem<CAP>& s, int text_bytes, int 
   return obase - 3;
 }
 
+// QuadHashV2 (cldutil_shared.cc:167-202, the same arithmetic as quad_hash_v2)
+// of the n bytes at LDS text position p: the words at p, p+4, p+8 from four
+// aligned dword reads, the bytes before and after from two byte reads.
+__device__ __forceinline__ uint32_t quad_hash_lds(const uint8_t* text, int p, int n) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(text);
+  const int i0 = p >> 2;
+  const uint32_t sh = (uint32_t)(p & 3);
+  const uint32_t x0 = tw[i0], x1 = tw[i0 + 1], x2 = tw[i0 + 2], x3 = tw[i0 + 3];
+  const uint32_t y0 = __builtin_amdgcn_alignbyte(x1, x0, sh), y1 = __builtin_amdgcn_alignbyte(x2, x1, sh),
+                 y2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+  const uint32_t pre = (text[p - 1] == ' ' ? 0x00004444u : 0u) | (text[p + n] == ' ' ? 0x44440000u : 0u);
+  const uint32_t m = (n & 3) ? (1u << (8 * (n & 3))) - 1u : 0xFFFFFFFFu;   // kWordMask0[n & 3]
+  const uint32_t a0 = n <= 4 ? (y0 & m) : y0;
+  const uint32_t w0 = (a0 ^ (a0 >> 3)) ^ pre;
+  const uint32_t a1 = n <= 8 ? (y1 & m) : y1;
+  const uint32_t w1 = a1 ^ (a1 << 4);
+  const uint32_t a2 = y2 & m;
+  const uint32_t w2 = a2 ^ (a2 << 2);
+  const uint32_t r = n <= 4 ? w0 : n <= 8 ? w0 + w1 : w0 + w1 + w2;
+  return n == 0 ? 0u : r;
+}
+
 // ------------------------------------------------ stage 3: hit streams
 // GetQuadHits (cldutil.cc:315-405).  The chain of quad starts is a pure
 // function of position, so next[] is computed for every byte in parallel and
@@ -627,12 +649,14 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   uint32_t h[C::NR], pr[C::NR];
   bool hit[C::NR];
 #pragma unroll
+  for (int r = 0; r < C::NR; ++r) { h[r] = 0; pr[r] = 0; hit[r] = false; }
+#pragma unroll
   for (int r = 0; r < C::NR; ++r) {
+    if (r * 64 >= n) break;                // (uniform: registers past the chain hold nothing)
     const int i = r * 64 + lane;
-    h[r] = 0; pr[r] = 0; hit[r] = false;
     if (i < n) {
       const int p = cp[r];
-      uint32_t hv = quad_hash_v2(text + p, (int)(nfo[p] & 31));
+      uint32_t hv = quad_hash_lds(text, p, (int)(nfo[p] & 31));
       uint32_t ind = 0;
       const uint32_t probs = quad_probe(T.quad, T.quad2, hv, ind);
       h[r] = hv;
@@ -648,6 +672,8 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   uint32_t A = 0, B = 0;                  // last two kept hashes (the reference's pq0/pq1 as a set)
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) {
+    keep[r] = 0;
+    if (r * 64 >= n) continue;
     const uint64_t hm = __ballot(hit[r]);
     const uint32_t hv = h[r];
     const uint64_t hb = hm & lanemask_lt(lane);
@@ -697,26 +723,6 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   return end;
 }
 
-// OctaHash40 (cldutil_shared.cc:234-354) of n <= 8 bytes already in two
-// little-endian dwords (lo = bytes 0-3, hi = 4-7), with the same 64-bit sums.
-__device__ __forceinline__ uint64_t octa_hash40_le8(uint32_t lo, uint32_t hi, int n, bool sp_before, bool sp_after) {
-  const uint64_t pre = (sp_before ? 0x00004444ull : 0ull) | (sp_after ? 0x44440000ull : 0ull);
-  const uint32_t m = kWordMask0[n & 3];
-  uint64_t w0 = (uint64_t)(n <= 4 ? (lo & m) : lo);
-  uint64_t sum = w0;
-  w0 ^= w0 >> 3;
-  if (n > 4) {
-    uint64_t w1 = (uint64_t)(hi & m);
-    sum += w1;
-    w1 ^= w1 << 4;
-    w0 += w1;
-  }
-  sum += sum >> 17;
-  sum += sum >> 9;
-  sum = (sum & 0xFF) << 32;
-  return (w0 ^ pre) + sum;
-}
-
 // GetOctaHits (cldutil.cc:416-533): one lane per space-terminated word.
 template <int CAP>
 __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int& nd, int& nx, int lane) {
@@ -742,9 +748,11 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
   uint64_t wh[C::NR];
   int ws[C::NR], pws[C::NR];
 #pragma unroll
+  for (int r = 0; r < C::NR; ++r) { wh[r] = 0; ws[r] = 0; pws[r] = 0; }
+#pragma unroll
   for (int r = 0; r < C::NR; ++r) {
+    if (r * 64 >= nw) break;
     const int i = r * 64 + lane;
-    wh[r] = 0; ws[r] = 0; pws[r] = 0;
     if (i < nw) {
       const int a = i == 0 ? start : s.a.wsp[i - 1] + 1;
       const int e = s.a.wsp[i];
@@ -808,6 +816,7 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
   bool over = false;
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) {
+    if (r * 64 >= nw) break;
     uint32_t pp = 0, xp = 0, dp = 0;
     const bool k = (keep[r] >> lane) & 1;
     if (k) {
