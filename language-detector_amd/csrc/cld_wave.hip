@@ -261,43 +261,39 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
     // round trip for the document instead of one per 64-byte window
     int idx[C::NM];
 #pragma unroll
+    for (int w = 0; w < C::NM; ++w) idx[w] = -1;
+#pragma unroll
     for (int w = 0; w < C::NM; ++w) {
+      if (w * 64 >= L) break;                           // (uniform)
+      // branch-free per byte: the document is zero-padded to DOC bytes
       const int p = w * 64 + lane;
-      idx[w] = -1;
-      if (p < L) {
-        const uint32_t c = s.doc[p];
-        if ((c & 0xC0) == 0x80) {
-          ++conts;
-        } else {
-          const int n = utf8_len((uint8_t)c);
-          const uint32_t b1 = s.doc[p + 1], b2 = s.doc[p + 2];
-          if (n > 3 || p + n > L || (n >= 2 && (b1 & 0xC0) != 0x80) || (n == 3 && (b2 & 0xC0) != 0x80)) {
-            slow = 1;
-          } else {
-            need += n - 1;
-            idx[w] = cpt_index(c, b1, b2, n);
-          }
-        }
-      }
+      const uint32_t c = s.doc[p], b1 = s.doc[p + 1], b2 = s.doc[p + 2];
+      const bool in = p < L;
+      const bool cont = in && (c & 0xC0) == 0x80, lead = in && !cont;
+      const int n = utf8_len((uint8_t)c);
+      const bool bad = lead && (n > 3 || p + n > L || (n >= 2 && (b1 & 0xC0) != 0x80) || (n == 3 && (b2 & 0xC0) != 0x80));
+      conts += cont ? 1 : 0;
+      slow |= bad ? 1 : 0;
+      const bool ok = lead && !bad;
+      need += ok ? n - 1 : 0;
+      idx[w] = ok ? cpt_index(c, b1, b2, n) : -1;
     }
     uint64_t ev[C::NM];
 #pragma unroll
     for (int w = 0; w < C::NM; ++w) ev[w] = idx[w] >= 0 ? gld(T.cpt + idx[w]) : 0ull;
+    uint64_t lm[C::NM];
 #pragma unroll
     for (int w = 0; w < C::NM; ++w) {
+      // script number at every byte (0 off the lead bytes: only lead bytes are read)
       const int p = w * 64 + lane;
-      bool ls = false;
-      if (idx[w] >= 0) {
-        const uint64_t e = ev[w];
-        const int st = (int)((e >> 8) & 3);
-        slow |= st == 3;
-        s.sn[p] = (uint8_t)e;
-        ls = st == 1 && (e & 0xFF) != 0;
-      }
-      const uint64_t m = __ballot(ls);
-      if (lane == 0) s.lsm[w] = m;
+      const uint64_t e = ev[w];
+      const int st = (int)((e >> 8) & 3);
+      slow |= st == 3 ? 1 : 0;
+      s.sn[p] = (uint8_t)e;
+      lm[w] = __ballot(st == 1 && (e & 0xFF) != 0);
     }
-    slow |= (wsum(conts) != wsum(need)) ? 1 : 0;
+    if (lane < C::NM) s.lsm[lane] = pick(lm, lane);
+    slow |= wsum(conts - need) != 0 ? 1 : 0;               // every continuation byte is claimed
     if (__ballot(slow != 0) == 0) {
       if (lane < 4) s.sn[L + lane] = (uint8_t)script_num(T, dv, L + lane);
       wsync();
@@ -1180,18 +1176,21 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     const int lo = lo_k == 0xFFFFFFFFu ? dummy_off : (int)lo_k;
     int hi = dummy_off;
     if (lane + 1 < K && s.lo[lane + 1] != 0xFFFFFFFFu) hi = (int)s.lo[lane + 1];
-    const int lang1 = from_per_script_number(T, ulscript, (uint8_t)ck1);
-    const int lang2 = from_per_script_number(T, ulscript, (uint8_t)ck2);
+    // language, close set and expected score of both keys: one gather each
+    // from the per-GPU key table (lng::keytab_eval: FromPerScriptNumber,
+    // close sets, kAvgDeltaOctaScore)
+    const uint64_t* kt = T.keytab + 256 * (uint32_t)ulscript;
+    const uint64_t i1 = gld(kt + (uint8_t)ck1), i2 = gld(kt + (uint8_t)ck2);
+    const int lang1 = (int)(i1 & 0xFFFF);
     const int len = hi - lo;
     int actual = 0;
     if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
-    const int esub = lang1 * 4 + lscript4(T, ulscript);
-    const int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? gld(T.expected + (esub)) : 0;
+    const int expected = (int16_t)(uint16_t)(i1 >> 32);
     const uint16_t bytes = (uint16_t)len, grams = (uint16_t)cgr;
     const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2;
     int rd = (uint8_t)reliability_delta(s1, s2, grams);
-    const int c1 = close_set(T, lang1);
-    if (c1 != 0 && c1 == close_set(T, lang2)) rd = 100;
+    const int c1 = (int)((i1 >> 16) & 0xFFFF);
+    if (c1 != 0 && c1 == (int)((i2 >> 16) & 0xFFFF)) rd = 100;
     const int rsc = (uint8_t)reliability_expected(actual, expected);
     sum_lang = (uint16_t)lang1; sum_bytes = bytes; sum_rel = rd < rsc ? rd : rsc;
     cs1 = s1;
