@@ -1,0 +1,308 @@
+// cld_html.hip -- HTML documents (cld_detect_batch_ex with CLD_FLAG_HTML,
+// is_plain_text = false) on the parallel kernels.
+//
+// In HTML mode the reference's span scanner (getonescriptspan.cc:592-1027)
+// differs from plain text in three ways only, all local to the bytes it meets:
+//   * a '<' it reaches starts a tag, skipped by ScanToPossibleLetter (:150-203,
+//     503-541), and a tag ends a run as any non-letter does;
+//   * a '&' it reaches is an entity (ReadEntity, :393-451): a decoded character
+//     is copied into the span in its place, an undecodable '&' is dropped (one
+//     byte consumed, nothing copied, the run goes on);
+//   * the lowercaser takes the HTML half of its remap pairs (:755-762).
+// Every '<' and '&' outside a skipped tag or entity is reached (the scanner
+// stops at both), so one left-to-right pass per document -- k_html_rewrite,
+// one lane per document -- rewrites the page into a plain document with the
+// same spans: each tag becomes one space, each entity its decoded bytes, a
+// dropped '&' nothing, and the page keeps its length (spaces after the text:
+// trailing spaces add nothing to any span).  k_wave / k_long then score it as
+// plain text.  Two details keep them exact:
+//   * a script lookahead (the next character's script, :1009-1016) that lands
+//     on an entity saw the raw '&' (script 0): the rewrite marks those
+//     positions in hflag, and the span builders read script 0 there;
+//   * the lowercaser's HTML half: a page holding a character whose HTML-mode
+//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, or
+//     more than kHtmlRewriteMax bytes (the span soft limit reads the raw length,
+//     :828-833) is not rewritten and stays on k_general.
+// A rewritten page that k_wave / k_long re-queue goes to k_general, which
+// scores the original page in HTML mode.
+//
+// One wavefront per page, in three steps (the reference's own pass is
+// sequential, but only its '<' / '&' stops carry state):
+//   1. the page goes to LDS; every '<' and '&' of it is a candidate; each
+//      lane evaluates one '&' as if the scan reached it (ReadEntity: bytes
+//      consumed, bytes decoded) into an LDS list;
+//   2. the scan's order decides which candidates it reaches: a candidate
+//      inside an earlier reached tag or entity is skipped (a scalar walk over
+//      the list, 64 candidates per register); a reached '<' is scanned there,
+//      by the whole wave, 64 bytes per step (scan_tag_wave);
+//   3. per 64-byte window, each byte's output (a text byte: itself; a reached
+//      tag: one space; a reached entity: its decoded bytes; a dropped '&' or a
+//      byte inside a reached tag / entity: nothing) is placed by a prefix sum.
+
+namespace cld {
+
+using wave::dpp_scan_incl;
+using wave::excl_scan;
+using wave::lanemask_lt;
+using wave::OpMax;
+using wave::rdl;
+using wave::rdlu;
+using wave::wshr1;
+using wave::wsum;
+using wave::wsync;
+
+constexpr int kHtmlRewriteMax = 8192;   // the page is staged in LDS (larger: k_general)
+constexpr int kHtmlCands = 512;        // '<' / '&' candidates per page (more: the page stays on k_general)
+constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
+#ifndef HTML_EXP
+#define HTML_EXP 0
+#endif
+
+// The character b0 b1 b2 (n bytes) lowers the same way in HTML mode as in plain text.
+__device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0, uint32_t b1, uint32_t b2, int n) {
+  if (n > 3) return false;
+  if (n >= 2 && (b1 & 0xC0) != 0x80) return false;
+  if (n == 3 && (b2 & 0xC0) != 0x80) return false;
+  return (gld(T.cpt + wave::cpt_index(b0, b1, b2, n)) & lng::kCptHtmlLower) == 0;
+}
+
+// ScanToPossibleLetter (getonescriptspan.cc:150-203, 503-541) with the tag
+// parser's transition function as two LDS tables built from tag_class /
+// tag_next (cld_pipeline.hip) at block start: one lookup per byte and no
+// branch per state, so lanes in different states do not serialise.
+constexpr int kTagStates = 40, kTagClasses = TC_PL + 1;
+struct TagTables {
+  uint8_t cls[256];
+  uint8_t next[kTagStates * kTagClasses];
+};
+// The scan by the whole wave (uniform arguments): the parser sits in one
+// state over long stretches (inside a tag, a quoted value, a comment, a
+// script or style block), so each step tests the next 64 bytes at once --
+// the transition each would make from the current state -- and jumps to the
+// first byte that changes the state.
+__device__ __forceinline__ int scan_tag_wave(const TagTables& tt, const uint8_t* text, int start, int len, int lane) {
+  int src = start, e = 0, st = 0;
+  const int lim = start + len;
+  bool brk = false;
+  while (src < lim) {
+    const int x = src + lane;
+    const int ns = tt.next[st * kTagClasses + tt.cls[x < lim ? text[x] : 0]];
+    const uint64_t chg = __ballot(x < lim && ns != st);
+    if (!chg) {                                  // 64 bytes (or the rest) in this state
+      e = st;
+      src = src + 64 < lim ? src + 64 : lim;
+      continue;
+    }
+    const int k = __builtin_ctzll(chg);
+    e = rdl(ns, k);
+    src += k + 1;
+    if (e <= 1) {
+      --src;
+      brk = true;
+      break;
+    }
+    st = e;
+  }
+  (void)brk;
+  if (src >= lim) return len;
+  if (e != 0 && e != 2) {
+    int off = src - start - 1;
+    while (0 < off && text[start + off] != '<') --off;
+    return off + 1;
+  }
+  return src - start;
+}
+
+struct HtmlSmem {
+  uint8_t text[kHtmlRewriteMax + 16];  // the page
+  uint16_t pos[kHtmlCands];            // candidate positions, in page order
+  uint16_t len[kHtmlCands];            // bytes the scan consumes there
+  uint32_t dec[kHtmlCands];            // an entity's decoded bytes
+  uint8_t meta[kHtmlCands];            // kind (0 tag, 1 entity, 2 dropped '&') | plen << 2 | bad << 5 | reached << 6
+};
+
+__global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables* __restrict__ Tp,
+                                                               const uint8_t* __restrict__ buf,
+                                                               const uint64_t* __restrict__ offs, int n,
+                                                               uint8_t* __restrict__ special,
+                                                               uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
+                                                               unsigned long long* __restrict__ prof) {
+  __shared__ HtmlSmem smem[kHtmlWPB];
+  __shared__ TagTables tt;
+  for (int t = threadIdx.x; t < 256 + kTagStates * kTagClasses; t += blockDim.x) {
+    if (t < 256) tt.cls[t] = (uint8_t)tag_class((uint8_t)t);
+    else tt.next[t - 256] = (uint8_t)tag_next((t - 256) / kTagClasses, (t - 256) % kTagClasses);
+  }
+  __syncthreads();
+  const DevTables& T = *Tp;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  HtmlSmem& S = smem[wv];
+  // ASCII characters whose HTML-mode lowering differs: a 128-bit mask
+  const uint64_t am0 = __ballot((gld(T.cpt + lane) & lng::kCptHtmlLower) != 0);
+  const uint64_t am1 = __ballot((gld(T.cpt + 64 + lane) & lng::kCptHtmlLower) != 0);
+  const int nw = gridDim.x * kHtmlWPB;
+  for (int i = blockIdx.x * kHtmlWPB + wv; i < n; i += nw) {
+    const uint8_t sp = special[i];
+    if (!(sp & kSpecialHtml)) continue;
+    const uint64_t a = offs[i];
+    const int64_t len64 = (int64_t)(offs[i + 1] - a);
+    if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: k_general
+    const int L = (int)len64;
+    // the page into LDS (16-byte pieces from aligned dwords), NUL padded
+    {
+      const uint8_t* g = buf + a;
+      for (int p = lane * 4; p < L + 16; p += 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v |= (uint32_t)(p + k < L ? g[p + k] : 0) << (8 * k);
+        *reinterpret_cast<uint32_t*>(&S.text[p]) = v;
+      }
+    }
+    wsync();
+    const DocView dv{S.text, L};
+    // 1a. candidates, in page order
+    int K = 0;
+    for (int w0 = 0; w0 < L; w0 += 64) {
+      const int p = w0 + lane;
+      const uint32_t c = p < L ? S.text[p] : 0u;
+      const bool cand = c == '<' || c == '&';
+      const uint64_t m = __ballot(cand);
+      const int k = K + __popcll(m & lanemask_lt(lane));
+      if (cand && k < kHtmlCands) S.pos[k] = (uint16_t)p;
+      K += __popcll(m);
+    }
+    if (K > kHtmlCands) continue;                                // stays HTML: k_general
+    wsync();
+    // 1b. each candidate as if the scan reached it
+    for (int j = lane; j < K; j += 64) {
+      const int p = S.pos[j];
+      int ln = 1, kind = 0, plen = 0;
+      bool bad = false;
+      uint32_t dec = 0;
+      if (S.text[p] == '<') {
+        ln = 0;                                                  // (a reached tag is scanned in step 2)
+      } else {
+        uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int tlen = 0;
+        entity_to_buffer(T, dv, p, L - p, tmp, &tlen, &plen);
+        if (plen > 0) {
+          kind = 1;
+          ln = tlen;
+          dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
+          bad = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
+                (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
+        } else {
+          kind = 2;                                              // undecodable: the '&' is dropped
+          plen = 0;
+        }
+      }
+      S.len[j] = (uint16_t)ln;
+      S.dec[j] = dec;
+      S.meta[j] = (uint8_t)(kind | (plen << 2) | (bad ? 0x20 : 0));
+    }
+    wsync();
+    // 2. which candidates the scan reaches: past the end of the last reached one
+    const long long t2 = prof ? (long long)clock64() : 0;
+    int cur = 0;
+    for (int j0 = 0; j0 < K; j0 += 64) {
+      const int j = j0 + lane;
+      const int p = j < K ? (int)S.pos[j] : 0x7FFFFFFF, ln = j < K ? (int)S.len[j] : 0;
+      const int m = K - j0 < 64 ? K - j0 : 64;
+      const uint64_t tag_m = __ballot(j < K && (S.meta[j] & 3) == 0);
+      uint64_t reach = 0;
+      for (int t = 0; t < m; ++t) {
+        const int pt = rdl(p, t);
+        if (pt >= cur) {
+          reach |= 1ull << t;
+          int lt = rdl(ln, t);
+          if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
+#if HTML_EXP == 1
+            lt = 1;
+#elif HTML_EXP == 2
+            lt = scan_tag_wave(tt, S.text, pt, L - pt, lane) > 0 ? 1 : 2;
+#else
+            lt = scan_tag_wave(tt, S.text, pt, L - pt, lane);
+#endif
+            if (lane == t) S.len[j] = (uint16_t)lt;
+          }
+          cur = pt + lt;
+        }
+      }
+      if (j < K) S.meta[j] = (uint8_t)(S.meta[j] | (((reach >> lane) & 1) ? 0x40 : 0));
+    }
+    wsync();
+    if (prof && lane == 0) atomicAdd(prof, (unsigned long long)((long long)clock64() - t2));
+    // 3. the output, window by window
+    uint8_t* o = hbuf + a;
+    uint8_t* f = hflag + a;
+    int q = 0, cb = 0, bad = 0, conts = 0, need = 0;
+    uint32_t cover = 0;                                          // end of the last reached candidate so far
+    uint32_t drop_prev = 0;                                      // the byte before this window was a dropped '&'
+    for (int w0 = 0; w0 < L; w0 += 64) {
+      const int p = w0 + lane;
+      const bool in = p < L;
+      const uint32_t c = in ? S.text[p] : 0u;
+      const bool cand = in && (c == '<' || c == '&');
+      const uint64_t cm = __ballot(cand);
+      const int j = cand ? cb + __popcll(cm & lanemask_lt(lane)) : 0;
+      cb += __popcll(cm);
+      const uint32_t meta = cand ? S.meta[j] : 0u;
+      const bool reached = (meta & 0x40) != 0;
+      const uint32_t end = reached ? (uint32_t)(p + S.len[j]) : 0u;
+      // covered: inside a reached candidate that starts before p (the running
+      // maximum of reached ends, carried across windows)
+      const uint32_t mx = dpp_scan_incl(end, 0u, OpMax());
+      const uint32_t before = wshr1(mx, 0u);
+      const uint32_t cov_end = before > cover ? before : cover;
+      const bool covered = in && !reached && (uint32_t)p < cov_end;
+      const int kind = meta & 3, plen = (meta >> 2) & 7;
+      const bool text = in && !covered && !reached;
+      int emit = 0;
+      if (reached) emit = kind == 0 ? 1 : kind == 1 ? plen : 0;
+      else if (text) emit = 1;
+      // the first byte after a dropped '&' carries the lookahead mark
+      const bool dropped = reached && kind == 2;
+      const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
+      const int at = q + excl_scan(emit, lane);
+      if (text) {
+        o[at] = (uint8_t)c;
+        f[at] = (uint8_t)dprev;
+        // plain characters: well formed, and the same lowering in HTML mode
+        if (c < 0x80) {
+          bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
+        } else if ((c & 0xC0) == 0x80) {
+          ++conts;
+        } else {
+          const int m = utf8_len((uint8_t)c);
+          const uint32_t b1 = S.text[p + 1], b2 = S.text[p + 2];      // (NUL padded)
+          bad |= (p + m > L || !html_lower_same(T, c, b1, b2, m)) ? 1 : 0;
+          need += m - 1;
+        }
+      } else if (reached && kind == 0) {
+        o[at] = ' ';
+        f[at] = (uint8_t)dprev;
+      } else if (reached && kind == 1) {
+        const uint32_t d = S.dec[j];
+        for (int k = 0; k < plen; ++k) {
+          o[at + k] = (uint8_t)(d >> (8 * k));
+          f[at + k] = k == 0 ? 1 : 0;
+        }
+        bad |= (meta & 0x20) ? 1 : 0;
+      }
+      q = rdl(at + emit, 63);
+      const uint32_t wmx = rdlu(mx, 63);
+      cover = wmx > cover ? wmx : cover;
+      drop_prev = rdlu(dropped ? 1u : 0u, 63);
+    }
+    // the page keeps its length: spaces after the text
+    for (int p = q + lane; p < L; p += 64) {
+      o[p] = ' ';
+      f[p] = 0;
+    }
+    bad |= wsum(conts - need) != 0 ? 1 : 0;                      // every continuation byte claimed
+    if (__ballot(bad != 0) == 0 && lane == 0) special[i] = (uint8_t)((sp & ~kSpecialHtml) | kSpecialRewritten);
+    wsync();
+  }
+}
+
+}  // namespace cld

@@ -28,7 +28,9 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
        kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
        kCtrSpecial = 16, kCtrSlots = 32 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
-enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2 };
+// kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
+// (hbuf / hflag); k_general, should it get it back, scores the original page.
+enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2, kSpecialRewritten = 4 };
 // k_long: waves per workgroup
 constexpr int kLongWPB = 4;
 
@@ -54,7 +56,15 @@ size_t cld_short_work_bytes();
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
-                           int special_ctr, uint32_t cflags, const uint32_t* priors, hipStream_t s);
+                           int special_ctr, uint32_t cflags, const uint32_t* priors, const uint8_t* hbuf,
+                           const uint8_t* hflag, hipStream_t s);
+// HTML documents of the batch (special & kSpecialHtml) rewritten into plain
+// text (cld_html.hip): hbuf / hflag are indexed like buf (offs); special is
+// updated in place (kSpecialHtml -> kSpecialRewritten for each rewritten page);
+// prof (nullable, CLD_PROFILE_STAGES=1): cycles of step 2 summed into prof[0].
+hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
+                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, unsigned long long* prof,
+                                   hipStream_t s);
 size_t cld_wave_smem_bytes();
 hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                             cld_result* out, uint32_t* requeue_list, uint32_t* counters,
@@ -89,6 +99,6 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, hipStream_t s);
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, hipStream_t s);
 }
 #endif

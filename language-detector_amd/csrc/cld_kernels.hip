@@ -15,6 +15,7 @@
 #include "cld_pipeline.hip"
 #include "cld_wave.hip"
 #include "cld_long.hip"
+#include "cld_html.hip"
 
 #ifndef GEN_LANES_PER_WAVE
 // k_general / k_general_vec: documents per wavefront.  One per wave: the
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp
     // cld_detect_batch_ex: HTML documents (special bit 0) and per-document
     // ApplyHints priors (16 langprobs each, bit 1)
     const uint8_t sp = special ? special[i] : 0;
-    int passes = detect_doc(T, d, w, &out[i], st, !(sp & kSpecialHtml),
+    int passes = detect_doc(T, d, w, &out[i], st, !(sp & (kSpecialHtml | kSpecialRewritten)),
                             (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, cflags);
     if (passes >= 1 && passes <= 3) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
     else atomicAdd(&counters[kCtrError], 1u);
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
     Status st{false};
     DocView d{buf + a, (int)(b - a)};
     const uint8_t sp = special ? special[i] : 0;
-    const int passes = detect_doc(T, d, w.g, &out[i], st, !(sp & kSpecialHtml),
+    const int passes = detect_doc(T, d, w.g, &out[i], st, !(sp & (kSpecialHtml | kSpecialRewritten)),
                                   (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, &vo, cflags);
     const bool bad = passes < 1 || passes > 3 || st.requeue || vo.over || vo.orig.over || vo.low.over;
     n_chunks[i] = bad ? -1 : vo.n;
@@ -185,7 +186,8 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
                                                    unsigned long long* __restrict__ prof,
                                                    const uint8_t* __restrict__ special,
                                                    uint32_t* __restrict__ special_list, int special_ctr,
-                                                   uint32_t cflags, const uint32_t* __restrict__ priors) {
+                                                   uint32_t cflags, const uint32_t* __restrict__ priors,
+                                                   const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag) {
   __shared__ wave::Smem<CAP> smem[WPB];
   // wave index through readfirstlane: the document pointer, its length, the
   // result pointer and the LDS base are then scalars, not VGPRs live across
@@ -208,8 +210,10 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   if (len > CAP) return;
   // stage cycles (CLD_PROFILE_STAGES=1) are sampled on one document in 64, so
   // the accounting atomics do not themselves become the bottleneck
-  const bool rq = !wave::detect<CAP>(T, buf + a, (int)len, smem[wv], lane, &out[i], (i & 63) == 0 ? prof : nullptr,
-                                     cflags, pri);
+  // a rewritten HTML page (cld_html.hip) is read from hbuf, with its lookahead marks
+  const bool rw = (sp & kSpecialRewritten) != 0;
+  const bool rq = !wave::detect<CAP>(T, (rw ? hbuf : buf) + a, (int)len, smem[wv], lane, &out[i],
+                                     (i & 63) == 0 ? prof : nullptr, cflags, pri, rw ? hflag + a : nullptr);
   if (rq && lane == 0) {                       // rare (state-machine or capacity cases)
     uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
     requeue_list[k] = (uint32_t)i;
@@ -272,7 +276,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   uint32_t* dbg, uint32_t dbg_doc,
                                                   unsigned long long* prof, uint32_t cflags,
                                                   const uint8_t* __restrict__ special,
-                                                  const uint32_t* __restrict__ priors) {
+                                                  const uint32_t* __restrict__ priors,
+                                                  const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -302,9 +307,11 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
       smem[wv].prof = DIAG ? prof : nullptr;
     }
     wave::wsync();
+    const uint8_t spi = special ? special[i] : (uint8_t)0;
+    const bool rw = (spi & kSpecialRewritten) != 0;   // a rewritten HTML page (cld_html.hip)
     if (exact && len <= (uint64_t)lng::kDocCap)
-      passes = lng::detect<DIAG>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
-                                 (special && (special[i] & kSpecialPriors)) ? priors + 16ull * i : nullptr);
+      passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
+                                 (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr);
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (lane == 0) {
@@ -463,17 +470,17 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, hipStream_t s) {
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag);
   return hipGetLastError();
 }
 
@@ -507,14 +514,25 @@ size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
-                           int special_ctr, uint32_t cflags, const uint32_t* priors, hipStream_t s) {
+                           int special_ctr, uint32_t cflags, const uint32_t* priors, const uint8_t* hbuf,
+                           const uint8_t* hflag, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(cld::k_route, dim3((n + 255) / 256), dim3(256), 0, s, offs, n, special, kWaveCap, counters,
                      requeue_list, special_list, special_ctr);
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
-                     requeue_list, counters, prof, special, special_list, special_ctr, cflags, priors);
+                     requeue_list, counters, prof, special, special_list, special_ctr, cflags, priors, hbuf, hflag);
+  return hipGetLastError();
+}
+
+hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
+                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, unsigned long long* prof,
+                                   hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = std::min((n + cld::kHtmlWPB - 1) / cld::kHtmlWPB, 2048);   // persistent: pages by stride
+  hipLaunchKernelGGL(cld::k_html_rewrite, dim3(blocks), dim3(64 * cld::kHtmlWPB), 0, s, d_T, buf, offs, n, special,
+                     hbuf, hflag, prof);
   return hipGetLastError();
 }
 

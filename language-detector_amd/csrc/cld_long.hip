@@ -362,8 +362,11 @@ __device__ __forceinline__ int scan_char(const DevTables& T, const DocView& d, i
 // per GPU by k_build_cpt from the very device functions below; 4-byte and
 // malformed sequences still run the machines.
 //   bits 0-7 script, 8-9 scan class (0 continue, 1 stop, 3 non-local),
-//   10 lowerable here, 11-14 lowered length, 32-63 lowered bytes
+//   10 lowerable here, 11-14 lowered length, 16 lowered differently in HTML
+//   mode (the HTML half of a remap pair, utf8statetable.cc:755-762), 32-63
+//   lowered bytes
 constexpr int kCptSize = 128 + 2048 + 65536;
+constexpr uint64_t kCptHtmlLower = 1ull << 16;
 using wave::cpt_index;
 __device__ uint64_t cpt_eval(const DevTables& T, const uint8_t* b, int n) {
   const DocView dv{b, n};
@@ -372,8 +375,13 @@ __device__ uint64_t cpt_eval(const DevTables& T, const uint8_t* b, int n) {
   uint64_t o = 0;
   int olen = 0;
   const bool lowok = lower_char(T, b, n, o, olen) && olen <= 4;
+  uint8_t lp[16], lh[16];
+  const int fp = lower_replace_sm(T.lower, b, n, lp, 16, true), fh = lower_replace_sm(T.lower, b, n, lh, 16, false);
+  bool hdiff = fp != fh;
+  for (int k = 0; k < fp && k < 16; ++k) hdiff |= lp[k] != lh[k];
   return (uint64_t)(sn & 0xFF) | ((uint64_t)(st < 0 ? 3 : st) << 8) | ((uint64_t)lowok << 10) |
-         ((uint64_t)(lowok ? olen : 0) << 11) | ((lowok ? (o & 0xFFFFFFFFull) : 0ull) << 32);
+         ((uint64_t)(lowok ? olen : 0) << 11) | (hdiff ? kCptHtmlLower : 0ull) |
+         ((lowok ? (o & 0xFFFFFFFFull) : 0ull) << 32);
 }
 
 // The rare characters the property table does not cover (4-byte or cut by
@@ -659,8 +667,9 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         } else {
           // the next character's script, only for a letter of another script
           // (rare inside a span): gathered here rather than for every byte
-          const int sc2 = cur_i2 >= 0 ? (int)(gld(reinterpret_cast<const uint32_t*>(T.cpt) + 2 * cur_i2) & 0xFF)
-                                      : script_num(T, dv, x + n);
+          int sc2 = cur_i2 >= 0 ? (int)(gld(reinterpret_cast<const uint32_t*>(T.cpt) + 2 * cur_i2) & 0xFF)
+                                : script_num(T, dv, x + n);
+          if (dv.hf && x + n < L && gld(dv.hf + x + n)) sc2 = 0;   // onto a rewritten HTML entity: the raw '&'
           brk = sc2 != common && sc2 != ss;
         }
       }
@@ -2724,7 +2733,7 @@ enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapa
 template <bool D>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
-                      const uint32_t* __restrict__ pri) {
+                      const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf) {
   const int unk = (int)T.unknown_lang;
   // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
   if (lane == 0) s.has_pri = pri != nullptr;
@@ -2744,7 +2753,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
     return 1;
   }
   if (L > kDocCap - 64) return -kWhyLength;
-  const DocView dv{g, L};
+  const DocView dv{g, L, hf};
   if constexpr (D) trace(tr, lane, doc, 1, L);
   long long t = (D && s.prof) ? (long long)clock64() : 0;
 

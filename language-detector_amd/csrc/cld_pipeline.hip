@@ -68,6 +68,10 @@ __device__ __forceinline__ int adv_space_vowel(uint8_t c) {   // cldutil_shared.
 struct DocView {
   const uint8_t* p;
   int len;
+  // (rewritten HTML documents only, cld_html.hip) one byte per position, 1
+  // where the original had an entity's '&': a script lookahead landing there
+  // sees that '&' (script 0), not the decoded character
+  const uint8_t* hf = nullptr;
   __device__ __forceinline__ uint8_t at(int i) const { return (unsigned)i < (unsigned)len ? p[i] : 0; }
 };
 

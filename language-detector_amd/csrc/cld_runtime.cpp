@@ -358,6 +358,8 @@ struct Device {
   uint64_t* d_offs = nullptr; size_t offs_cap = 0;
   cld_result* d_out = nullptr; size_t out_cap = 0;
   uint8_t* d_sbuf = nullptr; size_t sbuf_cap = 0;        // prepared text (CLD_FLAG_STRIP_EXTRAS / CSTRING)
+  uint8_t* d_hbuf = nullptr; size_t hbuf_cap = 0;        // HTML pages rewritten into plain text (cld_html.hip)
+  uint8_t* d_hflag = nullptr; size_t hflag_cap = 0;      //   and their entity lookahead marks
   uint64_t* d_soffs = nullptr; size_t soffs_cap = 0;
   uint8_t* d_sscr = nullptr; size_t sscr_cap = 0;
   hipEvent_t ev[4]{};
@@ -596,9 +598,20 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 // and ApplyHints langprobs (16 per document); HTML documents skip the wave and
 // long kernels and run whole in k_general, hinted plain ones take the wave /
 // long kernels with their priors.  cflags: CLD2's public flags (kCldFlags).
+// html_bytes > 0 (the batch holds HTML pages, special & kSpecialHtml; special
+// is then the runtime's own device copy): the pages are first rewritten into
+// plain text (cld_html.hip, k_html_rewrite) in d_hbuf, indexed like buf, whose
+// document bytes span [html_base, html_base + html_bytes) of the offsets.
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
-            const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0) {
+            const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0,
+            uint64_t html_base = 0, uint64_t html_bytes = 0) {
   cflags &= kCldFlags;
+  const uint8_t *hbuf = nullptr, *hflag = nullptr;
+  if (special && html_bytes) {
+    if (grow(&d->d_hbuf, &d->hbuf_cap, html_bytes) || grow(&d->d_hflag, &d->hflag_cap, html_bytes)) return CLD_ENOMEM;
+    hbuf = d->d_hbuf - html_base;
+    hflag = d->d_hflag - html_base;
+  }
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (d->n_slots > 0 && d->long_order) {
@@ -615,6 +628,9 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
   if (d->d_dbg) HIP_OK(hipMemsetAsync(d->d_dbg, 0, 4, s));
   HIP_OK(hipEventRecord(ev[0], s));
+  if (hbuf)
+    HIP_OK(cld_launch_html_rewrite(d->d_T, buf, offs, (int)n, const_cast<uint8_t*>(special), const_cast<uint8_t*>(hbuf),
+                                   const_cast<uint8_t*>(hflag), d->d_prof ? d->d_prof + 7 : nullptr, s));
   // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
@@ -623,7 +639,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
                             cflags, s));
   else
     HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
-                           sp_ctr, cflags, priors, s));
+                           sp_ctr, cflags, priors, hbuf, hflag, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
@@ -633,7 +649,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
-                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, s));
+                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, s));
@@ -812,7 +828,7 @@ struct HostReg {
 };
 
 int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
-                   const uint8_t* special = nullptr, const uint32_t* priors = nullptr) {
+                   const uint8_t* special = nullptr, const uint32_t* priors = nullptr, bool html = false) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
@@ -897,7 +913,7 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
       rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream, nullptr, nullptr, flags);
     } else {
       rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream, special ? h.d_sp : nullptr,
-                   (special && priors) ? h.d_pri : nullptr, flags);
+                   (special && priors) ? h.d_pri : nullptr, flags, base, (special && html) ? bytes : 0);
     }
     if (rc) break;
     HIP_OK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
@@ -1269,6 +1285,7 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree((void*)d->T.compat.adds); (void)hipFree(d->d_T); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
+    (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);
@@ -1406,14 +1423,14 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
   const size_t ndev = g_devs.size();
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
-  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, cf, sp, pr);
+  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, cf, sp, pr, html);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
     th.emplace_back([&, k] {
       rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], cf,
-                              sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr);
+                              sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr, html);
     });
   }
   for (auto& t : th) t.join();

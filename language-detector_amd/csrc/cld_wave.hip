@@ -159,7 +159,7 @@ struct Smem {
   uint8_t doc[C::DOC];
   uint8_t sn[C::DOC];                 // script number at each byte position (GetUTF8LetterScriptNum)
   uint64_t lsm[C::NM];                // letter stops: char start, scanner stops there, script != 0
-  uint64_t brk[C::NM];                // letters that end a run for the current span script
+  uint64_t ent[C::NM];                // rewritten HTML (cld_html.hip): lookaheads here see script 0
   union alignas(16) {                 // one span's life: raw text -> base hits -> chunk ids
     uint8_t sbuf[C::SB];              //   span text (raw); dead once lowered
     struct {                          //   quad chain (quad_hits, before its base hits are written)
@@ -228,7 +228,8 @@ __device__ __forceinline__ int cpt_index(uint32_t b0, uint32_t b1, uint32_t b2, 
 // and a scan started at any character either stops on it or continues to the
 // scan result of the next character.
 template <int CAP>
-__device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane) {
+__device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
+                              const uint8_t* __restrict__ hf) {
   using C = Cfg<CAP>;
   static_assert(CAP == 256 && C::DOC == 288, "one aligned dword per lane covers the document");
   {
@@ -247,6 +248,15 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
     const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
     reinterpret_cast<uint32_t*>(s.doc)[lane] = v & keep;
     if (lane < (C::DOC - 256) / 4) reinterpret_cast<uint32_t*>(s.doc)[64 + lane] = 0u;
+    // a rewritten HTML page's lookahead marks (one byte per position), else none
+    if (hf) {
+      for (int w = 0; w < C::NM; ++w) {
+        const uint64_t m = __ballot(w * 64 + lane < L && gld(hf + w * 64 + lane) != 0);
+        if (lane == 0) s.ent[w] = m;
+      }
+    } else if (lane < C::NM) {
+      s.ent[lane] = 0ull;
+    }
   }
   wsync();
   DocView dv{s.doc, L};
@@ -367,7 +377,9 @@ __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int
         if (sc == common) {
           brk = true;
         } else {
-          const int sc2 = s.sn[x + utf8_len((uint8_t)c)];
+          // (a lookahead onto a rewritten HTML entity sees the raw '&': script 0)
+          const int xn = x + utf8_len((uint8_t)c);
+          const int sc2 = (xn < 64 * C::NM && ((s.ent[xn >> 6] >> (xn & 63)) & 1)) ? 0 : s.sn[xn];
           brk = sc2 != common && sc2 != spanscript;
         }
       }
@@ -1388,7 +1400,7 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
 template <int CAP>
 __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L, Smem<CAP>& s, int lane,
                        cld_result* __restrict__ out, unsigned long long* __restrict__ prof, uint32_t cflags,
-                       const uint32_t* __restrict__ pri) {
+                       const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf) {
   // optional per-stage cycle accounting (CLD_PROFILE_STAGES=1): 0 load, 1 span,
   // 2 lower, 3 quad/uni, 4 octa/bi, 5 score, 6 document level
   long long t_stage = prof ? (long long)clock64() : 0;
@@ -1410,7 +1422,7 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     }
     return true;
   }
-  if (!load_document<CAP>(T, g, L, s, lane)) return false;
+  if (!load_document<CAP>(T, g, L, s, lane, hf)) return false;
   mark(0);
     WAVE_STOP_AT(0);
   if (lane == 0) s.dt.init();

@@ -4,9 +4,11 @@ The per-document priors come from the product's host hint code
 (cld_hint_priors, pinned to the reference's hint code by
 tests/test_html_hints.py::test_hint_priors_match_reference); the oracle then
 scores each document with the same priors and is_plain_text flag.  HTML
-documents run in k_general (the exact sequential kernel); hinted plain
-documents stay on the wave / long kernels, which add the prior boosts and
-apply the whacks in their chunk totes.
+pages are rewritten into plain text on the GPU (cld_html.hip: tags -> one
+space, entities decoded, lookahead marks) and scored by the wave / long
+kernels; pages the rewrite cannot take stay on k_general, the exact
+sequential kernel.  Hinted plain documents stay on the wave / long kernels,
+which add the prior boosts and apply the whacks in their chunk totes.
 """
 import numpy as np
 import pytest
@@ -50,7 +52,7 @@ def test_html_documents(gpu, oracle):
     n = len(offs) - 1
     got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
     st = gpu.last_stats()
-    assert st.general_docs == n                      # every HTML document runs the exact kernel
+    assert st.general_docs < n // 10                 # the rewritten pages run on the parallel kernels
     pr = priors_for(gpu, buf, offs, True, None)
     assert (pr != 0).any(axis=1).sum() > n // 2      # lang= attributes became priors
     ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=16)
@@ -73,6 +75,39 @@ def test_html_edge_documents(gpu, oracle):
     pr = priors_for(gpu, buf, offs, True, None)
     ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr)
     assert_same(got, ref, "html edge")
+
+
+def test_html_rewrite_lookahead_edges(gpu, oracle):
+    """The rewrite's exactness edges: a script lookahead from a letter of
+    another script onto an entity (decoded to a letter of either script, or
+    undecodable and dropped), entities next to tags, runs broken by decoded
+    non-letters, characters the HTML lowercaser treats differently, and pages
+    longer than the rewrite takes (kHtmlRewriteMax)."""
+    parts = ["abc\u03b1&eacute;def", "abc\u03b1&#945;def", "abc\u03b1&#1044;def", "abc\u03b1&bogus;def",
+             "abc\u03b1&amp;def", "abc\u03b1&xyz def", "\u0434\u043e\u043c&#x434;\u043c", "\u03b1&&eacute;b",
+             "x&lt;b&gt;y", "caf&eacute;<b>cr&egrave;me</b>", "na&iuml;ve&nbsp;text", "&#12354;&#12356;\u3042",
+             "ABC&#65;&#x42;C", "\u00c9t\u00e9 &Eacute;t&eacute;", "word&#0;word", "&#55296;x",
+             "<a <b>text</b> more", "<!-- c -->d&#101;f"]
+    rare = ["\u0130stanbul &#304;zmir", "a&#x10000;b", "\U0001f600 ok"]   # 4-byte / HTML-lowering candidates
+    rng = np.random.default_rng(7)
+    docs = []
+    for k in range(400):
+        words = [parts[int(rng.integers(0, len(parts)))] for _ in range(int(rng.integers(1, 40)))]
+        if k % 8 == 0:
+            words.append(rare[(k // 8) % len(rare)])
+        filler = ["le", "chat", "noir", "\u0434\u043e\u043c", "\u03b3\u03b1\u03c4\u03b1", "<i>", "</i>", "&amp;"]
+        words += [filler[int(rng.integers(0, len(filler)))] for _ in range(int(rng.integers(0, 60)))]
+        rng.shuffle(words)
+        docs.append(" ".join(words).encode())
+    docs.append(("<p>" + "caf&eacute; " * 4000 + "</p>").encode())        # > kHtmlRewriteMax: stays on k_general
+    buf, offs = gpu.pack(docs)
+    n = len(docs)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+    st = gpu.last_stats()
+    assert 1 <= st.general_docs < n // 4
+    pr = priors_for(gpu, buf, offs, True, None)
+    ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=8)
+    assert_same(got, ref, "html rewrite edges")
 
 
 @pytest.mark.parametrize("cfg,n,seed", [("c2", 20000, 31), ("c3", 300, 32), ("c4", 11000, 33), ("c5", 20000, 34)])
