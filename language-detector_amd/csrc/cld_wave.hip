@@ -62,6 +62,15 @@ __device__ __forceinline__ void wsync() {
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+// The lane id recomputed where a stage starts (v_mbcnt, as volatile asm): the
+// compiler would otherwise hoist the per-lane values derived from it out of
+// the document's span loop and spill them to scratch (8 waves/SIMD leave 64
+// VGPRs), a scratch write per lane and document.
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 
 // Register arrays indexed by a wave-uniform register number r (entry i of a
 // 64*N list lives in lane i&63 of register i>>6).
@@ -291,7 +300,6 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
     uint64_t ev[C::NM];
 #pragma unroll
     for (int w = 0; w < C::NM; ++w) ev[w] = idx[w] >= 0 ? gld(T.cpt + idx[w]) : 0ull;
-    uint64_t lm[C::NM];
 #pragma unroll
     for (int w = 0; w < C::NM; ++w) {
       // script number at every byte (0 off the lead bytes: only lead bytes are read)
@@ -300,9 +308,9 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
       const int st = (int)((e >> 8) & 3);
       slow |= st == 3 ? 1 : 0;
       s.sn[p] = (uint8_t)e;
-      lm[w] = __ballot(st == 1 && (e & 0xFF) != 0);
+      const uint64_t m = __ballot(st == 1 && (e & 0xFF) != 0);
+      if (lane == 0) s.lsm[w] = m;                      // (a lane-indexed register array would live in scratch)
     }
-    if (lane < C::NM) s.lsm[lane] = pick(lm, lane);
     slow |= wsum(conts - need) != 0 ? 1 : 0;               // every continuation byte is claimed
     if (__ballot(slow != 0) == 0) {
       if (lane < 4) s.sn[L + lane] = (uint8_t)script_num(T, dv, L + lane);
@@ -350,6 +358,7 @@ __device__ bool load_document(const DevTables& T, const uint8_t* __restrict__ g,
 // Returns text_bytes (0 = no further span); *next advances like next_byte_.
 template <int CAP>
 __device__ int next_span(const DevTables& T, Smem<CAP>& s, int L, int& next, int& ulscript, int lane) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const int common = (int)T.common, inherited = (int)T.inherited;
   const int q = find_first<C::NM>(s.lsm, next, L);
@@ -516,6 +525,7 @@ __device__ __forceinline__ bool lower_char(const DevTables& T, const uint8_t* sr
 // LowerScriptSpan (getonescriptspan.cc:1033-1054): returns text_bytes, or -1.
 template <int CAP>
 __device__ int lower_span(const DevTables& T, Smem<CAP>& s, int text_bytes, int lane) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const int ilen = text_bytes + 3;
   int obase = 0;
@@ -582,6 +592,7 @@ __device__ __forceinline__ uint32_t quad_hash_lds(const uint8_t* text, int p, in
 // Returns the end offset (reference `next`), or -1 on overflow.
 template <int CAP>
 __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, int lane) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const uint8_t* text = s.lbuf;
   int start = 1;
@@ -653,37 +664,29 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   for (int r = 0; r < C::NR; ++r) cp[r] = s.qchn[r * 64 + lane];
   wsync();                               // (the base hits below overwrite the chain lists)
   const int end = n == 0 ? start : limit;
-  // hashes and probes per chain entry
-  uint32_t h[C::NR], pr[C::NR];
-  bool hit[C::NR];
-#pragma unroll
-  for (int r = 0; r < C::NR; ++r) { h[r] = 0; pr[r] = 0; hit[r] = false; }
+  // per register of chain entries, in order: hashes and probes, the repeat
+  // filter (drop a hit equal to either of the last two kept hits), and the
+  // ordered compaction of the kept hits -- one register's values live at a
+  // time (the filter's state A, B and the compaction base carry over)
+  uint32_t A = 0, B = 0;                  // last two kept hashes (the reference's pq0/pq1 as a set)
+  int base = 0;
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) {
     if (r * 64 >= n) break;                // (uniform: registers past the chain hold nothing)
     const int i = r * 64 + lane;
+    uint32_t hv = 0, pr = 0;
+    bool hit = false;
     if (i < n) {
       const int p = cp[r];
-      uint32_t hv = quad_hash_lds(text, p, (int)(nfo[p] & 31));
+      hv = quad_hash_lds(text, p, (int)(nfo[p] & 31));
       uint32_t ind = 0;
-      const uint32_t probs = quad_probe(T.quad, T.quad2, hv, ind);
-      h[r] = hv;
-      pr[r] = ind;
-      hit[r] = probs != 0;
+      hit = quad_probe(T.quad, T.quad2, hv, ind) != 0;
+      pr = ind;
     }
-  }
-  WAVE_STOP_AT(33);
-  // repeat filter: drop a hit equal to either of the last two kept hits.
-  // Assume every hit is kept: then a hit's two predecessors are the previous
-  // hit lanes; from the first hit that equals one of them, resolve in order.
-  uint64_t keep[C::NR];
-  uint32_t A = 0, B = 0;                  // last two kept hashes (the reference's pq0/pq1 as a set)
-#pragma unroll
-  for (int r = 0; r < C::NR; ++r) {
-    keep[r] = 0;
-    if (r * 64 >= n) continue;
-    const uint64_t hm = __ballot(hit[r]);
-    const uint32_t hv = h[r];
+    WAVE_STOP_AT(33);
+    // Assume every hit is kept: then a hit's two predecessors are the previous
+    // hit lanes; from the first hit that equals one of them, resolve in order.
+    const uint64_t hm = __ballot(hit);
     const uint64_t hb = hm & lanemask_lt(lane);
     const int q1 = hb ? 63 - __builtin_clzll(hb) : -1;
     const uint64_t hb2 = q1 > 0 ? (hb & lanemask_lt(q1)) : 0ull;
@@ -692,7 +695,7 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
     const uint32_t h2 = (uint32_t)__shfl((int)hv, q2 < 0 ? lane : q2, 64);
     const uint32_t a = q1 < 0 ? A : h1;
     const uint32_t b = q1 < 0 ? B : (q2 < 0 ? A : h2);
-    const uint64_t cm = __ballot(hit[r] && (hv == a || hv == b));
+    const uint64_t cm = __ballot(hit && (hv == a || hv == b));
     uint64_t k = hm;
     if (cm) {
       const int f = __builtin_ctzll(cm);
@@ -714,17 +717,12 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
       B = r2 ? rdlu(hv, 63 - __builtin_clzll(r2)) : A;
       A = rdlu(hv, t1);
     }
-    keep[r] = k;
-  }
-  int base = 0;
-#pragma unroll
-  for (int r = 0; r < C::NR; ++r) {
-    if ((keep[r] >> lane) & 1) {
-      const int k = base + __popcll(keep[r] & lanemask_lt(lane));
-      s.b_off[k] = (uint16_t)cp[r];
-      s.b_ind[k] = pr[r];
+    if ((k >> lane) & 1) {
+      const int kk = base + __popcll(k & lanemask_lt(lane));
+      s.b_off[kk] = (uint16_t)cp[r];
+      s.b_ind[kk] = pr;
     }
-    base += __popcll(keep[r]);
+    base += __popcll(k);
   }
   nb = base;
   wsync();
@@ -734,6 +732,7 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
 // GetOctaHits (cldutil.cc:416-533): one lane per space-terminated word.
 template <int CAP>
 __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int& nd, int& nx, int lane) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const uint8_t* text = s.lbuf;
   int start = 1;
@@ -852,6 +851,7 @@ __device__ bool octa_hits(const DevTables& T, Smem<CAP>& s, int limit_next, int&
 // GetUniHits + GetBiHits (cldutil.cc:201-310), one lane per character.
 template <int CAP>
 __device__ int cjk_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, int& nd, int& nx, int lane) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const uint8_t* text = s.lbuf;
   int start = 1;
@@ -946,6 +946,7 @@ __device__ __forceinline__ void dt_add_wave(DocTote& dt, int k, int bytes, int s
 template <int CAP>
 __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int dummy_off, int& ring_sel, int lane, const uint32_t* __restrict__ pri) {
+  lane = lane_here();
   using C = Cfg<CAP>;
   const DevTbl& bo = cjk ? T.compat : T.quad;
   const DevTbl& bo2 = cjk ? T.compat : T.quad2;
