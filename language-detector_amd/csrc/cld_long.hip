@@ -537,6 +537,7 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // starts.  False if the document does not tile into characters with local
 // scanner behaviour (then k_general redoes it).
 __device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
+  lane = wave::lane_here();
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
   cut = false;
@@ -600,6 +601,7 @@ __device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, ui
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane) {
+  lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
   const int remaining = L - next;
@@ -957,6 +959,7 @@ __device__ __forceinline__ bool predict_window_lds(uint16_t* tbl, uint64_t* ovf,
 // the current one is processed.  hcarry carries from span to span.
 __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_t* text, int len, uint32_t& hcarry, bool careful,
                             bool& ok, int lane) {
+  lane = wave::lane_here();
   const int nw = (len + 63) >> 6;
   int D = 0, WD = 0;                     // dst, word_dst (as offsets)
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
@@ -1032,6 +1035,7 @@ __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_
 // of more than 2048 bytes: >= 25% spaces or >= 67% predicted bytes in the first
 // 256 bytes (fresh table, hash 0).
 __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, bool careful, int lane) {
+  lane = wave::lane_here();
   int sp = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) sp += text[lane * 4 + k] == ' ';
@@ -1059,6 +1063,7 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, bo
 // included, are dropped if more than half of the segment was predicted.
 __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
                          bool careful, bool& ok, int lane) {
+  lane = wave::lane_here();
   const int nw = (len + 63) >> 6;
   int cwl = 0, cgd = 0;                  // open segment: bytes / predicted bytes so far
   int carry = 0;
@@ -1295,6 +1300,7 @@ __device__ __forceinline__ void base_adds(const DevTbl& t1, const DevTbl& t2, ui
 // else mid (+1 on a vowel).  It never jumps over a space, so it enters every
 // word at its first byte and a word's entries depend on that word alone.
 __device__ __forceinline__ bool word_lists(Win& win, Smem& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+  lane = wave::lane_here();
   nws = 0;
   nsp = 0;
   bool ok = true;
@@ -1350,6 +1356,7 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
 }
 
 __device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, int nws, int lane) {
+  lane = wave::lane_here();
   int nch = 0;
   int sn = (LNG_PF & 1) && lane < nws ? S.wst[lane] : 0;       // word starts one block ahead
   for (int i0 = 0; i0 < nws; i0 += 64) {
@@ -1390,6 +1397,7 @@ __device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, 
 template <bool D>
 __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int nch, int& c0, int& nb,
                           int& eb, bool& ok, int lane) {
+  lane = wave::lane_here();
   nb = 0;
   eb = 0;
   uint32_t A = 0, B = 0;                 // last two kept hashes (pq0 / pq1 as a set)
@@ -1500,6 +1508,7 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm
 template <bool D>
 __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& sm, Slot& S, int nsp, int& j0, int off, int next,
                            int& nd, int& nx, int& edm, int& exm, bool& ok, int lane) {
+  lane = wave::lane_here();
   edm = 0;
   exm = 0;
   const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
@@ -1649,6 +1658,7 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& s
 template <bool D>
 __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int off, int& nb, int& nd,
                          int& nx, int& eb, int& edm, int& exm, bool& ok, int lane) {
+  lane = wave::lane_here();
   const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
   if (!ok) return tb;
   nb = 0;
@@ -1824,6 +1834,7 @@ __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, i
 template <bool D>
 LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int lowest, int dummy_off, int lane, int eb, int ed, int ex) {
+  lane = wave::lane_here();
   // The hit rounds (quad_round / octa_round / cjk_round) already turned their
   // nb / nd / nx hits into eb base, ed delta and ex distinct emissions (tote
   // adds, zero langprobs dropped) in be_* / d_* / x_*.
