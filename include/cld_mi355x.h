@@ -120,7 +120,8 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
 /* Same accounting split per kernel stage: ms[0] the wavefront kernel (k_wave),
- * ms[1] the long-document stage (length ordering + k_long), ms[2] the
+ * (with HTML pages: the GPU rewrite of the pages into plain text, k_html_rewrite,
+ * is counted in ms[0]), ms[1] the long-document stage (length ordering + k_long), ms[2] the
  * sequential kernel (k_general).  Sums since the previous call of either
  * function; resets. */
 int cld_kernel_times(int ctx, double* ms3, int* launches);
