@@ -11,7 +11,7 @@
 //   * the lowercaser takes the HTML half of its remap pairs (:755-762).
 // Every '<' and '&' outside a skipped tag or entity is reached (the scanner
 // stops at both), so one left-to-right pass per document -- k_html_rewrite,
-// one lane per document -- rewrites the page into a plain document with the
+// one wavefront per page -- rewrites the page into a plain document with the
 // same spans: each tag becomes one space, each entity its decoded bytes, a
 // dropped '&' nothing, and the page keeps its length (spaces after the text:
 // trailing spaces add nothing to any span).  k_wave / k_long then score it as
@@ -20,9 +20,11 @@
 //     on an entity saw the raw '&' (script 0): the rewrite marks those
 //     positions in hflag, and the span builders read script 0 there;
 //   * the lowercaser's HTML half: a page holding a character whose HTML-mode
-//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, or
-//     more than kHtmlRewriteMax bytes (the span soft limit reads the raw length,
-//     :828-833) is not rewritten and stays on k_general.
+//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, more
+//     than kHtmlCands '<' / '&' bytes, or more than kHtmlRewriteMax bytes is not
+//     rewritten and stays on k_general.  (The span soft limit reads the raw
+//     bytes left, :815-819; it splits nothing below kMaxScriptBytes, ~40 KB,
+//     so up to 32 KB raw and rewritten pages cut their spans alike.)
 // A rewritten page that k_wave / k_long re-queue goes to k_general, which
 // scores the original page in HTML mode.
 //
@@ -51,8 +53,9 @@ using wave::wshr1;
 using wave::wsum;
 using wave::wsync;
 
-constexpr int kHtmlRewriteMax = 8192;   // the page is staged in LDS (larger: k_general)
-constexpr int kHtmlCands = 512;        // '<' / '&' candidates per page (more: the page stays on k_general)
+constexpr int kHtmlRewriteMax = 32768;  // larger pages stay on k_general (the span soft limit, above)
+constexpr int kHtmlStage = 8192;        // pages up to this size are staged in LDS, larger ones read in place
+constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per page (more: the page stays on k_general)
 constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
 #ifndef HTML_EXP
 #define HTML_EXP 0
@@ -114,12 +117,172 @@ __device__ __forceinline__ int scan_tag_wave(const TagTables& tt, const uint8_t*
 }
 
 struct HtmlSmem {
-  uint8_t text[kHtmlRewriteMax + 16];  // the page
+  uint8_t text[kHtmlStage + 16];       // the page (up to kHtmlStage bytes)
   uint16_t pos[kHtmlCands];            // candidate positions, in page order
   uint16_t len[kHtmlCands];            // bytes the scan consumes there
   uint32_t dec[kHtmlCands];            // an entity's decoded bytes
   uint8_t meta[kHtmlCands];            // kind (0 tag, 1 entity, 2 dropped '&') | plen << 2 | bad << 5 | reached << 6
 };
+
+// A byte of the page: staged pages are NUL padded in LDS; larger ones are read
+// in place and bounded here.
+template <bool kStaged>
+__device__ __forceinline__ uint32_t txt_at(const uint8_t* txt, int p, int L) {
+  return kStaged || p < L ? txt[p] : 0u;
+}
+
+// One page (steps 1-3 above).  txt is the page in LDS (kStaged, up to
+// kHtmlStage bytes) or in place in HBM (up to kHtmlRewriteMax bytes).
+template <bool kStaged>
+__device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables& tt, HtmlSmem& S,
+                                             const uint8_t* txt, const int L, const uint64_t a, const int i,
+                                             const uint8_t sp, uint8_t* __restrict__ special,
+                                             uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
+                                             unsigned long long* __restrict__ prof, const uint64_t am0,
+                                             const uint64_t am1, const int lane) {
+  const DocView dv{txt, L};
+  // 1a. candidates, in page order
+  int K = 0;
+  for (int w0 = 0; w0 < L; w0 += 64) {
+    const int p = w0 + lane;
+    const uint32_t c = p < L ? txt[p] : 0u;
+    const bool cand = c == '<' || c == '&';
+    const uint64_t m = __ballot(cand);
+    const int k = K + __popcll(m & lanemask_lt(lane));
+    if (cand && k < kHtmlCands) S.pos[k] = (uint16_t)p;
+    K += __popcll(m);
+  }
+  if (K > kHtmlCands) return;                                // stays HTML: k_general
+  wsync();
+  // 1b. each candidate as if the scan reached it
+  for (int j = lane; j < K; j += 64) {
+    const int p = S.pos[j];
+    int ln = 1, kind = 0, plen = 0;
+    bool bad = false;
+    uint32_t dec = 0;
+    if (txt[p] == '<') {
+      ln = 0;                                                  // (a reached tag is scanned in step 2)
+    } else {
+      uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      int tlen = 0;
+      entity_to_buffer(T, dv, p, L - p, tmp, &tlen, &plen);
+      if (plen > 0) {
+        kind = 1;
+        ln = tlen;
+        dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
+        bad = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
+              (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
+      } else {
+        kind = 2;                                              // undecodable: the '&' is dropped
+        plen = 0;
+      }
+    }
+    S.len[j] = (uint16_t)ln;
+    S.dec[j] = dec;
+    S.meta[j] = (uint8_t)(kind | (plen << 2) | (bad ? 0x20 : 0));
+  }
+  wsync();
+  // 2. which candidates the scan reaches: past the end of the last reached one
+  const long long t2 = prof ? (long long)clock64() : 0;
+  int cur = 0;
+  for (int j0 = 0; j0 < K; j0 += 64) {
+    const int j = j0 + lane;
+    const int p = j < K ? (int)S.pos[j] : 0x7FFFFFFF, ln = j < K ? (int)S.len[j] : 0;
+    const int m = K - j0 < 64 ? K - j0 : 64;
+    const uint64_t tag_m = __ballot(j < K && (S.meta[j] & 3) == 0);
+    uint64_t reach = 0;
+    for (int t = 0; t < m; ++t) {
+      const int pt = rdl(p, t);
+      if (pt >= cur) {
+        reach |= 1ull << t;
+        int lt = rdl(ln, t);
+        if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
+#if HTML_EXP == 1
+          lt = 1;
+#elif HTML_EXP == 2
+          lt = scan_tag_wave(tt, txt, pt, L - pt, lane) > 0 ? 1 : 2;
+#else
+          lt = scan_tag_wave(tt, txt, pt, L - pt, lane);
+#endif
+          if (lane == t) S.len[j] = (uint16_t)lt;
+        }
+        cur = pt + lt;
+      }
+    }
+    if (j < K) S.meta[j] = (uint8_t)(S.meta[j] | (((reach >> lane) & 1) ? 0x40 : 0));
+  }
+  wsync();
+  if (prof && lane == 0) atomicAdd(prof, (unsigned long long)((long long)clock64() - t2));
+  // 3. the output, window by window
+  uint8_t* o = hbuf + a;
+  uint8_t* f = hflag + a;
+  int q = 0, cb = 0, bad = 0, conts = 0, need = 0;
+  uint32_t cover = 0;                                          // end of the last reached candidate so far
+  uint32_t drop_prev = 0;                                      // the byte before this window was a dropped '&'
+  for (int w0 = 0; w0 < L; w0 += 64) {
+    const int p = w0 + lane;
+    const bool in = p < L;
+    const uint32_t c = in ? txt[p] : 0u;
+    const bool cand = in && (c == '<' || c == '&');
+    const uint64_t cm = __ballot(cand);
+    const int j = cand ? cb + __popcll(cm & lanemask_lt(lane)) : 0;
+    cb += __popcll(cm);
+    const uint32_t meta = cand ? S.meta[j] : 0u;
+    const bool reached = (meta & 0x40) != 0;
+    const uint32_t end = reached ? (uint32_t)(p + S.len[j]) : 0u;
+    // covered: inside a reached candidate that starts before p (the running
+    // maximum of reached ends, carried across windows)
+    const uint32_t mx = dpp_scan_incl(end, 0u, OpMax());
+    const uint32_t before = wshr1(mx, 0u);
+    const uint32_t cov_end = before > cover ? before : cover;
+    const bool covered = in && !reached && (uint32_t)p < cov_end;
+    const int kind = meta & 3, plen = (meta >> 2) & 7;
+    const bool text = in && !covered && !reached;
+    int emit = 0;
+    if (reached) emit = kind == 0 ? 1 : kind == 1 ? plen : 0;
+    else if (text) emit = 1;
+    // the first byte after a dropped '&' carries the lookahead mark
+    const bool dropped = reached && kind == 2;
+    const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
+    const int at = q + excl_scan(emit, lane);
+    if (text) {
+      o[at] = (uint8_t)c;
+      f[at] = (uint8_t)dprev;
+      // plain characters: well formed, and the same lowering in HTML mode
+      if (c < 0x80) {
+        bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
+      } else if ((c & 0xC0) == 0x80) {
+        ++conts;
+      } else {
+        const int m = utf8_len((uint8_t)c);
+        const uint32_t b1 = txt_at<kStaged>(txt, p + 1, L), b2 = txt_at<kStaged>(txt, p + 2, L);
+        bad |= (p + m > L || !html_lower_same(T, c, b1, b2, m)) ? 1 : 0;
+        need += m - 1;
+      }
+    } else if (reached && kind == 0) {
+      o[at] = ' ';
+      f[at] = (uint8_t)dprev;
+    } else if (reached && kind == 1) {
+      const uint32_t d = S.dec[j];
+      for (int k = 0; k < plen; ++k) {
+        o[at + k] = (uint8_t)(d >> (8 * k));
+        f[at + k] = k == 0 ? 1 : 0;
+      }
+      bad |= (meta & 0x20) ? 1 : 0;
+    }
+    q = rdl(at + emit, 63);
+    const uint32_t wmx = rdlu(mx, 63);
+    cover = wmx > cover ? wmx : cover;
+    drop_prev = rdlu(dropped ? 1u : 0u, 63);
+  }
+  // the page keeps its length: spaces after the text
+  for (int p = q + lane; p < L; p += 64) {
+    o[p] = ' ';
+    f[p] = 0;
+  }
+  bad |= wsum(conts - need) != 0 ? 1 : 0;                      // every continuation byte claimed
+  if (__ballot(bad != 0) == 0 && lane == 0) special[i] = (uint8_t)((sp & ~kSpecialHtml) | kSpecialRewritten);
+}
 
 __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables* __restrict__ Tp,
                                                                const uint8_t* __restrict__ buf,
@@ -148,8 +311,10 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
     const int64_t len64 = (int64_t)(offs[i + 1] - a);
     if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: k_general
     const int L = (int)len64;
-    // the page into LDS (16-byte pieces from aligned dwords), NUL padded
-    {
+    if (L > kHtmlStage) {
+      rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, prof, am0, am1, lane);
+    } else {
+      // the page into LDS (from aligned dwords), NUL padded
       const uint8_t* g = buf + a;
       for (int p = lane * 4; p < L + 16; p += 256) {
         uint32_t v = 0;
@@ -157,150 +322,9 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
         for (int k = 0; k < 4; ++k) v |= (uint32_t)(p + k < L ? g[p + k] : 0) << (8 * k);
         *reinterpret_cast<uint32_t*>(&S.text[p]) = v;
       }
+      wsync();
+      rewrite_page<true>(T, tt, S, S.text, L, a, i, sp, special, hbuf, hflag, prof, am0, am1, lane);
     }
-    wsync();
-    const DocView dv{S.text, L};
-    // 1a. candidates, in page order
-    int K = 0;
-    for (int w0 = 0; w0 < L; w0 += 64) {
-      const int p = w0 + lane;
-      const uint32_t c = p < L ? S.text[p] : 0u;
-      const bool cand = c == '<' || c == '&';
-      const uint64_t m = __ballot(cand);
-      const int k = K + __popcll(m & lanemask_lt(lane));
-      if (cand && k < kHtmlCands) S.pos[k] = (uint16_t)p;
-      K += __popcll(m);
-    }
-    if (K > kHtmlCands) continue;                                // stays HTML: k_general
-    wsync();
-    // 1b. each candidate as if the scan reached it
-    for (int j = lane; j < K; j += 64) {
-      const int p = S.pos[j];
-      int ln = 1, kind = 0, plen = 0;
-      bool bad = false;
-      uint32_t dec = 0;
-      if (S.text[p] == '<') {
-        ln = 0;                                                  // (a reached tag is scanned in step 2)
-      } else {
-        uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int tlen = 0;
-        entity_to_buffer(T, dv, p, L - p, tmp, &tlen, &plen);
-        if (plen > 0) {
-          kind = 1;
-          ln = tlen;
-          dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
-          bad = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
-                (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
-        } else {
-          kind = 2;                                              // undecodable: the '&' is dropped
-          plen = 0;
-        }
-      }
-      S.len[j] = (uint16_t)ln;
-      S.dec[j] = dec;
-      S.meta[j] = (uint8_t)(kind | (plen << 2) | (bad ? 0x20 : 0));
-    }
-    wsync();
-    // 2. which candidates the scan reaches: past the end of the last reached one
-    const long long t2 = prof ? (long long)clock64() : 0;
-    int cur = 0;
-    for (int j0 = 0; j0 < K; j0 += 64) {
-      const int j = j0 + lane;
-      const int p = j < K ? (int)S.pos[j] : 0x7FFFFFFF, ln = j < K ? (int)S.len[j] : 0;
-      const int m = K - j0 < 64 ? K - j0 : 64;
-      const uint64_t tag_m = __ballot(j < K && (S.meta[j] & 3) == 0);
-      uint64_t reach = 0;
-      for (int t = 0; t < m; ++t) {
-        const int pt = rdl(p, t);
-        if (pt >= cur) {
-          reach |= 1ull << t;
-          int lt = rdl(ln, t);
-          if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
-#if HTML_EXP == 1
-            lt = 1;
-#elif HTML_EXP == 2
-            lt = scan_tag_wave(tt, S.text, pt, L - pt, lane) > 0 ? 1 : 2;
-#else
-            lt = scan_tag_wave(tt, S.text, pt, L - pt, lane);
-#endif
-            if (lane == t) S.len[j] = (uint16_t)lt;
-          }
-          cur = pt + lt;
-        }
-      }
-      if (j < K) S.meta[j] = (uint8_t)(S.meta[j] | (((reach >> lane) & 1) ? 0x40 : 0));
-    }
-    wsync();
-    if (prof && lane == 0) atomicAdd(prof, (unsigned long long)((long long)clock64() - t2));
-    // 3. the output, window by window
-    uint8_t* o = hbuf + a;
-    uint8_t* f = hflag + a;
-    int q = 0, cb = 0, bad = 0, conts = 0, need = 0;
-    uint32_t cover = 0;                                          // end of the last reached candidate so far
-    uint32_t drop_prev = 0;                                      // the byte before this window was a dropped '&'
-    for (int w0 = 0; w0 < L; w0 += 64) {
-      const int p = w0 + lane;
-      const bool in = p < L;
-      const uint32_t c = in ? S.text[p] : 0u;
-      const bool cand = in && (c == '<' || c == '&');
-      const uint64_t cm = __ballot(cand);
-      const int j = cand ? cb + __popcll(cm & lanemask_lt(lane)) : 0;
-      cb += __popcll(cm);
-      const uint32_t meta = cand ? S.meta[j] : 0u;
-      const bool reached = (meta & 0x40) != 0;
-      const uint32_t end = reached ? (uint32_t)(p + S.len[j]) : 0u;
-      // covered: inside a reached candidate that starts before p (the running
-      // maximum of reached ends, carried across windows)
-      const uint32_t mx = dpp_scan_incl(end, 0u, OpMax());
-      const uint32_t before = wshr1(mx, 0u);
-      const uint32_t cov_end = before > cover ? before : cover;
-      const bool covered = in && !reached && (uint32_t)p < cov_end;
-      const int kind = meta & 3, plen = (meta >> 2) & 7;
-      const bool text = in && !covered && !reached;
-      int emit = 0;
-      if (reached) emit = kind == 0 ? 1 : kind == 1 ? plen : 0;
-      else if (text) emit = 1;
-      // the first byte after a dropped '&' carries the lookahead mark
-      const bool dropped = reached && kind == 2;
-      const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
-      const int at = q + excl_scan(emit, lane);
-      if (text) {
-        o[at] = (uint8_t)c;
-        f[at] = (uint8_t)dprev;
-        // plain characters: well formed, and the same lowering in HTML mode
-        if (c < 0x80) {
-          bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
-        } else if ((c & 0xC0) == 0x80) {
-          ++conts;
-        } else {
-          const int m = utf8_len((uint8_t)c);
-          const uint32_t b1 = S.text[p + 1], b2 = S.text[p + 2];      // (NUL padded)
-          bad |= (p + m > L || !html_lower_same(T, c, b1, b2, m)) ? 1 : 0;
-          need += m - 1;
-        }
-      } else if (reached && kind == 0) {
-        o[at] = ' ';
-        f[at] = (uint8_t)dprev;
-      } else if (reached && kind == 1) {
-        const uint32_t d = S.dec[j];
-        for (int k = 0; k < plen; ++k) {
-          o[at + k] = (uint8_t)(d >> (8 * k));
-          f[at + k] = k == 0 ? 1 : 0;
-        }
-        bad |= (meta & 0x20) ? 1 : 0;
-      }
-      q = rdl(at + emit, 63);
-      const uint32_t wmx = rdlu(mx, 63);
-      cover = wmx > cover ? wmx : cover;
-      drop_prev = rdlu(dropped ? 1u : 0u, 63);
-    }
-    // the page keeps its length: spaces after the text
-    for (int p = q + lane; p < L; p += 64) {
-      o[p] = ' ';
-      f[p] = 0;
-    }
-    bad |= wsum(conts - need) != 0 ? 1 : 0;                      // every continuation byte claimed
-    if (__ballot(bad != 0) == 0 && lane == 0) special[i] = (uint8_t)((sp & ~kSpecialHtml) | kSpecialRewritten);
     wsync();
   }
 }

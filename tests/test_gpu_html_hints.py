@@ -110,6 +110,30 @@ def test_html_rewrite_lookahead_edges(gpu, oracle):
     assert_same(got, ref, "html rewrite edges")
 
 
+def test_html_rewrite_large_pages(gpu, oracle):
+    """Pages past the LDS stage (kHtmlStage, 8 KB) are rewritten in place in
+    HBM up to kHtmlRewriteMax (32 KB); more than kHtmlCands '<' / '&' bytes or
+    more than 32 KB keep the sequential kernel."""
+    parts = ["abcα&eacute;def", "дом&#x434;м", "x&lt;b&gt;y", "caf&eacute;<b>cr&egrave;me</b>",
+             "na&iuml;ve&nbsp;text", "&#12354;&#12356;あ", "<a <b>text</b> more", "<!-- c -->d&#101;f",
+             "le chat noir mange la souris grise"]
+    docs = [("<p>" + "le chat noir mange la souris grise &amp; " * 500 + "</p>").encode(),         # 21 KB
+            ("<p lang=ru>" + "русский текст " * 1200 + "</p>").encode(),  # 30 KB
+            (" ".join(parts) + " ").encode() * 45,                                                  # 8.6 KB, 765 candidates
+            ("<script>var x = '<p>';</script>" + "der Hund lief die Strasse entlang " * 400).encode(),  # 14 KB, a tag scan in HBM
+            ("<div>" + "der Hund l&auml;uft &uuml;ber die Stra&szlig;e <br> " * 300 + "</div>").encode(),  # > kHtmlCands
+            ("<p>" + "caf&eacute; " * 4000 + "</p>").encode()]                                       # > kHtmlRewriteMax
+    assert 8192 < min(len(d) for d in docs) and len(docs[1]) <= 32768
+    buf, offs = gpu.pack(docs)
+    n = len(docs)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+    st = gpu.last_stats()
+    assert 2 <= st.general_docs <= 3
+    pr = priors_for(gpu, buf, offs, True, None)
+    ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr)
+    assert_same(got, ref, "html large pages")
+
+
 @pytest.mark.parametrize("cfg,n,seed", [("c2", 20000, 31), ("c3", 300, 32), ("c4", 11000, 33), ("c5", 20000, 34)])
 def test_plain_documents_with_hints(gpu, oracle, cfg, n, seed):
     buf, offs = corpus.GENERATORS[cfg](n)
