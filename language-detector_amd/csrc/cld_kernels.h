@@ -43,7 +43,8 @@ size_t cld_vec_work_bytes();
 hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
-                                  const uint64_t* pool_off, int32_t* n_chunks, uint32_t cflags, hipStream_t s);
+                                  const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
+                                  hipStream_t s);
 hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
                                  const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
 size_t cld_short_work_bytes();

@@ -122,7 +122,8 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
                                                    const uint8_t* __restrict__ special,
                                                    const uint32_t* __restrict__ priors,
                                                    cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
-                                                   int32_t* __restrict__ n_chunks, uint32_t cflags) {
+                                                   int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ order,
+                                                   uint32_t cflags) {
   const DevTables& T = *Tp;
 #if GEN_LANES_PER_WAVE == 1
   if (threadIdx.x != 0) return;
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict_
   for (;;) {
     const uint32_t k = atomicAdd(&counters[kCtrDequeue2], 1u);
     if (k >= (uint32_t)n) break;                 // every lane reaches this exit
-    const uint32_t i = k;
+    const uint32_t i = order ? order[k] : k;     // longest documents first
     const uint64_t a = offs[i], b = offs[i + 1];
     VecOut& vo = w.vo;
     vo.orig.d = w.map_o; vo.orig.cap = kMapOrigCap; vo.orig.n = 0; vo.orig.over = false;
@@ -490,7 +491,8 @@ size_t cld_vec_work_bytes() { return sizeof(cld::VecWork); }
 hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
-                                  const uint64_t* pool_off, int32_t* n_chunks, uint32_t cflags, hipStream_t s) {
+                                  const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
+                                  hipStream_t s) {
   if (n <= 0) return hipSuccess;
 #if GEN_LANES_PER_WAVE == 1
   dim3 grid(lanes), block(64);
@@ -498,7 +500,7 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
   dim3 grid(lanes / 64), block(64);
 #endif
   hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
-                     priors, pool, pool_off, n_chunks, cflags);
+                     priors, pool, pool_off, n_chunks, order, cflags);
   return hipGetLastError();
 }
 

@@ -642,12 +642,22 @@ struct DevMap {
   uint8_t* d; int n, cap;
   int pend_op, pend_len, max_a, max_ap;
   bool over;                                  // capacity exceeded: the document reports an error
+  // MapBack's resume point: the start (byte index, A and A' offsets) of the
+  // range the last lookup settled on.  Entries before it never change (the
+  // map only grows at its end), and every range before it ends at or below
+  // its A' offset, so a lookup at or past that offset may start there: the
+  // summary buffer maps its chunks in increasing order, which made MapBack
+  // quadratic in the span length when every lookup walked from the start.
+  int cur_i, cur_a, cur_ap;
 };
 __device__ void dm_push(DevMap& m, int op, int len) {           // Emit :203-206
   if (m.n >= m.cap) { m.over = true; return; }
   m.d[m.n++] = (uint8_t)((op << 6) | (len & 0x3F));
 }
-__device__ void dm_clear(DevMap& m) { m.n = 0; m.pend_op = DM_COPY; m.pend_len = 0; m.max_a = 0; m.max_ap = 0; }
+__device__ void dm_clear(DevMap& m) {
+  m.n = 0; m.pend_op = DM_COPY; m.pend_len = 0; m.max_a = 0; m.max_ap = 0;
+  m.cur_i = 0; m.cur_a = 0; m.cur_ap = 0;
+}
 __device__ void dm_flush(DevMap& m) {                           // Flush :158-187
   if (m.pend_len == 0) return;
   if (m.pend_op == DM_COPY && m.n > 0) {
@@ -698,7 +708,9 @@ __device__ int dm_map_back(DevMap& m, int ap) {
   if (ap < 0) return 0;
   if (m.max_ap <= ap) return (ap - m.max_ap) + m.max_a;
   int lo_a = 0, lo_ap = 0, i = 0;
+  if (m.cur_ap <= ap) { i = m.cur_i; lo_a = m.cur_a; lo_ap = m.cur_ap; }
   while (i < m.n) {
+    const int i0 = i;
     int op = DM_PREFIX, len = 0;
     while (i < m.n && op == DM_PREFIX) {
       const uint8_t c = m.d[i++];
@@ -708,6 +720,7 @@ __device__ int dm_map_back(DevMap& m, int ap) {
     if (op == DM_PREFIX) break;
     const int hi_a = lo_a + (op == DM_INSERT ? 0 : len), hi_ap = lo_ap + (op == DM_DELETE ? 0 : len);
     if (ap < hi_ap) {
+      m.cur_i = i0; m.cur_a = lo_a; m.cur_ap = lo_ap;
       const int a = ap - (lo_ap - lo_a);
       return a >= hi_a ? hi_a : a;
     }

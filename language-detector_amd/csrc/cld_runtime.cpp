@@ -406,6 +406,7 @@ struct Device {
     uint64_t* pool_off = nullptr; size_t pool_off_cap = 0;
     int32_t* nch = nullptr; size_t nch_cap = 0;
     uint64_t* pos = nullptr; size_t pos_cap = 0;
+    uint32_t* order = nullptr; size_t order_cap = 0;
     cld_chunk* compact = nullptr; size_t compact_cap = 0;
   } vec;
   std::mutex mu;
@@ -986,7 +987,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     V.lanes = lanes;
   }
   const size_t kSub = 256 * 1024;
-  const uint64_t kSubBytes = 32ull << 20;
+  static const uint64_t kSubBytes = (getenv("CLD_VEC_SUB_MB") ? (uint64_t)atoi(getenv("CLD_VEC_SUB_MB")) : 32ull) << 20;
   // test hook: CLD_VEC_POOL_SMALL=1 makes first-pass pool regions too small so
   // the retry below runs (tests/test_gpu_vector.py)
   static const bool small_pool = getenv("CLD_VEC_POOL_SMALL") && atoi(getenv("CLD_VEC_POOL_SMALL")) > 0;
@@ -995,6 +996,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   // + 256); results to res, vector sizes to nch (-1: the document overflowed
   // its pool region or an offset map), the vectors to ch in document order.
   std::vector<uint64_t> pool_off, pos;
+  std::vector<uint32_t> order, bstart;
+  static const bool no_order = getenv("CLD_VEC_ORDER") && atoi(getenv("CLD_VEC_ORDER")) == 0;   // (A/B only)
   auto sub = [&](const uint8_t* b, const uint64_t* o, size_t m, cld_result* res, const uint8_t* sp,
                  const uint32_t* pr, bool big, std::vector<int32_t>& nch, std::vector<cld_chunk>& ch) -> int {
     const uint64_t base = o[0], bytes = o[m] - base;
@@ -1009,6 +1012,19 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
       return CLD_ENOMEM;
     if (sp && grow(&V.sp, &V.sp_cap, m)) return CLD_ENOMEM;
     if (pr && grow(&V.pri, &V.pri_cap, 16 * m)) return CLD_ENOMEM;
+    // Longest documents first: a wave runs one document start to end, so with
+    // more documents than waves a long one dequeued late sets the batch's end.
+    // A counting sort by bit length of the size (descending).
+    const bool ordered = !no_order && m > (size_t)V.lanes;
+    if (ordered) {
+      if (grow(&V.order, &V.order_cap, m)) return CLD_ENOMEM;
+      bstart.assign(66, 0);
+      auto bucket = [&](size_t i) { return 64 - __builtin_clzll((o[i + 1] - o[i]) | 1); };   // 1..64
+      for (size_t i = 0; i < m; ++i) ++bstart[65 - bucket(i)];
+      for (int k = 1; k < 66; ++k) bstart[k] += bstart[k - 1];
+      order.resize(m);
+      for (size_t i = 0; i < m; ++i) order[bstart[64 - bucket(i)]++] = (uint32_t)i;
+    }
     hipStream_t s = d->stream;
     HIP_OK(hipStreamWaitEvent(s, d->done, 0));
     if (bytes) HIP_OK(hipMemcpyAsync(V.in, b + base, bytes, hipMemcpyHostToDevice, s));
@@ -1016,10 +1032,11 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     HIP_OK(hipMemcpyAsync(V.pool_off, pool_off.data(), (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     if (sp) HIP_OK(hipMemcpyAsync(V.sp, sp, m, hipMemcpyHostToDevice, s));
     if (pr) HIP_OK(hipMemcpyAsync(V.pri, pr, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (ordered) HIP_OK(hipMemcpyAsync(V.order, order.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
     HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
                                   sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off, V.nch,
-                                  cflags & kCldFlags, s));
+                                  ordered ? V.order : nullptr, cflags & kCldFlags, s));
     nch.resize(m);
     HIP_OK(hipMemcpyAsync(res, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1296,7 +1313,7 @@ void cld_shutdown(void) {
     (void)hipHostFree(d->h_ctr);
     for (void* p : {(void*)d->vec.arena, (void*)d->vec.in, (void*)d->vec.offs, (void*)d->vec.out, (void*)d->vec.sp,
                     (void*)d->vec.pri, (void*)d->vec.pool, (void*)d->vec.pool_off, (void*)d->vec.nch,
-                    (void*)d->vec.pos, (void*)d->vec.compact})
+                    (void*)d->vec.pos, (void*)d->vec.order, (void*)d->vec.compact})
       if (p) (void)hipFree(p);
     (void)hipEventDestroy(d->done);
     (void)hipStreamDestroy(d->up_stream);
