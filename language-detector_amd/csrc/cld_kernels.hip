@@ -24,6 +24,16 @@
 // 52K -> 185K docs/s).
 #define GEN_LANES_PER_WAVE 1
 #endif
+// waves per SIMD the sequential kernels are compiled for (their register
+// budget); 0: the compiler's choice
+#ifndef GEN_WPE
+#define GEN_WPE 0
+#endif
+#if GEN_WPE > 0
+#define GEN_OCC __attribute__((amdgpu_waves_per_eu(GEN_WPE, GEN_WPE)))
+#else
+#define GEN_OCC
+#endif
 
 namespace cld {
 
@@ -61,7 +71,7 @@ __global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __res
   }
 }
 
-__global__ __launch_bounds__(64) void k_general(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64) GEN_OCC void k_general(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
                                                const uint64_t* __restrict__ offs,
                                                const uint32_t* __restrict__ list,
                                                cld_result* __restrict__ out,
@@ -114,7 +124,7 @@ struct VecWork {
   uint8_t map_l[kMapLowCap];
 };
 
-__global__ __launch_bounds__(64) void k_general_vec(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
+__global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
                                                    const uint64_t* __restrict__ offs, int n,
                                                    cld_result* __restrict__ out,
                                                    uint8_t* __restrict__ arena, uint64_t stride,

@@ -986,8 +986,12 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     if (hipMalloc(&V.arena, (uint64_t)lanes * V.stride) != hipSuccess) { V.arena = nullptr; return CLD_ENOMEM; }
     V.lanes = lanes;
   }
-  const size_t kSub = 256 * 1024;
-  static const uint64_t kSubBytes = (getenv("CLD_VEC_SUB_MB") ? (uint64_t)atoi(getenv("CLD_VEC_SUB_MB")) : 32ull) << 20;
+  // Sub-batches as large as memory allows: a launch lasts at least as long as
+  // its longest document (one wave runs it start to end), so every sub-batch
+  // pays that tail once -- 32 MB sub-batches held C5 to 76K docs/s, one launch
+  // for the 95 MB batch runs it at 208K.  256 MB of text takes ~5 GB of pool.
+  const size_t kSub = 1024 * 1024;
+  static const uint64_t kSubBytes = (getenv("CLD_VEC_SUB_MB") ? (uint64_t)atoi(getenv("CLD_VEC_SUB_MB")) : 256ull) << 20;
   // test hook: CLD_VEC_POOL_SMALL=1 makes first-pass pool regions too small so
   // the retry below runs (tests/test_gpu_vector.py)
   static const bool small_pool = getenv("CLD_VEC_POOL_SMALL") && atoi(getenv("CLD_VEC_POOL_SMALL")) > 0;
