@@ -38,6 +38,15 @@ typedef struct cld_result {
 #define CLD_ENODEV (-19)
 #define CLD_ENOMEM (-12)
 #define CLD_EIO (-5)
+#define CLD_EFAULT (-14)  /* a HIP runtime call failed (device error) */
+#define CLD_ENOSPC (-28)  /* cld_detect_batch_vec: chunk_cap too small for the vectors */
+
+/* summary_lang of a document the GPU could not score.  Such a document is
+ * redone alone once; if it fails again the call returns CLD_EIO and every
+ * other document's result is complete (lang3 = UNKNOWN, percent3 0,
+ * text_bytes 0 for the failed one).  The kernels have no such case short of
+ * a device fault: it exists so one bad document never costs a batch. */
+#define CLD_LANG_FAILED 0xFFFF
 
 /* cld_detect_batch flags: the service's text preparation, applied on the GPU
  * before detection (handlers.go:150-151).
@@ -109,9 +118,12 @@ void cld_shutdown(void);
  * One process per GPU (torch.distributed / bench.py) uses this. */
 int cld_init_device(const char* tables_path, int device);
 
-/* Byte-balanced document shards: cuts[0..nshards] (cuts[0]=0, cuts[nshards]=n)
- * such that shard k = documents [cuts[k], cuts[k+1]).  Host-only helper used
- * by cld_detect_batch's multi-GPU split and by multi-process callers. */
+/* Cost-balanced document shards: cuts[0..nshards] (cuts[0]=0, cuts[nshards]=n)
+ * such that shard k = documents [cuts[k], cuts[k+1]), each holding about
+ * 1/nshards of the estimated kernel cost (a document of <= 256 bytes: 480
+ * units, a longer one: 41/8 units per byte + 2500; measured per-document
+ * kernel times in units of 10 ps).  Host-only helper used by
+ * cld_detect_batch's multi-GPU split and by multi-process callers. */
 int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts);
 
 /* Sum of kernel durations (HIP events on the stream the kernels ran on) of
@@ -168,8 +180,8 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
  * cld_detect_batch_ex's for the same document, exactly as there.
  * chunk_offsets[n+1] receives document i's chunks as
  * chunks[chunk_offsets[i] .. chunk_offsets[i+1]).  If chunk_cap is too small
- * the call returns CLD_ENOMEM with out and chunk_offsets complete and chunks
- * holding the first chunk_cap entries.  A document whose vector outgrows its
+ * the call returns CLD_ENOSPC with out and chunk_offsets complete and chunks
+ * holding the first chunk_cap entries (CLD_ENOMEM: device memory ran out).  A document whose vector outgrows its
  * working region is redone alone with 8x the room; should that fail too, it
  * gets an empty vector and the call returns CLD_EIO with every other
  * document's result and vector complete.  Every document runs the sequential

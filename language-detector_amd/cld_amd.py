@@ -27,6 +27,8 @@ FLAG_SCORE_AS_QUADS = 0x0100   # CLD_FLAG_SCORE_AS_QUADS = kCLDFlagScoreAsQuads 
 FLAG_BEST_EFFORT = 0x4000      # CLD_FLAG_BEST_EFFORT = kCLDFlagBestEffort (compact_lang_det.h:349)
 UNKNOWN_ENCODING = 23      # encodings.h UNKNOWN_ENCODING
 UNKNOWN_LANGUAGE = 26      # generated_language.h UNKNOWN_LANGUAGE
+LANG_FAILED = 0xFFFF       # include/cld_mi355x.h CLD_LANG_FAILED: a document without a result
+EIO, ENOMEM, ENOSPC = -5, -12, -28   # include/cld_mi355x.h error codes
 
 RESULT_DTYPE = np.dtype([("lang3", "<u2", 3), ("summary_lang", "<u2"), ("percent3", "i1", 3),
                          ("is_reliable", "u1"), ("text_bytes", "<i4"), ("normalized3", "<f8", 3)])
@@ -63,6 +65,17 @@ class BatchStats(ctypes.Structure):
 
 class CldError(RuntimeError):
     pass
+
+
+class PartialBatchError(CldError):
+    """CLD_EIO from a batch call: every result is complete except the documents
+    in `failed` (summary_lang == LANG_FAILED), which the GPU could not score even
+    alone.  `value` is what the call would have returned."""
+
+    def __init__(self, what, value, failed):
+        super().__init__("%s: %d document(s) without a result" % (what, int(np.count_nonzero(failed))))
+        self.value = value
+        self.failed = failed
 
 
 def build():
@@ -229,6 +242,8 @@ def detect_batch(docs=None, buf=None, offsets=None, flags=0):
         return out
     bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
     rc = lib().cld_detect_batch(bptr, offsets.ctypes.data, n, out.ctypes.data, flags)
+    if rc == EIO:
+        raise PartialBatchError("cld_detect_batch", out, out["summary_lang"] == LANG_FAILED)
     if rc != 0:
         raise CldError("cld_detect_batch failed: %d" % rc)
     return out
@@ -254,6 +269,8 @@ def detect_batch_ex(docs=None, buf=None, offsets=None, hints=None, html=False, f
     bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
     rc = lib().cld_detect_batch_ex(bptr, offsets.ctypes.data, n, ctypes.cast(harr, ctypes.c_void_p) if harr else None,
                                    (FLAG_HTML if html else 0) | flags, out.ctypes.data)
+    if rc == EIO:
+        raise PartialBatchError("cld_detect_batch_ex", out, out["summary_lang"] == LANG_FAILED)
     if rc != 0:
         raise CldError("cld_detect_batch_ex failed: %d" % rc)
     return out
@@ -287,7 +304,10 @@ def detect_batch_vec(docs=None, buf=None, offsets=None, hints=None, html=False, 
                                         coffs.ctypes.data)
         if rc == 0:
             return out, chunks[:int(coffs[-1])], coffs
-        if rc != -12 or chunk_cap is not None:
+        if rc == EIO:                                      # some document got no vector (an empty one)
+            raise PartialBatchError("cld_detect_batch_vec", (out, chunks[:int(coffs[-1])], coffs),
+                                    out["summary_lang"] == LANG_FAILED)
+        if rc != ENOSPC or chunk_cap is not None:
             break
         cap = int(coffs[-1])
     raise CldError("cld_detect_batch_vec failed: %d" % rc)

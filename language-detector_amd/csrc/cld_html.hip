@@ -57,9 +57,6 @@ constexpr int kHtmlRewriteMax = 32768;  // larger pages stay on k_general (the s
 constexpr int kHtmlStage = 8192;        // pages up to this size are staged in LDS, larger ones read in place
 constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per page (more: the page stays on k_general)
 constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
-#ifndef HTML_EXP
-#define HTML_EXP 0
-#endif
 
 // The character b0 b1 b2 (n bytes) lowers the same way in HTML mode as in plain text.
 __device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0, uint32_t b1, uint32_t b2, int n) {
@@ -197,13 +194,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
         reach |= 1ull << t;
         int lt = rdl(ln, t);
         if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
-#if HTML_EXP == 1
-          lt = 1;
-#elif HTML_EXP == 2
-          lt = scan_tag_wave(tt, txt, pt, L - pt, lane) > 0 ? 1 : 2;
-#else
           lt = scan_tag_wave(tt, txt, pt, L - pt, lane);
-#endif
           if (lane == t) S.len[j] = (uint16_t)lt;
         }
         cur = pt + lt;

@@ -6,9 +6,6 @@
 #include <stdint.h>
 #include "cld_device.h"
 
-// Short-document bucket: documents up to kShortCap bytes run one per lane with
-// private buffers sized for that length (span text <= 2*CAP).
-constexpr int kShortCap = 256;
 // Wavefront-per-document bucket (cld_wave.hip)
 constexpr int kWaveCap = 256;
 #ifndef WAVE_WPB
@@ -17,9 +14,7 @@ constexpr int kWaveCap = 256;
 constexpr int kWaveWPB = WAVE_WPB;   // waves (documents) per workgroup
 // Largest kLgProbV2Tbl score byte the packed wave tote accepts (runtime checks the blob)
 constexpr int kMaxLgProbScore = 16;
-constexpr int kShortSB = 2 * kShortCap + 64;
-constexpr int kShortLB = kShortSB * 3 / 2 + 64;
-constexpr int kShortHB = kShortCap + 32;
+
 
 // Device counter slots (two 64-byte lines, zeroed per batch)
 // kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general;
@@ -47,7 +42,6 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
                                   hipStream_t s);
 hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
                                  const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
-size_t cld_short_work_bytes();
 // special (nullable): per-document kSpecial* bits; HTML documents are appended
 // to special_list under counters[special_ctr] instead of being scored, hinted
 // ones (kSpecialPriors) are scored with their 16 ApplyHints langprobs
@@ -67,14 +61,11 @@ hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, con
                                    uint8_t* special, uint8_t* hbuf, uint8_t* hflag, unsigned long long* prof,
                                    hipStream_t s);
 size_t cld_wave_smem_bytes();
-hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
-                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                            const uint8_t* special, uint32_t* special_list, int special_ctr, uint32_t cflags,
-                            hipStream_t s);
 hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, hipStream_t s);
+                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, uint32_t fault_doc,
+                              hipStream_t s);
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
                                  uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s);
 size_t cld_long_slot_bytes();
@@ -93,6 +84,8 @@ hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, in
                                     uint64_t* out_offs, void* scratch, hipStream_t s);
 hipError_t cld_launch_strip_write(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,
                                   const uint64_t* out_offs, uint8_t* out, hipStream_t s);
+// fault_doc (k_long, k_general): test hook, batch index of a document made to
+// fail (0xFFFFFFFF: none).  k_long hands it on, k_general marks it failed.
 // d_T: the device's DevTables copy in HBM (k_long reads the table set through
 // it: holding the by-value kernel argument in registers made the kernel spill
 // it to scratch and reload table fields from there at every probe)
@@ -100,6 +93,7 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, hipStream_t s);
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
+                           hipStream_t s);
 }
 #endif

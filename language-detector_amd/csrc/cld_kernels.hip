@@ -1,9 +1,5 @@
 // cld_kernels.hip -- batch kernels over the device pipeline.
 //
-//  k_short<CAP>  one lane per document of <= CAP bytes, all state in private
-//                memory, pass 1 only.  Anything it cannot finish (longer
-//                document, Squeeze restart, Repeats pass, capacity) is
-//                appended to the re-queue list.
 //  k_wave<CAP>   one wavefront per document of <= CAP bytes, state in LDS.
 //  k_long        one wavefront per document of any length up to lng::kDocCap,
 //                per-wave slot in HBM; persistent grid over the wave kernel's
@@ -12,6 +8,11 @@
 //                persistent grid pulling documents from the re-queue list
 //                with one atomic dequeue per document.
 #include "cld_kernels.h"
+// The A/B knobs of earlier rounds that gave wrong results by design are gone;
+// refuse a build that still asks for one.
+#if defined(WAVE_STOP) || defined(LNG_EXP_NOADDS) || defined(HTML_EXP) || defined(LNG_INC)
+#error "experiment knobs (WAVE_STOP, LNG_EXP_NOADDS, HTML_EXP, LNG_INC) are not part of the product build"
+#endif
 #include "cld_pipeline.hip"
 #include "cld_wave.hip"
 #include "cld_long.hip"
@@ -37,39 +38,7 @@
 
 namespace cld {
 
-using ShortWork = Work<kShortSB, kShortLB, kShortHB, false>;
 using GeneralWork = Work<kMaxScriptBuffer, kMaxScriptLowerBuffer, kMaxScoringHits + 8, true>;
-
-__global__ __launch_bounds__(256) void k_short(DevTables T, const uint8_t* __restrict__ buf,
-                                              const uint64_t* __restrict__ offs, int n,
-                                              cld_result* __restrict__ out,
-                                              uint32_t* __restrict__ requeue_list,
-                                              uint32_t* __restrict__ counters,
-                                              const uint8_t* __restrict__ special,
-                                              uint32_t* __restrict__ special_list, int special_ctr,
-                                              uint32_t cflags) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (special && special[i]) {
-    special_list[atomicAdd(&counters[special_ctr], 1u)] = (uint32_t)i;
-    atomicAdd(&counters[kCtrSpecial], 1u);
-    return;
-  }
-  const uint64_t a = offs[i], b = offs[i + 1];
-  const int64_t len = (int64_t)(b - a);
-  bool rq = len > kShortCap;
-  if (!rq) {
-    ShortWork w;
-    Status st{false};
-    DocView d{buf + a, (int)len};
-    detect_doc(T, d, w, &out[i], st, true, nullptr, nullptr, cflags);
-    rq = st.requeue;
-  }
-  if (rq) {
-    uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
-    requeue_list[k] = (uint32_t)i;
-  }
-}
 
 __global__ __launch_bounds__(64) GEN_OCC void k_general(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
                                                const uint64_t* __restrict__ offs,
@@ -78,7 +47,8 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general(const DevTables* __restr
                                                uint8_t* __restrict__ arena, uint64_t stride,
                                                uint32_t* __restrict__ counters, int ctr_count, int ctr_deq,
                                                const uint8_t* __restrict__ special,
-                                               const uint32_t* __restrict__ priors, uint32_t cflags) {
+                                               const uint32_t* __restrict__ priors, uint32_t cflags,
+                                               uint32_t fault_doc) {
   const DevTables& T = *Tp;
 #if GEN_LANES_PER_WAVE == 1
   // one document per wavefront (lane 0): no divergence between documents
@@ -105,8 +75,15 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general(const DevTables* __restr
     const uint8_t sp = special ? special[i] : 0;
     int passes = detect_doc(T, d, w, &out[i], st, !(sp & (kSpecialHtml | kSpecialRewritten)),
                             (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, cflags);
-    if (passes >= 1 && passes <= 3) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
-    else atomicAdd(&counters[kCtrError], 1u);
+    if (i == fault_doc) passes = 0;              // fault injection (CLD_FAULT_DOC, tests only)
+    if (passes >= 1 && passes <= 3) {
+      atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
+    } else {
+      // No result for this document: it is marked (summary CLD_LANG_FAILED) and
+      // counted; the host redoes it alone, the rest of the batch stands.
+      atomicAdd(&counters[kCtrError], 1u);
+      mark_failed(T, &out[i]);
+    }
   }
 }
 
@@ -151,7 +128,8 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __r
     vo.orig.d = w.map_o; vo.orig.cap = kMapOrigCap; vo.orig.n = 0; vo.orig.over = false;
     vo.low.d = w.map_l; vo.low.cap = kMapLowCap; vo.low.n = 0; vo.low.over = false;
     dm_clear(vo.orig); dm_clear(vo.low);
-    vo.v = pool + pool_off[i]; vo.cap = (int)(pool_off[i + 1] - pool_off[i]); vo.n = 0; vo.over = false;
+    const uint64_t reg = pool_off[i + 1] - pool_off[i];
+    vo.v = pool + pool_off[i]; vo.cap = reg > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)reg; vo.n = 0; vo.over = false;
     vo.doc = buf + a; vo.doc_len = (int)(b - a);
     Status st{false};
     DocView d{buf + a, (int)(b - a)};
@@ -288,7 +266,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   unsigned long long* prof, uint32_t cflags,
                                                   const uint8_t* __restrict__ special,
                                                   const uint32_t* __restrict__ priors,
-                                                  const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag) {
+                                                  const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag,
+                                                  uint32_t fault_doc) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -325,6 +304,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                  (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr);
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
+    if (i == fault_doc) passes = -lng::kWhyLength;   // fault injection (CLD_FAULT_DOC): on to k_general
     if (lane == 0) {
       if (passes >= 1 && passes <= 3) {
         atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
@@ -481,17 +461,20 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, hipStream_t s) {
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
+                           hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       fault_doc);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag);
+                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       fault_doc);
   return hipGetLastError();
 }
 
@@ -520,7 +503,6 @@ hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off
   hipLaunchKernelGGL(cld::k_vec_gather, dim3((n + 255) / 256), dim3(256), 0, s, pool, pool_off, n_chunks, pos, n, dst);
   return hipGetLastError();
 }
-size_t cld_short_work_bytes() { return sizeof(cld::ShortWork); }
 size_t cld_wave_smem_bytes() { return sizeof(cld::wave::Smem<kWaveCap>); }
 
 hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
@@ -548,28 +530,18 @@ hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, con
   return hipGetLastError();
 }
 
-hipError_t cld_launch_short(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n,
-                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
-                            const uint8_t* special, uint32_t* special_list, int special_ctr, uint32_t cflags,
-                            hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  dim3 grid((n + 255) / 256), block(256);
-  hipLaunchKernelGGL(cld::k_short, grid, block, 0, s, *T, buf, offs, n, out, requeue_list, counters, special,
-                     special_list, special_ctr, cflags);
-  return hipGetLastError();
-}
-
 hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, hipStream_t s) {
+                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, uint32_t fault_doc,
+                              hipStream_t s) {
 #if GEN_LANES_PER_WAVE == 1
   dim3 grid(lanes), block(64);                   // `lanes` documents in flight, one per wavefront
 #else
   dim3 grid(lanes / 64), block(64);
 #endif
   hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, d_T, buf, offs, list, out, arena, stride,
-                     counters, ctr_count, ctr_deq, special, priors, cflags);
+                     counters, ctr_count, ctr_deq, special, priors, cflags, fault_doc);
   return hipGetLastError();
 }
 }

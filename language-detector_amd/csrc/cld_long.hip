@@ -76,40 +76,14 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 // LDS: the chain walk, the gram hashes and the word scans then read the text
 // at LDS latency instead of through the per-wave HBM slot.  Longer spans run
 // the same code on the slot copy.
-#ifndef LNG_INC
-#define LNG_INC 0
-#endif
 #ifndef LNG_TEXT
-#if LNG_INC
-#define LNG_TEXT 3584                    // the text window; with the emission rings it fills the LDS a wave has
-#else
 #define LNG_TEXT 6128                    // fills the 8 KB the scoring state shares with the Repeats predictor
 #endif
-#endif
 constexpr int kLdsText = LNG_TEXT;
-// Quad spans are scored chunk by chunk as their emissions appear (score_quad):
-// base / delta / distinct emissions not yet in a chunk tote wait in LDS rings
-// (offset, index into the per-GPU tote-adds table).  LNG_INC=0 (default): the
-// round-at-a-time path (hit rounds write every emission to the slot, then
-// score_round).  Measured round 3 on MI355X: LNG_INC=1 is bit-exact but slower
-// (C3 0.97M vs 1.16M docs/s, C5 15.9M vs 17.8M; 416 B/lane scratch vs 304),
-// so it stays an A/B variant (make variant V=inc VFLAGS=-DLNG_INC=1).
-constexpr int kPB = 256, kPD = 128, kPX = 256;    // ring capacities (powers of two)
-constexpr int kRingSlack = 8;                      // consumed entries whose offsets may still be read
 // Read-ahead of the slot's streams (bit 1 word starts, 2 quad chain, 4 octa
 // word ends): overlap vs the registers it costs (measured: only 4 pays).
 #ifndef LNG_PF
 #define LNG_PF 4
-#endif
-// Timing experiment only (wrong results): -DLNG_EXP_NOADDS compiles out the
-// emission tote-add streams (stores in the hit rounds, loads in score_round)
-// so an A/B run prices them.
-#ifdef LNG_EXP_NOADDS
-#define LNG_ADD_ST(dst, v) ((void)(v))
-#define LNG_ADD_LD(src) (0x0101ull)
-#else
-#define LNG_ADD_ST(dst, v) ((dst) = (v))
-#define LNG_ADD_LD(src) (src)
 #endif
 // Inlining of the two largest stages (A/B: a call keeps the caller's
 // registers free, inlining lets the slot / LDS accesses stay global / ds).
@@ -170,14 +144,6 @@ struct alignas(16) Smem {
           uint16_t bst[kMaxCh + 1];
           uint16_t st[2][kMaxCh + 1];    // first delta [0] / distinct [1] emission of chunk k
         };
-#if LNG_INC
-        struct {                         // chunk-at-a-time scoring (score_quad: quad spans)
-          uint16_t pb_off[kPB], pd_off[kPD], px_off[kPX];   // emission offsets, by emission number mod ring
-          uint32_t pb_idx[kPB], pd_idx[kPD], px_idx[kPX];   // their tote adds: T.compat.adds[idx]
-          uint16_t Eq[kMaxCh];           // the round's chunk plan, once its hit count is final
-          uint64_t xlast[4];             // the last distinct adds of an add pass (boost ring update)
-        };
-#endif
       };
     };
     uint16_t pred[kPredictionTableSize]; // Repeats predictor, 16-bit codes (pred_code)
@@ -1479,11 +1445,11 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)p;
-        LNG_ADD_ST(S.be_add[o], l1);
+        S.be_add[o] = l1;
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)p;
-        LNG_ADD_ST(S.be_add[o + 1], l2);
+        S.be_add[o + 1] = l2;
       }
     }
     if (lastl < 64) {
@@ -1606,16 +1572,16 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& s
       edm = rdl(od + md, 63);
       if (in && (apx >> 63)) {
         S.x_off[ox] = (uint16_t)pws;
-        LNG_ADD_ST(S.x_add[ox], apx);
+        S.x_add[ox] = apx;
         ++ox;
       }
       if (in && (axp >> 63)) {
         S.x_off[ox] = (uint16_t)a;
-        LNG_ADD_ST(S.x_add[ox], axp);
+        S.x_add[ox] = axp;
       }
       if (in && (adp >> 63)) {
         S.d_off[od] = (uint16_t)a;
-        LNG_ADD_ST(S.d_add[od], adp);
+        S.d_add[od] = adp;
       }
     }
     if (D && lane <= cut) {
@@ -1698,11 +1664,11 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)(x + len);
-        LNG_ADD_ST(S.be_add[o], l1);
+        S.be_add[o] = l1;
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)(x + len);
-        LNG_ADD_ST(S.be_add[o + 1], l2);
+        S.be_add[o + 1] = l2;
       }
     }
     if (lastl < 64) {
@@ -1742,11 +1708,11 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
       exm = rdl(ox + mx, 63);
       if (md) {
         S.d_off[od] = (uint16_t)x;
-        LNG_ADD_ST(S.d_add[od], adp);
+        S.d_add[od] = adp;
       }
       if (mx) {
         S.x_off[ox] = (uint16_t)x;
-        LNG_ADD_ST(S.x_add[ox], axp);
+        S.x_add[ox] = axp;
       }
     }
     if (D && lane <= cut) {
@@ -1800,12 +1766,12 @@ __device__ __forceinline__ uint64_t chunk_add(const Slot& S, const Smem& s, uint
   int u = t;
   const int seedn = k == 0 ? 1 : 0;
   if (u < seedn) return seed;
-  if ((u -= seedn) < nB) return LNG_ADD_LD(S.be_add[bs + u]);
-  if ((u -= nB) < nD) return LNG_ADD_LD(S.d_add[ds + u]);
-  if ((u -= nD) < nX) return LNG_ADD_LD(S.x_add[xs + u]);
+  if ((u -= seedn) < nB) return S.be_add[bs + u];
+  if ((u -= nB) < nD) return S.d_add[ds + u];
+  if ((u -= nD) < nX) return S.x_add[xs + u];
   if (u - nX >= kMaxBoosts) return s.pri_add[rs][u - nX - kMaxBoosts];   // prior boosts (has_pri)
   const int v = xe - kMaxBoosts + (u - nX);
-  return v < 0 ? s.ring[rs][v + kMaxBoosts] : LNG_ADD_LD(gld(&S.x_add[v]));   // (gld: no LDS/global pointer select)
+  return v < 0 ? s.ring[rs][v + kMaxBoosts] : gld(&S.x_add[v]);   // (gld: no LDS/global pointer select)
 }
 // Chunk plan of k: emission ranges and the number of adds.
 __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
@@ -2037,7 +2003,7 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     uint64_t r4[4];
     for (int i = 0; i < 4; ++i) {
       const int u = ex - kMaxBoosts + i;
-      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : LNG_ADD_LD(gld(&S.x_add[u]));
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : gld(&S.x_add[u]);
     }
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
@@ -2045,614 +2011,6 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   if constexpr (D) mark_sub(s, lane, 4, t2);
 }
 
-#if LNG_INC
-// ------------------------------------------ quad spans: chunks scored as they fill
-// ScoreQuadScriptSpan's rounds (scoreonescriptspan.cc:1231-1277: GetQuadHits,
-// GetOctaHits, LinearizeAll, ChunkAll, ScoreAllHits) without materialising a
-// round's hit or emission streams.  Chain entries are probed 64 at a time and
-// words 64 at a time; their emissions (offset, index into the per-GPU tote-adds
-// table) wait in three small LDS rings, and chunk c is scored as soon as its
-// extent and all of its emissions are known:
-//   * its extent (ChunkAll :978-1031): 20 base entries once the round has
-//     >= 20c + 40 hits -- only the last two chunks of a round depend on the
-//     round's final hit count -- else the plan made at the round's end;
-//   * its base entries: emission numbers up to E_c (the seed is entry 1);
-//   * its delta / distinct entries: offsets <= theta_c, the offset of base
-//     entry E_c (LinearizeAll puts delta < distinct < base on equal offsets),
-//     complete once the word frontier is past theta_c.
-// Entries that belong to chunk c whatever the round's hit count -- its first
-// 15 base entries (ChunkAll gives a chunk >= 15 entries unless it is the last,
-// which takes everything) and the delta / distinct entries up to the 15th's
-// offset -- enter the tote as soon as they exist, so the rings hold only the
-// undecided tail.  Where quad hits are sparse that tail can outgrow a ring:
-// the stream's later emissions of the round then go to the slot instead
-// (be_off / d_off / x_off and the index words beside them), as in the
-// round-at-a-time path.
-struct Inc {                 // one round's state (wave-uniform)
-  int nb, eb;                // quad hits / base emissions so far
-  int nd, nx, ed, ex;        // delta / distinct hits (the caps count hits) and emissions
-  int c, K, Eprev;           // chunk being filled, chunks in the round (once qdone), entry closing chunk c-1
-  int pb_lo, pd_lo, px_lo;   // first emission of each stream not yet in a tote
-  int clo, cgr;              // chunk c: lowest offset so far, base entries so far (the seed included)
-  int qpos;                  // position of the next chain entry (tb when none): later hits are at or after it
-  int ofront;                // no later delta / distinct emission has a smaller offset
-  bool qdone, odone;
-  int next;                  // the round's end (GetQuadHits' next_offset), once qdone
-  uint32_t qA, qB;           // quad repeat filter
-  uint64_t oA, oB;           // octa repeat filter
-  int oc1, oc2;              // octa: the spaces ending the last two words processed (start - 1 before any)
-  int start;                 // the round's first word start
-  int pbg, pdg, pxg;         // emissions from these numbers on are in the slot, not the LDS rings
-};
-constexpr int kInfOff = 0x7FFFFFFF;
-
-// Base emissions of a base hit as (tote adds, index into the adds table) (LinearizeAll :927-964)
-__device__ __forceinline__ void base_adds_idx(const DevTables& T, uint32_t qb, uint32_t q2b, uint32_t ind, uint64_t& l1,
-                                              uint64_t& l2, uint32_t& i1, uint32_t& i2) {
-  const DevTbl* lb = &T.quad;
-  uint32_t base = qb;
-  if (ind & 0x80000000u) {
-    lb = &T.quad2;
-    base = q2b;
-    ind &= ~0x80000000u;
-  }
-  l2 = 0;
-  i2 = 0;
-  if (ind < lb->size_one) {
-    l1 = adds_at(*lb, ind);
-    i1 = base + ind;
-  } else {
-    ind += ind - lb->size_one;
-    l1 = adds_at(*lb, ind);
-    l2 = adds_at(*lb, ind + 1);
-    i1 = base + ind;
-    i2 = base + ind + 1;
-    if (!(l1 >> 63)) {
-      l1 = l2;
-      i1 = i2;
-      l2 = 0;
-    }
-  }
-}
-
-// An emission's offset / adds index, from its ring or (spilled) from the slot.
-__device__ __forceinline__ int pb_off_at(const Slot& S, const Smem& s, const Inc& R, int i) {
-  return i >= R.pbg ? (int)gld(&S.be_off[i]) : (int)s.pb_off[i & (kPB - 1)];
-}
-__device__ __forceinline__ int pd_off_at(const Slot& S, const Smem& s, const Inc& R, int i) {
-  return i >= R.pdg ? (int)gld(&S.d_off[i]) : (int)s.pd_off[i & (kPD - 1)];
-}
-__device__ __forceinline__ int px_off_at(const Slot& S, const Smem& s, const Inc& R, int i) {
-  return i >= R.pxg ? (int)gld(&S.x_off[i]) : (int)s.px_off[i & (kPX - 1)];
-}
-__device__ __forceinline__ uint32_t* be_idx(Slot& S) { return reinterpret_cast<uint32_t*>(S.be_add); }
-
-// The three tote adds of an emission into the chunk tote (ProcessProbV2Tote, cldutil.cc:128-138)
-__device__ __forceinline__ void tote_add(Smem& s, uint64_t a) {
-  const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
-  if (k1) atomicAdd(&s.tote[k1], ((uint32_t)(a >> 8) & 0xFF) | 0x10000u);
-  if (k2) atomicAdd(&s.tote[k2], ((uint32_t)(a >> 24) & 0xFF) | 0x10000u);
-  if (k3) atomicAdd(&s.tote[k3], ((uint32_t)(a >> 40) & 0xFF) | 0x10000u);
-}
-
-// Adds to chunk c's tote the pending base emissions below bt and the pending
-// delta / distinct emissions at offsets <= thr (a prefix of each ring: their
-// offsets never decrease); the boost ring keeps the last four distinct ones.
-__device__ __forceinline__ void inc_add(const uint64_t* __restrict__ adds, Slot& S, Smem& s, Inc& R, int bt, int thr,
-                                        int rs, int lane) {
-  int nd = 0, nx = 0;
-  for (int i0 = R.pd_lo; i0 < R.ed; i0 += 64) {
-    const int i = i0 + lane;
-    const int c = __popcll(__ballot(i < R.ed && pd_off_at(S, s, R, i) <= thr));
-    nd += c;
-    if (c < 64) break;
-  }
-  for (int i0 = R.px_lo; i0 < R.ex; i0 += 64) {
-    const int i = i0 + lane;
-    const int c = __popcll(__ballot(i < R.ex && px_off_at(S, s, R, i) <= thr));
-    nx += c;
-    if (c < 64) break;
-  }
-  const int nB = bt - R.pb_lo, tot = nB + nd + nx;
-  if (tot <= 0) return;
-  if (nB > 0) R.clo = min(R.clo, ufl(pb_off_at(S, s, R, R.pb_lo)));
-  if (nd > 0) R.clo = min(R.clo, ufl(pd_off_at(S, s, R, R.pd_lo)));
-  if (nx > 0) R.clo = min(R.clo, ufl(px_off_at(S, s, R, R.px_lo)));
-  R.cgr += nB;
-  for (int t0 = 0; t0 < tot; t0 += 64) {
-    const int t = t0 + lane;
-    uint32_t idx = 0;
-    int xu = -1;
-    if (t < nB) {
-      const int i = R.pb_lo + t;
-      idx = i >= R.pbg ? gld(be_idx(S) + i) : s.pb_idx[i & (kPB - 1)];
-    } else if (t < nB + nd) {
-      const int i = R.pd_lo + t - nB;
-      idx = i >= R.pdg ? gld(&S.d_ind[i]) : s.pd_idx[i & (kPD - 1)];
-    } else if (t < tot) {
-      xu = t - nB - nd;
-      const int i = R.px_lo + xu;
-      idx = i >= R.pxg ? gld(&S.x_ind[i]) : s.px_idx[i & (kPX - 1)];
-    }
-    const uint64_t a = t < tot ? gld(adds + idx) : 0ull;
-    if (xu >= 0 && xu >= nx - kMaxBoosts) s.xlast[xu - (nx - kMaxBoosts)] = a;
-    tote_add(s, a);
-  }
-  if (nx > 0) {                        // AddDistinctBoost2 (scoreonescriptspan.cc:112-121), oldest first
-    wsync();
-    if (lane < kMaxBoosts) {
-      const uint64_t v = lane < kMaxBoosts - nx ? s.ring[rs][lane + nx] : s.xlast[lane];
-      s.ring[rs][lane] = v;
-    }
-  }
-  R.pb_lo = bt;
-  R.pd_lo += nd;
-  R.px_lo += nx;
-}
-
-// Chunk c is complete: ScoreBoosts (scoreonescriptspan.cc:125-152), the top two
-// keys (SetChunkSummary reads two of CurrentTopThreeKeys' three), kept in lane
-// c for the round's summaries; the tote is cleared for chunk c + 1.
-__device__ __forceinline__ void inc_finalize(Smem& s, Inc& R, int rs, int lane, int& ck1, int& ck2, int& cs1, int& cs2,
-                                             int& cgr) {
-  wsync();
-  if (lane < 2 * kMaxBoosts) {
-    const uint64_t a = lane < kMaxBoosts ? s.ring[rs][lane] : (s.has_pri ? s.pri_add[rs][lane - kMaxBoosts] : 0ull);
-    tote_add(s, a);
-  }
-  wsync();
-  if (s.has_pri) {                     // the prior whacks zero their key's score (ZeroPSLang :39-42)
-    const int wk = lane < 4 ? s.pri_wk[rs][lane] : 0;
-    if (wk) atomicAnd(&s.tote[wk], 0xFFFF0000u);
-    wsync();
-  }
-  const uint4 v4 = reinterpret_cast<const uint4*>(s.tote)[lane];
-  const bool inuse = ((v4.x | v4.y | v4.z | v4.w) >> 16) != 0;
-  const uint32_t cand[4] = {v4.x & 0xFFFF, v4.y & 0xFFFF, v4.z & 0xFFFF, v4.w & 0xFFFF};
-  int key3[2] = {-1, -1};
-  uint32_t sc3[2] = {0, 0};
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    uint32_t best = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = lane * 4 + i;
-      const bool taken = key == key3[0];
-      const uint32_t comp = (inuse && !taken) ? ((cand[i] + 1) << 8) | (uint32_t)(255 - key) : 0u;
-      best = comp > best ? comp : best;
-    }
-    best = wave::wmax(best);
-    if (best) {
-      key3[r] = 255 - (int)(best & 0xFF);
-      sc3[r] = (best >> 8) - 1;
-    }
-  }
-  if (lane == R.c) {
-    ck1 = key3[0]; ck2 = key3[1];
-    cs1 = key3[0] >= 0 ? (int)sc3[0] : 0;
-    cs2 = key3[1] >= 0 ? (int)sc3[1] : 0;
-    cgr = R.cgr;
-  }
-  if (lane == 0) s.lo[R.c] = R.clo == kInfOff ? kInf : (uint32_t)R.clo;
-  wsync();
-  reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
-  wsync();
-  ++R.c;
-  R.clo = kInfOff;
-  R.cgr = 0;
-}
-
-// Scores every chunk of the round that can be scored now.
-__device__ __forceinline__ void inc_drain(const uint64_t* __restrict__ adds, Slot& S, Smem& s, Inc& R, int rs, int lane,
-                                          int& ck1, int& ck2, int& cs1, int& cs2, int& cgr) {
-  for (;;) {
-    if (R.qdone && R.c >= R.K) return;
-    int Ec = -1;                                   // entry number closing chunk c (kInfOff: the last chunk)
-    if (R.qdone) Ec = s.Eq[R.c] == 0xFFFF ? kInfOff : (int)s.Eq[R.c];
-    else if (R.nb >= kChunksizeQuads * R.c + 2 * kChunksizeQuads) Ec = kChunksizeQuads * (R.c + 1);
-    const bool fin = Ec >= 0 && (Ec == kInfOff ? R.qdone : (Ec - 2 < R.eb || R.qdone));
-    int bt, thr;
-    if (fin) {
-      thr = (Ec != kInfOff && Ec - 2 < R.eb) ? ufl(pb_off_at(S, s, R, Ec - 2)) : kInfOff;   // theta_c
-      bt = Ec == kInfOff ? R.eb : min(R.eb, Ec - 1);
-    } else {                                       // the part of chunk c no hit count can move
-      const int t15 = R.Eprev + 13;                // base emission of entry E_{c-1} + 15
-      bt = min(R.eb, R.Eprev + 14);
-      thr = R.eb > t15 ? ufl(pb_off_at(S, s, R, t15)) : kInfOff;
-    }
-    inc_add(adds, S, s, R, bt, thr, rs, lane);
-    if (!fin || !(R.odone || R.ofront > thr)) return;
-    inc_finalize(s, R, rs, lane, ck1, ck2, cs1, cs2, cgr);
-    R.Eprev = Ec;
-  }
-}
-
-// One block of GetQuadHits (cldutil.cc:315-405): up to nq chain entries from
-// c0; their base emissions join the ring.  The 1000th hit ends the round (qdone).
-__device__ __forceinline__ void inc_quad_block(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int nch, int& c0,
-                                               Inc& R, uint32_t qb, uint32_t q2b, bool& ok, int lane) {
-  if (R.pbg == kInfOff && R.eb - R.pb_lo + 128 > kPB - kRingSlack) R.pbg = R.eb;   // the ring is full: spill
-  const int i0 = c0, iend = min(nch, i0 + 64);
-  const uint8_t* text = win_text(win, sm, ufl(S.chain[i0]) - 1, ufl(S.chain[iend - 1]) + 24, ok, lane);
-  if (!ok) return;
-  const int i = i0 + lane;
-  bool hit = false;
-  uint32_t hv = 0, ind = 0;
-  int p = 0;
-  if (i < iend) {
-    p = S.chain[i];
-    int e = p;
-    e += adv_but_space(text[e]);
-    e += adv_but_space(text[e]);
-    e += adv_but_space(text[e]);
-    e += adv_but_space(text[e]);
-    hv = quad_hash_v2(text + p, e - p);
-    const uint32_t probs = quad_probe(T.quad, T.quad2, hv, ind);
-    hit = probs != 0;
-  }
-  // the "not one of the last two hits" filter (quad_round)
-  const uint32_t A = R.qA, B = R.qB;
-  const uint64_t hm = __ballot(hit);
-  const uint64_t hb = hm & lanemask_lt(lane);
-  const int q1 = hb ? topbit(hb) : -1;
-  const uint64_t hb2 = q1 > 0 ? (hb & lanemask_lt(q1)) : 0ull;
-  const int q2 = hb2 ? topbit(hb2) : -1;
-  const uint32_t h1 = shfl32(hv, q1 < 0 ? lane : q1), h2 = shfl32(hv, q2 < 0 ? lane : q2);
-  const uint32_t a = q1 < 0 ? A : h1;
-  const uint32_t bb = q1 < 0 ? B : (q2 < 0 ? A : h2);
-  const uint64_t cm = __ballot(hit && (hv == a || hv == bb));
-  uint64_t keep = hm;
-  uint32_t nA, nB;
-  if (cm) {
-    const int f = __builtin_ctzll(cm);
-    keep = hm & lanemask_lt(f);
-    uint32_t xA = rdlu(a, f), xB = rdlu(bb, f);
-    for (uint64_t r = hm & ~lanemask_lt(f); r; r &= r - 1) {
-      const int l = __builtin_ctzll(r);
-      const uint32_t v = rdlu(hv, l);
-      if (v == xA || v == xB) continue;
-      xB = xA;
-      xA = v;
-      keep |= 1ull << l;
-    }
-    nA = xA;
-    nB = xB;
-  } else if (hm) {
-    const int t1 = topbit(hm);
-    nA = rdlu(hv, t1);
-    const uint64_t r2 = hm & ~(1ull << t1);
-    nB = r2 ? rdlu(hv, topbit(r2)) : A;
-  } else {
-    nA = A;
-    nB = B;
-  }
-  const int kc = __popcll(keep);
-  int lastl = 64;
-  if (R.nb + kc >= kMaxScoringHits) {
-    lastl = nth_bit(keep, kMaxScoringHits - R.nb - 1);
-    keep &= mask_le(lastl);
-  }
-  const bool kept = (keep >> lane) & 1;
-  R.nb += __popcll(keep);
-  {
-    uint64_t l1 = 0, l2 = 0;
-    uint32_t x1 = 0, x2 = 0;
-    if (kept) base_adds_idx(T, qb, q2b, ind, l1, l2, x1, x2);
-    const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
-    const int o = R.eb + excl_scan(c, lane);
-    R.eb = rdl(o + c, 63);
-    if (R.pbg == kInfOff) {
-      if (l1 >> 63) {
-        sm.pb_off[o & (kPB - 1)] = (uint16_t)p;
-        sm.pb_idx[o & (kPB - 1)] = x1;
-      }
-      if (l2 >> 63) {
-        sm.pb_off[(o + 1) & (kPB - 1)] = (uint16_t)p;
-        sm.pb_idx[(o + 1) & (kPB - 1)] = x2;
-      }
-    } else {
-      if (l1 >> 63) {
-        S.be_off[o] = (uint16_t)p;
-        be_idx(S)[o] = x1;
-      }
-      if (l2 >> 63) {
-        S.be_off[o + 1] = (uint16_t)p;
-        be_idx(S)[o + 1] = x2;
-      }
-    }
-  }
-  if (lastl < 64) {
-    c0 = i0 + lastl + 1;
-    R.qdone = true;
-  } else {
-    c0 = iend;
-    R.qA = nA;
-    R.qB = nB;
-    if (c0 >= nch) R.qdone = true;
-  }
-  R.qpos = c0 < nch ? (int)ufl(S.chain[c0]) : tb;
-  if (R.qdone) R.next = R.qpos;
-  if (R.pbg != kInfOff) gsync();       // spilled emissions are read back by other lanes
-  wsync();
-}
-
-// One block of GetOctaHits (cldutil.cc:416-533): the words from j0 that end
-// below `bound`, at most 64 and what the rings can take; the caps (1000 delta /
-// 999 distinct hits) end the round's words (odone).  Returns false if no word
-// could be taken.
-__device__ __forceinline__ bool inc_octa_block(const DevTables& T, Win& win, Smem& sm, Slot& S, int nsp, int& j0, Inc& R,
-                                               int bound, uint32_t dob, uint32_t xob, bool& ok, int lane) {
-  if (j0 >= nsp) return false;
-  if (R.pdg == kInfOff && R.ed - R.pd_lo + 64 > kPD - kRingSlack) R.pdg = R.ed;       // a full ring: spill
-  if (R.pxg == kInfOff && R.ex - R.px_lo + 128 > kPX - kRingSlack) R.pxg = R.ex;
-  const int jl = min(nsp, j0 + 64) - 1;
-  const uint8_t* text = win_text(win, sm, R.oc1, min((int)ufl(S.wsp[jl]), bound) + 8, ok, lane);
-  if (!ok) return false;
-  const int j = j0 + lane;
-  const int ej = j <= jl ? (int)S.wsp[j] : kInfOff;
-  const bool v = j <= jl && ej < bound;
-  const uint64_t vm = __ballot(v);
-  if (!vm) return false;
-  const int nv = __popcll(vm);
-  const int e1 = (int)wave::wshr1((uint32_t)ej, (uint32_t)R.oc1);          // wsp[j - 1]
-  const int e2 = (int)wave::wshr1((uint32_t)e1, (uint32_t)R.oc2);          // wsp[j - 2]
-  int a = R.start, pws = R.start, e = 0;
-  uint64_t wh = 0;
-  if (v) {
-    e = ej;
-    a = e1 + 1;
-    pws = e2 + 1;
-    int we = a, q = a, cc = 0;
-    while (q < e) {
-      ++cc;
-      q += utf8_len(text[q]);
-      if (cc <= 8) we = q;
-      else break;
-    }
-    wh = octa_hash40(text + a, we - a);
-  }
-  const uint64_t A = R.oA, B = R.oB;
-  const uint64_t h1 = wave::wshr1_64(wh), h2 = wave::wshr1_64(h1);
-  const uint64_t pa = lane >= 1 ? h1 : A;
-  const uint64_t pb = lane >= 2 ? h2 : (lane == 1 ? A : B);
-  const uint64_t cm = __ballot(v && (wh == pa || wh == pb));
-  uint64_t keep = vm;
-  uint32_t tlo = (uint32_t)pa, thi = (uint32_t)(pa >> 32);    // pair partner = previous kept word
-  uint64_t nA, nB;
-  if (cm) {
-    const int f = __builtin_ctzll(cm);
-    keep = vm & lanemask_lt(f);
-    uint64_t xA = rdl64(pa, f), xB = rdl64(pb, f);
-    for (int l = f; l < nv; ++l) {
-      const uint64_t hv = rdl64(wh, l);
-      if (hv == xA || hv == xB) continue;
-      if (lane == l) {
-        tlo = (uint32_t)xA;
-        thi = (uint32_t)(xA >> 32);
-      }
-      xB = xA;
-      xA = hv;
-      keep |= 1ull << l;
-    }
-    nA = xA;
-    nB = xB;
-  } else {
-    nA = rdl64(wh, nv - 1);
-    nB = nv >= 2 ? rdl64(wh, nv - 2) : A;
-  }
-  uint32_t pp = 0, xp = 0, dp = 0;
-  if ((keep >> lane) & 1) {
-    const uint64_t tph = ((uint64_t)thi << 32) | tlo;
-    if (tph != 0 && tph != wh) pp = octa_lookup(T.distinctocta, pair_hash(tph, wh));
-    xp = octa_lookup(T.distinctocta, wh);
-    dp = octa_lookup(T.deltaocta, wh);
-  }
-  const uint32_t xm = ~T.distinctocta.key_mask, dmk = ~T.deltaocta.key_mask;
-  const uint64_t apx = pp ? adds_at(T.distinctocta, pp & xm) : 0ull;
-  const uint64_t axp = xp ? adds_at(T.distinctocta, xp & xm) : 0ull;
-  const uint64_t adp = dp ? adds_at(T.deltaocta, dp & dmk) : 0ull;
-  const int cx = (pp != 0) + (xp != 0), cd = (dp != 0);
-  const int exs = excl_scan(cx, lane), eds = excl_scan(cd, lane);
-  const uint64_t capm =
-      __ballot(v && (R.nx + exs + cx >= kMaxScoringHits - 1 || R.nd + eds + cd >= kMaxScoringHits));
-  const int cut = capm ? __builtin_ctzll(capm) : 64;
-  {
-    const bool in = lane <= cut;
-    const int mx = in ? (int)(apx >> 63) + (int)(axp >> 63) : 0, md = in ? (int)(adp >> 63) : 0;
-    int ox = R.ex + excl_scan(mx, lane);
-    const int od = R.ed + excl_scan(md, lane);
-    R.ex = rdl(ox + mx, 63);
-    R.ed = rdl(od + md, 63);
-    const bool gx = R.pxg != kInfOff, gd = R.pdg != kInfOff;
-    if (in && (apx >> 63)) {
-      if (gx) { S.x_off[ox] = (uint16_t)pws; S.x_ind[ox] = xob + (pp & xm); }
-      else { sm.px_off[ox & (kPX - 1)] = (uint16_t)pws; sm.px_idx[ox & (kPX - 1)] = xob + (pp & xm); }
-      ++ox;
-    }
-    if (in && (axp >> 63)) {
-      if (gx) { S.x_off[ox] = (uint16_t)a; S.x_ind[ox] = xob + (xp & xm); }
-      else { sm.px_off[ox & (kPX - 1)] = (uint16_t)a; sm.px_idx[ox & (kPX - 1)] = xob + (xp & xm); }
-    }
-    if (in && (adp >> 63)) {
-      if (gd) { S.d_off[od] = (uint16_t)a; S.d_ind[od] = dob + (dp & dmk); }
-      else { sm.pd_off[od & (kPD - 1)] = (uint16_t)a; sm.pd_idx[od & (kPD - 1)] = dob + (dp & dmk); }
-    }
-  }
-  const int lastl = cut < 64 ? cut : nv - 1;
-  R.nx += rdl(exs + cx, lastl);
-  R.nd += rdl(eds + cd, lastl);
-  if (cut < 64) {
-    R.odone = true;
-    R.ofront = kInfOff;
-  } else {
-    R.oc2 = nv >= 2 ? rdl(ej, nv - 2) : R.oc1;
-    R.oc1 = rdl(ej, nv - 1);
-    R.oA = nA;
-    R.oB = nB;
-    R.ofront = rdl(a, nv - 1);          // the next word's pair hit is at this word's start
-    j0 += nv;
-  }
-  if ((R.pdg & R.pxg) != kInfOff) gsync();
-  wsync();
-  return true;
-}
-
-// SetChunkSummary for the round's K chunks, one lane per chunk, then their
-// DocTote adds in chunk order (SummaryBufferToDocTote :305-315).
-template <bool D>
-__device__ __forceinline__ void round_summaries(const DevTables& T, Smem& s, int ulscript, int K, int dummy_off, int ck1,
-                                                int ck2, int cs1, int cs2, int cgr, int lane) {
-  int lo = 0, hi = 0, lang1 = 0, lang2 = 0, rd = 0, rsc = 0;
-  if (lane < K) {
-    const uint32_t lo_k = s.lo[lane];
-    lo = lo_k == kInf ? dummy_off : (int)lo_k;
-    hi = dummy_off;
-    if (lane + 1 < K && s.lo[lane + 1] != kInf) hi = (int)s.lo[lane + 1];
-    const uint64_t* kt = T.keytab + 256 * (uint32_t)ulscript;
-    const uint64_t i1 = gld(kt + (uint8_t)ck1), i2 = gld(kt + (uint8_t)ck2);
-    lang1 = (int)(i1 & 0xFFFF); lang2 = (int)(i2 & 0xFFFF);
-    const int len = hi - lo;
-    int actual = 0;
-    if (len > 0) actual = (int)((uint32_t)cs1 << 10) / len;
-    const int expected = (int16_t)(uint16_t)(i1 >> 32);
-    const uint16_t s1 = (uint16_t)cs1, s2 = (uint16_t)cs2, grams = (uint16_t)cgr;
-    rd = (uint8_t)reliability_delta(s1, s2, grams);
-    const int c1 = (int)((i1 >> 16) & 0xFFFF);
-    if (c1 != 0 && c1 == (int)((i2 >> 16) & 0xFFFF)) rd = 100;
-    rsc = (uint8_t)reliability_expected(actual, expected);
-    cs1 = s1; cs2 = s2; cgr = grams;
-  }
-  for (int k = 0; k < K; ++k) {
-    const int l1 = rdl(lang1, k), l0 = rdl(lo, k), h0 = rdl(hi, k), sc = rdl(cs1, k);
-    const int r1 = rdl(rd, k), r2 = rdl(rsc, k);
-    if (lane == 0) {
-      const uint16_t bytes = (uint16_t)(h0 - l0);
-      if (k < kMaxSummaries) s.dt.add((uint16_t)l1, bytes, sc, r1 < r2 ? r1 : r2);
-      if (D && s.dbg) {
-        uint32_t* o = s.dbg + 1 + s.dbg_pos;
-        const uint32_t v[18] = {'C', (uint32_t)l0, (uint32_t)h0, (uint32_t)l1, (uint32_t)rdl(lang2, k),
-                                (uint32_t)sc, (uint32_t)rdl(cs2, k), (uint32_t)rdl(cgr, k), (uint32_t)r1,
-                                (uint32_t)r2, 0, 0, 0, 0, 0, 0, 0, (uint32_t)K};
-        for (int i = 0; i < 18; ++i) o[i] = v[i];
-        s.dbg_pos += 18;
-        s.dbg[0] = s.dbg_pos;
-      }
-    }
-  }
-  wsync();
-}
-
-// The rounds of a quad span (ScoreQuadScriptSpan :1231-1277), chunk at a time.
-// Returns false when a ring or the text window cannot take a block (the
-// document then goes to k_general).
-template <bool D>
-__device__ __forceinline__ bool score_quad(const DevTables& T, Slot& S, Smem& s, Win& win, int tb, int ulscript, int start,
-                                           int nch, int nsp, int lane) {
-  const uint64_t* adds = T.compat.adds;                   // the per-GPU adds table (k_build_adds)
-  const uint32_t qb = (uint32_t)(T.quad.adds - adds), q2b = (uint32_t)(T.quad2.adds - adds);
-  const uint32_t dob = (uint32_t)(T.deltaocta.adds - adds), xob = (uint32_t)(T.distinctocta.adds - adds);
-  const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
-  const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
-  long long t = (D && s.prof) ? (long long)clock64() : 0;
-  reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
-  int c0 = 0, j0 = 0, off = 1;
-  bool ok = true;
-  (void)start;
-  while (off < tb) {
-    Inc R;
-    R.nb = R.eb = R.nd = R.nx = R.ed = R.ex = 0;
-    R.c = 0; R.K = 0; R.Eprev = 0;
-    R.pb_lo = R.pd_lo = R.px_lo = 0;
-    R.qA = R.qB = 0; R.oA = R.oB = 0;
-    R.pbg = R.pdg = R.pxg = kInfOff;
-    R.qdone = c0 >= nch;
-    R.odone = false;
-    R.qpos = c0 < nch ? (int)ufl(S.chain[c0]) : tb;
-    R.next = R.qdone ? tb : 0;
-    R.start = off + (ufl(win_text(win, s, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
-    if (!ok) return false;
-    R.oc1 = R.oc2 = R.start - 1;
-    R.ofront = R.start;
-    // linear entry 1: the default language's seed at the round's lowest offset (LinearizeAll :885-891)
-    wsync();
-    if (lane == 0) tote_add(s, seed);
-    R.clo = off;
-    R.cgr = 1;
-    int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane` of the round: top keys, scores, grams
-    bool planned = false;
-    for (;;) {
-      if (R.qdone && !planned) {                            // ChunkAll's plan from the final hit count
-        if (lane == 0) {
-          int K = 0;
-          if (R.nb <= 0) {
-            s.Eq[0] = 0xFFFF;
-            K = 1;
-          } else {
-            int left = R.nb, e = 0;
-            while (left > 0) {
-              int blen = kChunksizeQuads;
-              if (left < kChunksizeQuads + (kChunksizeQuads >> 1)) blen = left;
-              else if (left < 2 * kChunksizeQuads) blen = (left + 1) >> 1;
-              e += blen;
-              s.Eq[K++] = (uint16_t)e;
-              left -= blen;
-            }
-            s.Eq[K - 1] = 0xFFFF;
-          }
-        }
-        int K = 1;
-        if (R.nb > 0) {
-          int left = R.nb;
-          K = 0;
-          while (left > 0) {
-            int blen = kChunksizeQuads;
-            if (left < kChunksizeQuads + (kChunksizeQuads >> 1)) blen = left;
-            else if (left < 2 * kChunksizeQuads) blen = (left + 1) >> 1;
-            ++K;
-            left -= blen;
-          }
-        }
-        R.K = K;
-        planned = true;
-        wsync();
-      }
-      inc_drain(adds, S, s, R, rs, lane, ck1, ck2, cs1, cs2, cgr);
-      if constexpr (D) mark(s, lane, 7, t);
-      if (R.qdone && R.c >= R.K) break;
-      const int bound = R.qdone ? R.next + 1 : R.qpos;     // words ending there are in the round for sure
-      if (!R.odone && j0 < nsp && (int)ufl(S.wsp[j0]) < bound) {
-        if (!inc_octa_block(T, win, s, S, nsp, j0, R, bound, dob, xob, ok, lane)) return false;
-        if constexpr (D) mark(s, lane, 6, t);
-        continue;
-      }
-      if (R.qdone) {
-        if (R.odone) return false;                           // (cannot happen: every chunk is complete)
-        R.odone = true;
-        R.ofront = kInfOff;
-        continue;
-      }
-      inc_quad_block(T, win, s, tb, S, nch, c0, R, qb, q2b, ok, lane);
-      if (!ok) return false;
-      if constexpr (D) mark(s, lane, 5, t);
-    }
-    // the next round's words start after `next` (a chain position, never a space)
-    {
-      const int lim = R.next + 1;
-      int lo = j0, hi = nsp;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((int)ufl(S.wsp[mid]) < lim) lo = mid + 1;
-        else hi = mid;
-      }
-      j0 = lo;
-    }
-    round_summaries<D>(T, s, ulscript, R.K, R.next, ck1, ck2, cs1, cs2, cgr, lane);
-    off = R.next;
-  }
-  return true;
-}
-
-#endif  // LNG_INC
 
 __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, bool octa, int lane) {
   if (!s.dbg) return;
@@ -2713,9 +2071,6 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
   if (nch < 0) return false;
   if constexpr (D) trace(tr, lane, doc, 11, nch);
   if constexpr (D) mark(s, lane, 4, t);
-#if LNG_INC
-  return score_quad<D>(T, S, s, win, tb, ulscript, start, nch, nsp, lane);
-#endif
   int c0 = 0, j0 = 0;
   while (off < tb) {
     int nb, nd, nx;

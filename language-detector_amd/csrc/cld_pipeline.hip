@@ -1965,6 +1965,18 @@ __device__ void write_result(cld_result* r, const Extract& x, int summary, bool 
   *r = o;
 }
 
+// A document the kernels could not score: no language, summary CLD_LANG_FAILED.
+__device__ void mark_failed(const DevTables& T, cld_result* r) {
+  for (int k = 0; k < 3; ++k) {
+    r->lang3[k] = (uint16_t)T.unknown_lang;
+    r->percent3[k] = 0;
+    r->normalized3[k] = 0.0;
+  }
+  r->summary_lang = (uint16_t)CLD_LANG_FAILED;
+  r->is_reliable = 0;
+  r->text_bytes = 0;
+}
+
 // DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (HTML mode when
 // !plain, the ApplyHints priors when given, a ResultChunkVector when vo;
 // cflags: the caller's public flags, kCLDFlagScoreAsQuads / kCLDFlagBestEffort);

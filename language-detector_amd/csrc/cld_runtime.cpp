@@ -33,13 +33,23 @@
 
 namespace {
 
+// Inside a loop that has enqueued DMA on the caller's buffers: record the
+// error and leave the loop, so the drain after it still runs.
+#define HIP_BRK(x)                                                          \
+  if (hipError_t e_ = (x); e_ != hipSuccess) {                              \
+    fprintf(stderr, "cld_mi355x: %s failed: %s (%s:%d)\n", #x,              \
+            hipGetErrorString(e_), __FILE__, __LINE__);                     \
+    rc = CLD_EFAULT;                                                        \
+    break;                                                                  \
+  }
+
 #define HIP_OK(x)                                                           \
   do {                                                                      \
     hipError_t e_ = (x);                                                    \
     if (e_ != hipSuccess) {                                                 \
       fprintf(stderr, "cld_mi355x: %s failed: %s (%s:%d)\n", #x,            \
               hipGetErrorString(e_), __FILE__, __LINE__);                   \
-      return CLD_EIO;                                                       \
+      return CLD_EFAULT;                                                    \
     }                                                                       \
   } while (0)
 
@@ -337,7 +347,6 @@ struct Device {
   uint8_t* d_arena = nullptr;
   uint64_t stride = 0;
   int lanes = 0;
-  int front = 0;              // 0: wavefront-per-document kernel, 1: lane-per-document (CLD_FRONT=lane)
   uint8_t* d_slots = nullptr; // k_long per-wave slots (0 slots: CLD_LONG=0, long documents go to k_general)
   int n_slots = 0;
   uint32_t* d_requeue2 = nullptr;
@@ -349,6 +358,7 @@ struct Device {
   uint32_t* h_trace = nullptr;  // CLD_TRACE=1: pinned host progress words, 4 per k_long wave
   uint32_t* d_dbg = nullptr;    // CLD_DEBUG_DOC=i: k_long dumps document i's rounds/chunks
   uint32_t dbg_doc = 0xFFFFFFFFu;
+  uint32_t fault_doc = 0xFFFFFFFFu;   // CLD_FAULT_DOC=i (tests): batch document i fails in k_long and k_general
   double trace_timeout = 0;
   unsigned long long* d_prof = nullptr;   // per-stage cycle sums (CLD_PROFILE_STAGES=1)
   uint32_t* d_counters = nullptr;
@@ -541,7 +551,6 @@ int init_device(Device* d) {
   lanes = std::max(64, (lanes / 64) * 64);
   while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
   d->lanes = lanes;
-  if (const char* e = getenv("CLD_FRONT")) d->front = strcmp(e, "lane") == 0 ? 1 : 0;
   if (const char* e = getenv("CLD_PROFILE_STAGES")) {
     if (atoi(e) > 0) {
       HIP_OK(hipMalloc(&d->d_prof, 16 * sizeof(unsigned long long)));
@@ -561,6 +570,7 @@ int init_device(Device* d) {
     HIP_OK(hipMemset(d->d_slots, 0, (uint64_t)n_slots * slot));   // predictor epochs start at 0
     d->n_slots = n_slots;
   }
+  if (const char* e = getenv("CLD_FAULT_DOC")) d->fault_doc = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("CLD_DEBUG_DOC")) {
     d->dbg_doc = (uint32_t)atoll(e);
     HIP_OK(hipMalloc(&d->d_dbg, 64u << 20));
@@ -635,12 +645,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
-  if (d->front == 1)
-    HIP_OK(cld_launch_short(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, special, sp_list, sp_ctr,
-                            cflags, s));
-  else
-    HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
-                           sp_ctr, cflags, priors, hbuf, hflag, s));
+  HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
+                         sp_ctr, cflags, priors, hbuf, hflag, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
@@ -650,14 +656,15 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
-                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, s));
+                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, d->fault_doc,
+                           s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, s));
+                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
   } else {
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, cflags, s));
+                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, cflags, d->fault_doc, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -828,6 +835,10 @@ struct HostReg {
   ~HostReg() { release(); }
 };
 
+// run_host_shard's "some documents failed" return (k_general counted and
+// marked them); internal, never returned to a caller.
+constexpr int kDocsFailed = 1;
+
 int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
                    const uint8_t* special = nullptr, const uint32_t* priors = nullptr, bool html = false) {
   std::lock_guard<std::mutex> lk(d->mu);
@@ -897,17 +908,17 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
       }
     }
     // upload (after the slot's previous kernels stopped reading its device buffers)
-    HIP_OK(hipStreamWaitEvent(d->up_stream, h.comp, 0));
-    if (bytes) HIP_OK(hipMemcpyAsync(h.d_in, src_in, bytes, hipMemcpyHostToDevice, d->up_stream));
-    HIP_OK(hipMemcpyAsync(h.d_offs, src_offs, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->up_stream));
+    HIP_BRK(hipStreamWaitEvent(d->up_stream, h.comp, 0))
+    if (bytes) HIP_BRK(hipMemcpyAsync(h.d_in, src_in, bytes, hipMemcpyHostToDevice, d->up_stream))
+    HIP_BRK(hipMemcpyAsync(h.d_offs, src_offs, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, d->up_stream))
     if (special) {
-      HIP_OK(hipMemcpyAsync(h.d_sp, h.h_sp, m, hipMemcpyHostToDevice, d->up_stream));
+      HIP_BRK(hipMemcpyAsync(h.d_sp, h.h_sp, m, hipMemcpyHostToDevice, d->up_stream))
       if (priors)
-        HIP_OK(hipMemcpyAsync(h.d_pri, h.h_pri, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, d->up_stream));
+        HIP_BRK(hipMemcpyAsync(h.d_pri, h.h_pri, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, d->up_stream))
     }
-    HIP_OK(hipEventRecord(h.up, d->up_stream));
+    HIP_BRK(hipEventRecord(h.up, d->up_stream))
     // kernels: buffer base biased so that the caller's offsets index it directly
-    HIP_OK(hipStreamWaitEvent(d->stream, h.up, 0));
+    HIP_BRK(hipStreamWaitEvent(d->stream, h.up, 0))
     const uint8_t* kbuf = h.d_in - base;
     if (flags & kPrepFlags) {
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
@@ -917,14 +928,14 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
                    (special && priors) ? h.d_pri : nullptr, flags, base, (special && html) ? bytes : 0);
     }
     if (rc) break;
-    HIP_OK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, d->stream));
-    HIP_OK(hipEventRecord(h.comp, d->stream));
+    HIP_BRK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, d->stream))
+    HIP_BRK(hipEventRecord(h.comp, d->stream))
     // download
-    HIP_OK(hipStreamWaitEvent(d->down_stream, h.comp, 0));
-    HIP_OK(hipMemcpyAsync(out_pinned ? dst : h.h_out, h.d_out, m * sizeof(cld_result), hipMemcpyDeviceToHost,
-                          d->down_stream));
-    HIP_OK(hipEventRecord(h.down, d->down_stream));
+    HIP_BRK(hipStreamWaitEvent(d->down_stream, h.comp, 0))
+    HIP_BRK(hipMemcpyAsync(out_pinned ? dst : h.h_out, h.d_out, m * sizeof(cld_result), hipMemcpyDeviceToHost,
+                          d->down_stream))
+    HIP_BRK(hipEventRecord(h.down, d->down_stream))
     h.pending_n = m;
     h.pending_dst = out_pinned ? nullptr : dst;
     h.busy = true;
@@ -934,7 +945,11 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     int r = deliver(h);
     if (rc == CLD_OK) rc = r;
   }
-  HIP_OK(hipStreamSynchronize(d->stream));
+  // an upload or a kernel enqueued before an error in the loop may still read
+  // the caller's (possibly registered) buffers: all three streams drain
+  // before the HostReg objects above unregister them
+  for (hipStream_t q : {d->up_stream, d->stream, d->down_stream})
+    if (hipStreamSynchronize(q) != hipSuccess && rc == CLD_OK) rc = CLD_EFAULT;
   if (rc) return rc;
   if (d->d_dbg) {             // debug: write the dumped words to $CLD_DEBUG_OUT
     uint32_t cnt = 0;
@@ -961,8 +976,44 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     st.short_ms += x; st.long_ms += y; st.general_ms += z;
   }
   d->stats_pending = false;
-  return err ? CLD_EIO : CLD_OK;
+  return err ? kDocsFailed : CLD_OK;
 }
+
+// Documents the kernels could not score come back marked CLD_LANG_FAILED
+// (k_general, kDocsFailed above); each is redone alone, so one bad document
+// never costs the batch.  CLD_EIO only if one still fails on its own.
+int run_host_shard_isolating(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out,
+                             uint32_t flags, const uint8_t* special = nullptr, const uint32_t* priors = nullptr,
+                             bool html = false) {
+  int rc = run_host_shard(d, buf, offs, n, out, flags, special, priors, html);
+  if (rc != kDocsFailed) return rc;
+  bool left = false;
+  for (size_t i = 0; i < n; ++i) {
+    if (out[i].summary_lang != CLD_LANG_FAILED) continue;
+    const int r = run_host_shard(d, buf, offs + i, 1, out + i, flags, special ? special + i : nullptr,
+                                 priors ? priors + 16 * i : nullptr, html);
+    if (r != CLD_OK) {
+      left = true;
+      if (r != kDocsFailed) return r;          // a device error, not a document
+    }
+  }
+  if (left) fprintf(stderr, "cld_mi355x: documents without a result after a retry (summary CLD_LANG_FAILED)\n");
+  return left ? CLD_EIO : CLD_OK;
+}
+
+// Multi-GPU fan-out: large pageable caller buffers are page-locked once by
+// the dispatching thread, so the shards (whose offset and result ranges share
+// boundary entries and pages) find them pinned instead of each registering an
+// overlapping range.
+struct FanoutReg {
+  HostReg b, o, r;
+  FanoutReg(size_t ndev, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out) {
+    if (ndev < 2 || offs[n] - offs[0] < register_min_bytes()) return;
+    if (!host_pinned(buf + offs[0]) && b.take(buf + offs[0], offs[n] - offs[0]) && !host_pinned(offs))
+      o.take(offs, (n + 1) * sizeof(uint64_t));
+    if (!host_pinned(out)) r.take(out, n * sizeof(cld_result));
+  }
+};
 
 // ResultChunkVector mode on one device: documents in sub-batches (the
 // kernel is the exact sequential pipeline; no overlap needed), each
@@ -991,7 +1042,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   // pays that tail once -- 32 MB sub-batches held C5 to 76K docs/s, one launch
   // for the 95 MB batch runs it at 208K.  256 MB of text takes ~5 GB of pool.
   const size_t kSub = 1024 * 1024;
-  static const uint64_t kSubBytes = (getenv("CLD_VEC_SUB_MB") ? (uint64_t)atoi(getenv("CLD_VEC_SUB_MB")) : 256ull) << 20;
+  static const uint64_t kSubBytes0 = (getenv("CLD_VEC_SUB_MB") ? (uint64_t)atoi(getenv("CLD_VEC_SUB_MB")) : 256ull) << 20;
+  uint64_t kSubBytes = kSubBytes0;   // halved while the device cannot hold a sub-batch's pool
   // test hook: CLD_VEC_POOL_SMALL=1 makes first-pass pool regions too small so
   // the retry below runs (tests/test_gpu_vector.py)
   static const bool small_pool = getenv("CLD_VEC_POOL_SMALL") && atoi(getenv("CLD_VEC_POOL_SMALL")) > 0;
@@ -1068,8 +1120,13 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     std::vector<int32_t> nch;
     std::vector<cld_chunk> ch;
     if (int rc = sub(buf, offs + a, m, out + a, special ? special + a : nullptr, priors ? priors + 16 * a : nullptr,
-                     false, nch, ch))
+                     false, nch, ch)) {
+      if (rc == CLD_ENOMEM && m > 1 && kSubBytes > (1u << 20)) {   // smaller sub-batches, same documents
+        kSubBytes /= 2;
+        continue;
+      }
       return rc;
+    }
     // A document whose vector did not fit runs again, alone with the others
     // that did not, with 8x the pool region; the rest of the batch is kept.
     std::vector<size_t> bad;
@@ -1280,20 +1337,31 @@ int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches
   return CLD_OK;
 }
 
+// Estimated kernel cost of one document, in units of 10 ps, from this tree's
+// measured per-document times on one MI355X:
+//   <= 256 B   k_wave, one wavefront per document: 4.8 ms per 1 M tweets
+//   longer     k_long: 84.4 ms per 100 K 16 KB pages = 0.0515 ns/B, plus
+//              ~25 ns per document (C5's long half: 51.3 ms)
+// so a 16 KB page weighs as much as ~180 tweets, not the ~110 that bytes +
+// 64 per document said.
+static uint64_t doc_cost(uint64_t len) { return len <= (uint64_t)kWaveCap ? 480 : (len * 41) / 8 + 2500; }
+
 int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts) {
   if (!offsets || !cuts || nshards < 1) return CLD_EINVAL;
-  const uint64_t total = (offsets[n] - offsets[0]) + 64ull * n;
+  // Contiguous ranges of equal estimated kernel cost (doc_cost above): the
+  // long-document kernel costs more per byte than the wavefront kernel, so a
+  // byte split would leave the shard with the long pages last to finish.
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += doc_cost(offsets[i + 1] - offsets[i]);
   cuts[0] = 0;
-  cuts[nshards] = n;
+  uint64_t acc = 0;
+  size_t i = 0;
   for (int k = 1; k < nshards; ++k) {
-    uint64_t target = total * (uint64_t)k / (uint64_t)nshards;
-    size_t lo = cuts[k - 1], hi = n;
-    while (lo < hi) {
-      size_t mid = (lo + hi) / 2;
-      if ((offsets[mid] - offsets[0]) + 64ull * mid < target) lo = mid + 1; else hi = mid;
-    }
-    cuts[k] = lo;
+    const uint64_t target = (uint64_t)((unsigned __int128)total * (uint64_t)k / (uint64_t)nshards);
+    while (i < n && acc < target) acc += doc_cost(offsets[i + 1] - offsets[i]), ++i;
+    cuts[k] = i;
   }
+  cuts[nshards] = n;
   return CLD_OK;
 }
 
@@ -1332,6 +1400,19 @@ void cld_shutdown(void) {
   g_init_rc = CLD_ENODEV;
 }
 
+namespace {
+// A device error of any shard wins over CLD_EIO (some documents without a
+// result, every other one complete).
+int first_error(const std::vector<int>& rcs) {
+  int partial = CLD_OK;
+  for (int r : rcs) {
+    if (r == CLD_EIO) partial = CLD_EIO;
+    else if (r) return r;
+  }
+  return partial;
+}
+}  // namespace
+
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_result* out, uint32_t flags) {
   if ((flags & ~(kPrepFlags | kPublicFlags)) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
@@ -1345,16 +1426,18 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   // Shard by byte count (+ a per-document weight) at document boundaries.
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
-  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, flags);
+  if (ndev == 1) return run_host_shard_isolating(g_devs[0], buf, offsets, n, out, flags);
+  FanoutReg reg(ndev, buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
-    th.emplace_back([&, k] { rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], flags); });
+    th.emplace_back([&, k] {
+      rcs[k] = run_host_shard_isolating(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], flags);
+    });
   }
   for (auto& t : th) t.join();
-  for (int r : rcs) if (r) return r;
-  return CLD_OK;
+  return first_error(rcs);
 }
 
 int cld_hint_priors(const uint8_t* doc, size_t len, int is_plain_text, const cld_hints* hints, int16_t* priors14,
@@ -1444,19 +1527,19 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
   const size_t ndev = g_devs.size();
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
-  if (ndev == 1) return run_host_shard(g_devs[0], buf, offsets, n, out, cf, sp, pr, html);
+  if (ndev == 1) return run_host_shard_isolating(g_devs[0], buf, offsets, n, out, cf, sp, pr, html);
+  FanoutReg reg(ndev, buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
   for (size_t k = 0; k < ndev; ++k) {
     if (cut[k + 1] == cut[k]) continue;
     th.emplace_back([&, k] {
-      rcs[k] = run_host_shard(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], cf,
+      rcs[k] = run_host_shard_isolating(g_devs[k], buf, offsets + cut[k], cut[k + 1] - cut[k], out + cut[k], cf,
                               sp ? sp + cut[k] : nullptr, pr ? pr + 16 * cut[k] : nullptr, html);
     });
   }
   for (auto& t : th) t.join();
-  for (int r : rcs) if (r) return r;
-  return CLD_OK;
+  return first_error(rcs);
 }
 
 int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, const cld_hints* hints,
@@ -1505,7 +1588,7 @@ int cld_detect_batch_vec(const uint8_t* buf, const uint64_t* offsets, size_t n, 
     if (at < chunk_cap)
       memcpy(chunks + at, vs[k].data(), std::min<uint64_t>(vs[k].size(), chunk_cap - at) * sizeof(cld_chunk));
   }
-  return total > chunk_cap ? CLD_ENOMEM : partial;
+  return total > chunk_cap ? CLD_ENOSPC : partial;
 }
 
 int cld_detect_batch_device(int device, const uint8_t* d_buf, const uint64_t* d_offsets, size_t n,
@@ -1676,8 +1759,10 @@ int cld_convert_data_file(const char* data_file, const char* base_cldt, const ch
 // document as one batch; the others wait for their slot to be filled.
 const char* detect_language(const char* text) {
   if (cld_init(nullptr, 0) != CLD_OK) {
+    // a deployment without a usable GPU (or tables): there is no CPU fallback,
+    // and wrapper.h has no error channel, so the process stops loudly
     fprintf(stderr, "cld_mi355x: detect_language: GPU runtime unavailable\n");
-    abort();   // no CPU fallback: fail loudly
+    abort();
   }
   Pending p;
   p.text = text ? text : "";
@@ -1700,8 +1785,22 @@ const char* detect_language(const char* text) {
       std::vector<cld_result> res(batch.size());
       int rc = cld_detect_batch((const uint8_t*)bytes.data(), offs.data(), batch.size(), res.data(), 0);
       if (rc != CLD_OK) {
-        fprintf(stderr, "cld_mi355x: detect_language batch failed (%d)\n", rc);
-        abort();
+        // One caller's document never costs the others their answers.  After
+        // CLD_EIO only the documents marked CLD_LANG_FAILED lack a result;
+        // after any other error every document is retried on its own.  A
+        // document that still fails gets the reference's answer for "no
+        // language" (UNKNOWN -> "en", compact_lang_det.cc:91-93) and a line
+        // on stderr: wrapper.h has no error channel to carry it.
+        for (size_t i = 0; i < batch.size(); ++i) {
+          if (rc == CLD_EIO && res[i].summary_lang != CLD_LANG_FAILED) continue;
+          const uint64_t one[2] = {offs[i], offs[i + 1]};
+          int r = cld_detect_batch((const uint8_t*)bytes.data(), one, 1, &res[i], 0);
+          if (r != CLD_OK || res[i].summary_lang == CLD_LANG_FAILED) {
+            fprintf(stderr, "cld_mi355x: detect_language: no result for a document (%d); answering \"en\"\n", r);
+            std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+            res[i].summary_lang = (uint16_t)g_tab.meta.unknown_language;
+          }
+        }
       }
       lk.lock();
       for (size_t i = 0; i < batch.size(); ++i) { batch[i]->res = res[i]; batch[i]->done = true; }

@@ -32,14 +32,6 @@
 namespace cld {
 namespace wave {
 
-// -DWAVE_STOP=k (instruction-count A/B only, wrong results): the wave ends
-// (s_endpgm) at stop point k of its document's first span, so PMC differences
-// between variants price each stage (tools/sessions/r3c_stages.sh).
-#ifdef WAVE_STOP
-#define WAVE_STOP_AT(k) if (WAVE_STOP == (k)) __builtin_amdgcn_endpgm()
-#else
-#define WAVE_STOP_AT(k) (void)0
-#endif
 
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t uflu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -631,7 +623,6 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   if (nws > C::NB) return -1;
   if (lane < C::QM) s.qmark[lane] = 0u;
   wsync();
-  WAVE_STOP_AT(31);
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) {
     if (r * 64 >= nws) break;
@@ -658,7 +649,6 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
   }
   if (n > C::NB) return -1;
   wsync();
-  WAVE_STOP_AT(32);
   int cp[C::NR];
 #pragma unroll
   for (int r = 0; r < C::NR; ++r) cp[r] = s.qchn[r * 64 + lane];
@@ -683,7 +673,6 @@ __device__ int quad_hits(const DevTables& T, Smem<CAP>& s, int limit, int& nb, i
       hit = quad_probe(T.quad, T.quad2, hv, ind) != 0;
       pr = ind;
     }
-    WAVE_STOP_AT(33);
     // Assume every hit is kept: then a hit's two predecessors are the previous
     // hit lanes; from the first hit that equals one of them, resolve in order.
     const uint64_t hm = __ballot(hit);
@@ -1002,7 +991,6 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     if (lp) { s.x_off[o] = off; s.x_ind[o] = lp; }
     ex = rdl(o + (lp != 0), 63);
   }
-  WAVE_STOP_AT(51);
   // chunk plan from the base-hit count (ChunkAll :978-1031)
   int K = 0;
   if (nb <= 0) {
@@ -1096,7 +1084,6 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
   const int nboost = pri ? 2 * kMaxBoosts : kMaxBoosts;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
   wsync();
-  WAVE_STOP_AT(52);
   for (int k = 0; k < K; ++k) {
     const int seedn = k == 0 ? 1 : 0;
     const int bs = s.st[0][k], nB = s.st[0][k + 1] - bs, ds = s.st[1][k], nD = s.st[1][k + 1] - ds;
@@ -1180,7 +1167,6 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     }
     wsync();
   }
-  WAVE_STOP_AT(53);
   // SetChunkSummary (scoreonescriptspan.cc:60-96) for every chunk at once, one
   // lane per chunk; the DocTote adds then run in chunk order on lane 0
   int sum_lang = 0, sum_bytes = 0, sum_rel = 0;
@@ -1209,7 +1195,6 @@ __device__ bool score_round(const DevTables& T, Smem<CAP>& s, int ulscript, bool
     cs1 = s1;
   }
   const int nsum = K < kMaxSummaries ? K : kMaxSummaries;
-  WAVE_STOP_AT(54);
   for (int k = 0; k < nsum; ++k) {
     const int l1 = rdl(sum_lang, k), by = rdl(sum_bytes, k), sc = rdl(cs1, k), rl = rdl(sum_rel, k);
     dt_add_wave(s.dt, l1, by, sc, rl, lane);
@@ -1351,16 +1336,13 @@ __device__ __forceinline__ double rdl_f64(double v, int l) {
 __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
                                int lane, bool best_effort = false) {
   SlotRegs r = load_slots(dt, lane);
-  WAVE_STOP_AT(61);
   refine_close_pairs_regs(T, r, lane);
   sort3_regs(r, lane);
   double ns;
-  WAVE_STOP_AT(62);
   DocSum x = extract_regs(T, r, total, lane, ns);
   const bool good = final || total <= 256 || (x.reliable && x.pct[0] >= 70) ||
                     (x.reliable && x.pct[0] + x.pct[1] >= 93);
   if (!good) return 0;
-  WAVE_STOP_AT(63);
   if (!best_effort) {
     // RemoveUnreliableLanguages (:997-1101) only when some slot is unreliable
     const bool unrel = lane < 24 && r.key != kUnusedKey && r.val != 0 && r.rl / (r.val ? r.val : 1) < 41;
@@ -1425,7 +1407,6 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
   }
   if (!load_document<CAP>(T, g, L, s, lane, hf)) return false;
   mark(0);
-    WAVE_STOP_AT(0);
   if (lane == 0) s.dt.init();
   if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
   wsync();
@@ -1434,11 +1415,9 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
     int ulscript = 0;
     int tb = next_span<CAP>(T, s, L, next, ulscript, lane);
     mark(1);
-    WAVE_STOP_AT(1);
     if (tb == 0) break;
     tb = lower_span<CAP>(T, s, tb, lane);
     mark(2);
-    WAVE_STOP_AT(2);
     if (tb < 0) return false;
     int rt = rtype_of(T, ulscript);
     if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
@@ -1455,17 +1434,14 @@ __device__ bool detect(const DevTables& T, const uint8_t* __restrict__ g, int L,
       } else {
         endo = quad_hits<CAP>(T, s, tb, nb, lane);
         mark(3);
-        WAVE_STOP_AT(3);
         if (endo < 0) return false;
         if (!octa_hits<CAP>(T, s, endo, nd, nx, lane)) return false;
         mark(4);
-        WAVE_STOP_AT(4);
       }
       if (endo < tb) return false;     // a second round would be needed (never for short documents)
       int rsel;
       if (1 < tb && !score_round<CAP>(T, s, ulscript, cjk, nb, nd, nx, endo, rsel, lane, pri)) return false;
       mark(5);
-      WAVE_STOP_AT(5);
     }
     total += tb;
   }

@@ -1,8 +1,9 @@
 """Document sharding across ranks (one process per GPU).
 
 Documents are independent, so a corpus is split into
-contiguous, byte-balanced document ranges (cld_plan_shards, the same split
-cld_detect_batch uses across the GPUs of one process).  Each rank scores its
+contiguous document ranges of equal estimated kernel cost (cld_plan_shards,
+the same split cld_detect_batch uses across the GPUs of one process; the cost
+model is doc_costs below).  Each rank scores its
 own range on its own GPU; nothing is exchanged on the hot path.  Only the
 40-byte result records travel back to the root rank, once, after scoring.
 """
@@ -11,8 +12,16 @@ import numpy as np
 import cld_amd
 
 
+def doc_costs(offsets):
+    """Estimated kernel cost per document, cld_plan_shards' model (include/cld_mi355x.h):
+    480 units for a document of <= 256 bytes (k_wave), 41/8 per byte + 2500 for a
+    longer one (k_long); units of 10 ps of one MI355X."""
+    ln = np.diff(np.asarray(offsets, dtype=np.uint64)).astype(np.int64)
+    return np.where(ln <= 256, 480, (ln * 41) // 8 + 2500)
+
+
 def shard_bounds(offsets, rank, world):
-    """[lo, hi) document range of `rank` out of `world` (byte + per-doc weight balanced)."""
+    """[lo, hi) document range of `rank` out of `world` (estimated-cost balanced)."""
     cuts = cld_amd.plan_shards(offsets, world)
     return int(cuts[rank]), int(cuts[rank + 1])
 

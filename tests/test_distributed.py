@@ -57,12 +57,16 @@ def test_gloo_sharded_equals_single_process(world):
 def test_plan_shards_cover_and_balance():
     import cld_amd
     import corpus
+    import sharding
     buf, offs = corpus.c5(20000)
     for world in (1, 2, 3, 8, 64):
         cuts = cld_amd.plan_shards(offs, world)
         assert cuts[0] == 0 and cuts[-1] == len(offs) - 1 and np.all(np.diff(cuts) >= 0)
-        w = (offs[cuts[1:]] - offs[cuts[:-1]]).astype(np.int64) + 64 * np.diff(cuts)
-        assert w.max() <= w.sum() / world + int(np.max(np.diff(offs))) + 64
+        # every shard carries 1/world of the estimated kernel cost, within one document
+        c = np.concatenate([[0], np.cumsum(sharding.doc_costs(offs))])
+        w = c[cuts[1:]] - c[cuts[:-1]]
+        assert w.max() <= c[-1] / world + sharding.doc_costs(offs).max()
+        assert w.min() >= c[-1] / world - sharding.doc_costs(offs).max() or world > len(offs) - 1
     # degenerate inputs
     z = np.zeros(1, np.uint64)
     assert list(cld_amd.plan_shards(z, 4)) == [0, 0, 0, 0, 0]

@@ -1,5 +1,6 @@
 """GPU path vs the reference CLD2 itself (no oracle in between), on the GPU
-box: oracle/_ref/librefcld2.so is the reference's own sources built in its
+box, with the synthetic Q1 tables and again with the product's shipped Q0
+(conftest.ref_tables): oracle/_ref/librefcld2.so is the reference's own sources built in its
 dynamic-data mode (oracle/refcld), and it travels with the tree like the
 product's library.  Tables: the same CLDT the GPU loads, written as a
 cld2_data_file00 and read by the reference's loader.  A missing checker, or
@@ -17,10 +18,9 @@ FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "nor
 
 
 @pytest.fixture(scope="module")
-def ref():
-    import refcld
-    refcld.verify_build()
-    return refcld.instance(os.environ["CLD_MI355X_TABLES"])
+def ref(ref_tables):
+    """The reference on the tables of this round of the module (Q1, then the shipped Q0)."""
+    return ref_tables[1]
 
 
 def same(got, want, what):
@@ -50,7 +50,7 @@ def test_gpu_equals_reference_html_hints(gpu, ref):
 
 
 @pytest.mark.parametrize("flags", [0x0100, 0x4000, 0x4100], ids=["score_as_quads", "best_effort", "both"])
-def test_gpu_equals_reference_with_flags(gpu, ref, golden, flags):
+def test_gpu_equals_reference_with_flags(gpu, ref, ref_tables, golden, flags):
     """CLD2's result-affecting flags (compact_lang_det.h:343-349) through every
     batch entry point: the wave / long kernels (cld_detect_batch), the hinted
     and HTML paths (cld_detect_batch_ex), each equal to the reference called
@@ -65,8 +65,9 @@ def test_gpu_equals_reference_with_flags(gpu, ref, golden, flags):
     same(got, want, "batch flags %#x" % flags)
     same(gpu.detect_batch_ex(buf=buf, offsets=offs, flags=flags), want, "batch_ex flags %#x" % flags)
     base = gpu.detect_batch(buf=buf, offsets=offs)
-    assert ((got["summary_lang"] != base["summary_lang"]) | (got["is_reliable"] != base["is_reliable"]) |
-            (got["lang3"] != base["lang3"]).any(axis=1)).sum() >= 10
+    if ref_tables[0] == "q1":                # (with Q0 most Latin documents have no language to move)
+        assert ((got["summary_lang"] != base["summary_lang"]) | (got["is_reliable"] != base["is_reliable"]) |
+                (got["lang3"] != base["lang3"]).any(axis=1)).sum() >= 10
     from test_gpu_html_hints import random_hints
     hb, ho = corpus.html(500, seed=510)
     n = len(ho) - 1
