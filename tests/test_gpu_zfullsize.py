@@ -31,6 +31,7 @@ def ub_docs(buf, offs):
     return ub
 
 
+@pytest.mark.timeout(900)                     # (the first one may wait for its corpus generator)
 @pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
 def test_full_size_equals_reference(gpu, ref_tables, name):
     label, ref = ref_tables
