@@ -35,11 +35,25 @@ size_t cld_vec_work_bytes();
 // ResultChunkVector mode: all n documents in k_general_vec; document i builds
 // its vector in pool[pool_off[i] .. pool_off[i+1]) and writes its size (or -1)
 // to n_chunks[i]; counters[kCtrDequeue2] must be zero.
+// count (nullable): run only the *count documents listed in `order` (the
+// parallel vec path's hand-ons), else all n (order: optional permutation).
 hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
                                   const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
-                                  hipStream_t s);
+                                  const uint32_t* count, hipStream_t s);
+// ResultChunkVector mode on the parallel kernels: k_route_vec lists plain
+// documents under counters[kCtrRequeue] (long_list) and HTML pages under
+// counters[kCtrRequeue2] (gen_list); k_long<VEC> then scores the first list
+// with one VecSlot per resident wave (vslots: n_slots * cld_vec_slot_bytes())
+// and appends what it cannot reproduce to requeue2 (= gen_list).
+size_t cld_vec_slot_bytes();
+hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counters, uint32_t* long_list,
+                                uint32_t* gen_list, hipStream_t s);
+hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
+                               uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
+                               cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s);
 hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
                                  const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
 // special (nullable): per-document kSpecial* bits; HTML documents are appended

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __r
                                                    const uint32_t* __restrict__ priors,
                                                    cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
                                                    int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ order,
-                                                   uint32_t cflags) {
+                                                   uint32_t cflags, const uint32_t* __restrict__ count) {
   const DevTables& T = *Tp;
 #if GEN_LANES_PER_WAVE == 1
   if (threadIdx.x != 0) return;
@@ -119,9 +119,12 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __r
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
 #endif
   VecWork& w = *reinterpret_cast<VecWork*>(arena + (uint64_t)lane * stride);
+  // count (nullable): the list `order` holds *count documents (the ones the
+  // parallel vec kernel handed on), else every document 0..n-1
+  const uint32_t total = count ? __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (uint32_t)n;
   for (;;) {
     const uint32_t k = atomicAdd(&counters[kCtrDequeue2], 1u);
-    if (k >= (uint32_t)n) break;                 // every lane reaches this exit
+    if (k >= total) break;                       // every lane reaches this exit
     const uint32_t i = order ? order[k] : k;     // longest documents first
     const uint64_t a = offs[i], b = offs[i + 1];
     VecOut& vo = w.vo;
@@ -142,6 +145,12 @@ __global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __r
     else atomicAdd(&counters[kCtrError], 1u);
   }
 }
+
+// Vec-mode routing: plain documents to k_long<VEC>'s list, HTML pages to the
+// sequential kernel's (one atomic per wavefront each).
+__global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restrict__ special,
+                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ long_list,
+                                                  uint32_t* __restrict__ gen_list);
 
 // Compaction of the per-document pool regions into document order.
 __global__ __launch_bounds__(256) void k_vec_gather(const cld_chunk* __restrict__ pool,
@@ -224,6 +233,15 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t* ctr, uint32_t* 
   if (pred) list[base + __popcll(m & wave::lanemask_lt(lane))] = val;
 }
 
+__global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restrict__ special,
+                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ long_list,
+                                                  uint32_t* __restrict__ gen_list) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool html = i < n && special && (special[i] & kSpecialHtml);
+  wave_append(html, &counters[kCtrRequeue2], gen_list, (uint32_t)i, nullptr);
+  wave_append(i < n && !html, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
+}
+
 // Routing before k_wave, one thread per document: HTML documents to
 // k_general's list, documents longer than k_wave's CAP to k_long's, each with
 // one atomic per wavefront instead of one per document (a batch of 100K pages
@@ -254,7 +272,7 @@ __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs
 #ifndef LNG_WPS
 #define LNG_WPS 4
 #endif
-template <int WPB, bool DIAG>
+template <int WPB, bool DIAG, bool VEC>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __restrict__ Tp,
                                                   const uint8_t* __restrict__ buf,
                                                   const uint64_t* __restrict__ offs,
@@ -267,7 +285,9 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   const uint8_t* __restrict__ special,
                                                   const uint32_t* __restrict__ priors,
                                                   const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag,
-                                                  uint32_t fault_doc) {
+                                                  uint32_t fault_doc, uint8_t* __restrict__ vslots,
+                                                  cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
+                                                  int32_t* __restrict__ n_chunks) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -299,9 +319,29 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     wave::wsync();
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const bool rw = (spi & kSpecialRewritten) != 0;   // a rewritten HTML page (cld_html.hip)
-    if (exact && len <= (uint64_t)lng::kDocCap)
-      passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
-                                 (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr);
+    if constexpr (VEC) {
+      // ResultChunkVector mode (cld_detect_batch_vec): the vector goes to the
+      // document's pool region; a vector that outgrows it reports -1 (the host
+      // redoes the document with a larger region)
+      lng::VecState V;
+      V.vs = reinterpret_cast<lng::VecSlot*>(vslots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::VecSlot));
+      const uint64_t reg = pool_off[i + 1] - pool_off[i];
+      V.v = pool + pool_off[i];
+      V.cap = reg > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)reg;
+      V.n = 0;
+      V.over = false;
+      V.doc = buf + a;
+      V.L = (int)len;
+      V.last_off = V.last_bytes = V.last_lang = 0;
+      if (exact && len <= (uint64_t)lng::kDocCap)
+        passes = lng::detect<DIAG, true>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
+                                         (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, &V);
+      if (lane == 0 && passes >= 1 && passes <= 3) n_chunks[i] = V.over ? -1 : V.n;
+    } else {
+      if (exact && len <= (uint64_t)lng::kDocCap)
+        passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
+                                   (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr);
+    }
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (i == fault_doc) passes = -lng::kWhyLength;   // fault injection (CLD_FAULT_DOC): on to k_general
@@ -468,13 +508,35 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off
   if (trace || dbg || prof)
-    hipLaunchKernelGGL((cld::k_long<kLongWPB, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL((cld::k_long<kLongWPB, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+size_t cld_vec_slot_bytes() { return sizeof(cld::lng::VecSlot); }
+
+hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counters, uint32_t* long_list,
+                                uint32_t* gen_list, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cld::k_route_vec, dim3((n + 255) / 256), dim3(256), 0, s, n, special, counters, long_list,
+                     gen_list);
+  return hipGetLastError();
+}
+
+hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
+                               uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
+                               cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
+  if (n_slots < kLongWPB) return hipErrorInvalidValue;
+  dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
+  hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
+                     requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, nullptr,
+                     nullptr, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks);
   return hipGetLastError();
 }
 
@@ -485,7 +547,7 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
                                   cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
                                   const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
                                   const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
-                                  hipStream_t s) {
+                                  const uint32_t* count, hipStream_t s) {
   if (n <= 0) return hipSuccess;
 #if GEN_LANES_PER_WAVE == 1
   dim3 grid(lanes), block(64);
@@ -493,7 +555,7 @@ hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, cons
   dim3 grid(lanes / 64), block(64);
 #endif
   hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
-                     priors, pool, pool_off, n_chunks, order, cflags);
+                     priors, pool, pool_off, n_chunks, order, cflags, count);
   return hipGetLastError();
 }
 

@@ -159,6 +159,41 @@ struct alignas(16) Smem {
 };
 static_assert(sizeof(Smem) <= 10240, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
 
+// ------------------------------------------------ ResultChunkVector (vec mode)
+// cld_detect_batch_vec runs k_long<.., VEC = true> over every plain document:
+// the same span, hit and scoring stages, plus what the reference's vector
+// needs (scoreonescriptspan.cc:389-548, 671-845; offsetmap.cc):
+//   * the span builder records, per byte of the span text, the document offset
+//     ScriptScanner::MapBack returns for it (omap): map2original_'s ops are
+//     Copy for letters, Delete + Insert(1) for a gap turned into one space
+//     (Copy(1) when the gap is one byte), Insert(4) for the pads; map2uplow_ is
+//     the identity because vec mode keeps documents whose lowering changes a
+//     character's length on the sequential kernel;
+//   * Repeats overwrite instead of cutting (CheapRepWordsInplaceOverwrite), so
+//     those offsets stay valid; Squeeze documents go to the sequential kernel;
+//   * per round, linear[] is materialised from the emission streams (rank =
+//     merge position, LinearizeAll's tie order) for SharpenBoundaries, whose
+//     BetterBoundary window scan runs across lanes; the sharpened chunk bytes
+//     feed the DocTote, as there;
+//   * SummaryBufferToVector / ItemToVector, the close-pair relabelling and
+//     FinishResultVector append to the document's region of the vector pool.
+constexpr int kLinCap = 1 + kEB + 2 * kHB + 1;        // seed + base + delta + distinct emissions + dummy
+struct VecSlot {                                       // per resident wave, HBM
+  uint32_t omap[kLB];                                  // span text position -> document offset
+  uint32_t lin_off[kLinCap];                           // the round's linear[]: offsets
+  uint64_t lin_add[kLinCap];                           //   langprobs as tote adds
+  int32_t vd[kLinCap];                                 // BetterBoundary: pslang0 - pslang1 score per entry
+};
+struct VecState {                                      // wave-uniform
+  VecSlot* vs;
+  cld_chunk* v;                                        // the document's region of the pool
+  int cap, n;
+  bool over;                                           // the vector outgrew its region
+  const uint8_t* doc;
+  int L;
+  int last_off, last_bytes, last_lang;                 // v[n - 1], mirrored
+};
+
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
 // 3 repeats, 4 word lists + quad chain, 5 quad hits, 6 octa/uni/bi hits,
 // 7 linearize/chunk/score.  Built with -DLNG_PROF_SUB, slots 0-5 instead split
@@ -565,8 +600,23 @@ __device__ __noinline__ int lower_tail(DevSM sm, const uint8_t* in, int ilen, ui
 // with NUL bytes (DocView), and the lowercaser stops at its lead byte: that
 // tail is lowered sequentially by lane 0, so text_bytes can even be < 1 there.
 // status: 1 span (returns its lowered text_bytes), 0 no span left, -1 re-queue.
+// First letter stop at or after y (the end of a gap the reference's
+// non-letter loop deletes), L if none; per lane.
+__device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
+  if (y >= L) return L;
+  int w = y >> 6;
+  uint64_t m = lsm[w] & (~0ull << (y & 63));
+  while (!m) {
+    if ((++w << 6) >= L) return L;
+    m = lsm[w];
+  }
+  const int r = (w << 6) + __builtin_ctzll(m);
+  return r < L ? r : L;
+}
+
+template <bool VEC = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
-                         int& status, int lane) {
+                         int& status, int lane, uint32_t* omap = nullptr) {
   lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
@@ -582,6 +632,13 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   }
   int ss = 0;                                    // the span script: read off q's lane in the first window
   if (lane == 0) lb[0] = ' ';
+  if constexpr (VEC) {
+    // map2original_ at the leading space (getonescriptspan.cc:835-848):
+    // Delete(offset) Delete(skip) Insert(1) maps it past the skipped bytes, to
+    // the first letter q; skip == 1 is a Copy(1) of the skipped byte; and
+    // Delete(1) Insert(1) (offset 1, skip 0) merges into Copy(1) of byte 0
+    if (lane == 0) omap[0] = (uint32_t)((q - next == 1) ? next : (q == 1 ? 0 : q));
+  }
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
   // software pipeline: while window w is processed, window w+1's property
@@ -670,6 +727,19 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     grow += olen > n ? olen - n : 0;
     const int tl = olen + ((act && (sep || hard_here)) ? 1 : 0);
     const int opre = excl_scan(tl, lane);
+    if constexpr (VEC) {
+      if (out_chr && olen != n) bad = 1;         // map2uplow_ not the identity: the sequential kernel maps it
+      if (out_chr)
+        for (int k = 0; k < olen; ++k) omap[lpos + opre + k] = (uint32_t)(x + k);   // Copy
+      if (act && (sep || hard_here)) {
+        // the run's ' ': Delete(gap) then Insert(1) maps it to the letter after
+        // the gap; a gap of one byte makes that a Copy(1) of the gap byte, no
+        // gap an Insert at the run end (:955-993)
+        const int from = sep ? x : x + n;
+        const int nl = next_stop(S.lsm, from, L);
+        omap[lpos + opre + olen] = (uint32_t)(nl - from >= 2 ? nl : from);
+      }
+    }
     if (out_chr)
       for (int k = 0; k < olen; ++k) lb[lpos + opre + k] = (uint8_t)(lw >> (8 * k));
     if (act && (sep || hard_here)) lb[lpos + opre + olen] = ' ';
@@ -693,6 +763,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     if ((w << 6) + 64 >= L) {                                         // end of document
       if (run && wmax((uint32_t)(cutx + 1)) == 0) {                 // (a cut character brings its own)
         if (lane == 0) lb[lpos] = ' ';
+        if (VEC && lane == 0) omap[lpos] = (uint32_t)L;              // Insert(1) at the document end
         ++lpos;
         ++put;
       }
@@ -717,6 +788,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     lpos -= 3;                                                        // text_bytes = filled - 3
   } else {
     for (int k = lane; k < 40; k += 64) lb[lpos + k] = k < 3 ? ' ' : 0;   // "   " (lowered pads), NULs
+    if (VEC && lane < 4) omap[lpos + lane] = (uint32_t)nxt;            // Insert(4): where the scan stopped
   }
   // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
   // spans near the 40 KB limit that also grow; re-queue those.
@@ -1027,6 +1099,10 @@ __device__ __forceinline__ bool squeeze_trigger(Slot& S, const uint8_t* text, bo
 // segment runs from a space (inclusive: its byte counts for the next word) to
 // the next space; at that space the bytes after the previous space, this space
 // included, are dropped if more than half of the segment was predicted.
+// OW (vec mode): CheapRepWordsInplaceOverwrite (:697-770) -- the same
+// segments and predictions, but a mostly-predicted segment's bytes before its
+// closing space become '.' and the text keeps its length.
+template <bool OW = false>
 __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* dst, int len, uint32_t& hcarry, uint32_t ep,
                          bool careful, bool& ok, int lane) {
   lane = wave::lane_here();
@@ -1072,6 +1148,26 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
   // copy pad bytes too: k_general takes that (malformed) document
   ok = carry == 0;
   if (!ok) return len;
+  if constexpr (OW) {
+    for (int w = 0; w < nw; ++w) {
+      const int x = (w << 6) + lane;
+      if (x < len) {
+        int ww = w;
+        uint64_t m = S.spm[w] & (~0ull << lane);
+        while (!m && ((ww + 1) << 6) < len) m = S.spm[++ww];
+        bool dot = false;
+        if (m) {
+          const int sp = __builtin_ctzll(m);
+          dot = ((S.delm[ww] >> sp) & 1) && !(ww == w && sp == lane);   // the closing space stays
+        }
+        dst[x] = dot ? (uint8_t)'.' : src[x];
+      }
+    }
+    if (dst != src)
+      for (int k = lane; k < 48; k += 64) dst[len + k] = src[len + k];   // pads as they are (:758-767)
+    gsync();
+    return len;
+  }
   int dpos = 0;
   for (int w = 0; w < nw; ++w) {
     const int x = (w << 6) + lane;
@@ -1787,6 +1883,96 @@ __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, i
   return (k == 0 ? 1 : 0) + nB + nD + nX + kMaxBoosts + (s.has_pri ? kMaxBoosts : 0);
 }
 
+// ---------------------------------------------------- vec mode helpers
+// GetLangScore (cldutil.cc:141-152) on a langprob's tote adds: the scores of
+// the keys equal to pslang.
+__device__ __forceinline__ int add_score(uint64_t a, uint32_t ps) {
+  int r = 0;
+  if ((uint32_t)(a & 0xFF) == ps) r += (int)((a >> 8) & 0xFF);
+  if ((uint32_t)((a >> 16) & 0xFF) == ps) r += (int)((a >> 24) & 0xFF);
+  if ((uint32_t)((a >> 32) & 0xFF) == ps) r += (int)((a >> 40) & 0xFF);
+  return r;
+}
+// ScriptScanner::MapBack (getonescriptspan.cc:1076-1078) for y in [0, text_bytes]
+__device__ __forceinline__ int vec_map_back(const VecState& V, int y) { return y < 0 ? 0 : (int)gld(V.vs->omap + y); }
+__device__ __forceinline__ void vec_store(VecState& V, int lane) {
+  if (lane == 0 && !V.over && V.n > 0) {
+    cld_chunk c;
+    c.offset = V.last_off;
+    c.bytes = V.last_bytes;
+    c.lang1 = (uint16_t)V.last_lang;
+    c.pad = 0;
+    V.v[V.n - 1] = c;
+  }
+}
+// ItemToVector (scoreonescriptspan.cc:323-360): extend the last item when the
+// language repeats (over any gap), else append
+__device__ __forceinline__ void vec_item(VecState& V, int lang, int off, int len, int lane) {
+  if (V.n > 0 && lang == V.last_lang) {
+    V.last_bytes = off + len - V.last_off;
+  } else {
+    if (V.n >= V.cap) {
+      V.over = true;
+      return;
+    }
+    ++V.n;
+    V.last_off = off;
+    V.last_bytes = len;
+    V.last_lang = lang;
+  }
+  vec_store(V, lane);
+}
+__device__ __forceinline__ uint64_t wmax64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const uint64_t t = shfl64(v, wave::lane_here() ^ o);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+// Entries of a sorted u16 stream <= o (le) or < o.
+__device__ __forceinline__ int count_upto(const uint16_t* a, int n, int o, bool le) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const int v = a[mid];
+    if (le ? v <= o : v < o) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// BetterBoundary (scoreonescriptspan.cc:671-720) across lanes: the window
+// sum at left end i is R(i) = d[i..i+3] - d[i+4..i+7]; the scan keeps the first
+// i with the largest R(i) > 0 among windows holding both a positive and a
+// negative d, and moves the boundary to i + 4.
+__device__ int better_boundary_w(VecSlot* vs, uint32_t ps0, uint32_t ps1, int lin0, int lin1, int lin2, int lane) {
+  if (lin2 - lin0 <= 8) return lin1;
+  for (int j = lin0 + lane; j < lin2; j += 64) {
+    const uint64_t a = vs->lin_add[j];
+    vs->vd[j] = add_score(a, ps0) - add_score(a, ps1);
+  }
+  gsync();
+  uint64_t best = 0;
+  for (int i = lin0 + lane; i < lin2 - 8; i += 64) {
+    int r = 0;
+    bool plus = false, minus = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int dv = vs->vd[i + k];
+      r += k < 4 ? dv : -dv;
+      plus |= dv > 0;
+      minus |= dv < 0;
+    }
+    if (plus && minus && r > 0) {
+      const uint64_t key = ((uint64_t)(uint32_t)r << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)i);
+      best = key > best ? key : best;
+    }
+  }
+  best = wmax64(best);
+  gsync();
+  return best ? (int)(0xFFFFFFFFu - (uint32_t)best) + 4 : lin1;
+}
+
 // ------------------------------------- linearize + chunk + score (one round)
 // LinearizeAll / ChunkAll / ScoreAllHits (scoreonescriptspan.cc:856-1031,
 // 208-302) without materialising linear[].  Linear order = the seed (offset
@@ -1797,9 +1983,9 @@ __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, i
 // entries and lands in the first chunk k with that count < E_k, i.e. with
 // o <= theta_k = be_off[E_k - 2].  Every chunk is therefore one contiguous
 // range of each stream.
-template <bool D>
+template <bool D, bool VEC = false>
 LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
-                            int lowest, int dummy_off, int lane, int eb, int ed, int ex) {
+                            int lowest, int dummy_off, int lane, int eb, int ed, int ex, VecState* V = nullptr) {
   lane = wave::lane_here();
   // The hit rounds (quad_round / octa_round / cjk_round) already turned their
   // nb / nd / nx hits into eb base, ed delta and ex distinct emissions (tote
@@ -1977,6 +2163,71 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     rsc = (uint8_t)reliability_expected(actual, expected);
     cs1 = s1; cs2 = s2; cgr = grams;
   }
+  const int Kv = K < kMaxSummaries ? K : kMaxSummaries;   // the summary buffer keeps this many
+  if constexpr (VEC) {
+    // linear[] of the round (LinearizeAll :856-975): the seed, then by offset
+    // with delta < distinct < base on ties, each stream in its own order; the
+    // dummy entry at the round end
+    VecSlot* vs = V->vs;
+    const int NL = 1 + eb + ed + ex;
+    if (lane == 0) {
+      vs->lin_off[0] = (uint32_t)lowest;
+      vs->lin_add[0] = seed;
+      vs->lin_off[NL] = (uint32_t)dummy_off;
+      vs->lin_add[NL] = 0;
+    }
+    for (int t = lane; t < eb; t += 64) {
+      const int o = S.be_off[t];
+      const int r = 1 + t + count_upto(S.d_off, ed, o, true) + count_upto(S.x_off, ex, o, true);
+      vs->lin_off[r] = (uint32_t)o;
+      vs->lin_add[r] = S.be_add[t];
+    }
+    for (int j = lane; j < ed; j += 64) {
+      const int o = S.d_off[j];
+      const int r = 1 + j + count_upto(S.x_off, ex, o, false) + count_upto(S.be_off, eb, o, false);
+      vs->lin_off[r] = (uint32_t)o;
+      vs->lin_add[r] = S.d_add[j];
+    }
+    for (int j = lane; j < ex; j += 64) {
+      const int o = S.x_off[j];
+      const int r = 1 + j + count_upto(S.d_off, ed, o, true) + count_upto(S.be_off, eb, o, false);
+      vs->lin_off[r] = (uint32_t)o;
+      vs->lin_add[r] = S.x_add[j];
+    }
+    gsync();
+    // chunk k's first linear entry (chunk_start): the seed and every earlier
+    // chunk's emissions come before it
+    int cst = 0;
+    if (lane > 0 && lane < K) cst = min(1 + (int)s.bst[lane] + (int)s.st[0][lane] + (int)s.st[1][lane], NL);
+    // SharpenBoundaries (:780-845), chunk after chunk; chunk i's new start
+    // moves its offset, and so the bytes of chunks i - 1 and i
+    int prior_linear = 0, prior_lang = rdl(lang1, 0);
+    for (int i = 1; i < Kv; ++i) {
+      const int this_lang = rdl(lang1, i), this_linear = rdl(cst, i);
+      if (this_lang == prior_lang) {
+        prior_linear = this_linear;
+        continue;
+      }
+      const int next_linear = i + 1 < Kv ? rdl(cst, i + 1) : NL;
+      if (same_close_set(T, prior_lang, this_lang)) {
+        prior_linear = this_linear;
+        prior_lang = this_lang;
+        continue;
+      }
+      const uint32_t ps0 = per_script_number(T, ulscript, prior_lang), ps1 = per_script_number(T, ulscript, this_lang);
+      const int better = better_boundary_w(vs, ps0, ps1, prior_linear, this_linear, next_linear, lane);
+      const int noff = (int)vs->lin_off[better];
+      if (lane == i) {
+        lo = noff;
+        cst = better;
+      }
+      prior_linear = better;
+      prior_lang = this_lang;
+    }
+    // bytes = the (sharpened) next start minus this one
+    const int nlo = __shfl(lo, lane + 1 < 64 ? lane + 1 : lane, 64);
+    if (lane < K) hi = lane + 1 < K ? nlo : dummy_off;
+  }
   for (int k = 0; k < K; ++k) {
     const int l1 = rdl(lang1, k), l0 = rdl(lo, k), h0 = rdl(hi, k), sc = rdl(cs1, k);
     const int r1 = rdl(rd, k), r2 = rdl(rsc, k);
@@ -1998,6 +2249,47 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     }
   }
   wsync();
+  if constexpr (VEC) {
+    // SummaryBufferToVector (:389-509), chunk after chunk
+    VecState& Vr = *V;
+    const int unk = (int)T.unknown_lang;
+    for (int i = 0; i < Kv; ++i) {
+      const int uoff = rdl(lo, i), ulen = rdl(hi, i) - uoff;
+      const int l1 = rdl(lang1, i), l2 = rdl(lang2, i), r1 = rdl(rd, i), r2 = rdl(rsc, i);
+      int moff = vec_map_back(Vr, uoff);
+      if (moff > 0) {
+        // trim back to a word start in the original text: at most 12 bytes,
+        // leaving 3 in the prior item; over bytes >= 0x41, plus one '"#@
+        const int prior_size = Vr.n > 0 ? Vr.last_bytes : 0;
+        int nlim = min(min(prior_size - 3, moff), 12);
+        const bool in = lane < nlim;
+        const uint8_t b = in ? gld(Vr.doc + moff - lane - 1) : (uint8_t)0;
+        const uint64_t stop = __ballot(in && b < 0x41);
+        int k = stop ? __builtin_ctzll(stop) : 0;
+        if (k < nlim) {
+          const uint32_t c = gld(Vr.doc + moff - k - 1);
+          if (c == '\'' || c == '"' || c == '#' || c == '@') ++k;
+        }
+        if (k > 0) {
+          Vr.last_bytes -= k;
+          vec_store(Vr, lane);
+          moff -= k;
+        }
+      }
+      const int mlen = vec_map_back(Vr, uoff + ulen) - moff;
+      int nl = l1;
+      bool delta_bad = r1 < 75, score_bad = r2 < 75;         // kUnreliablePercentThreshold
+      const int prior_lang = Vr.n > 0 ? Vr.last_lang : unk;
+      if (prior_lang == l1) delta_bad = false;
+      if (same_close_set(T, l1, prior_lang)) { nl = prior_lang; delta_bad = false; }
+      if (same_close_set(T, l1, l2) && prior_lang == l2) { nl = prior_lang; delta_bad = false; }
+      const int next_lang = i + 1 < Kv ? rdl(lang1, i + 1) : unk;   // NextChunkLang
+      if (delta_bad && prior_lang == l2 && next_lang == l2) { nl = prior_lang; delta_bad = false; }
+      if (delta_bad || score_bad) nl = unk;
+      vec_item(Vr, nl, moff, mlen, lane);
+    }
+    gsync();
+  }
   // the ring keeps the last four distinct langprobs
   if (lane == 0) {
     uint64_t r4[4];
@@ -2032,14 +2324,21 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
-template <bool D>
+template <bool D, bool VEC = false>
 __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, Win& win, int tb,
-                                           int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags) {
+                                           int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags,
+                                           VecState* V = nullptr) {
   int rt = rtype_of(T, ulscript);
   if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
   if (rt == RTypeNone || rt == RTypeOne) {
     if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
     wsync();
+    if constexpr (VEC) {
+      // JustOneItemToVector (:513-548): the span after its leading space
+      if (tb < 1) return false;                      // (a span of one cut character: the sequential kernel)
+      const int moff = vec_map_back(*V, 1);
+      vec_item(*V, default_language(T, ulscript), moff, vec_map_back(*V, tb) - moff, lane);
+    }
     return true;
   }
   if (tb <= 1) return true;
@@ -2056,7 +2355,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
       if constexpr (D) trace(tr, lane, doc, 21, next);
       if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
       if constexpr (D) mark(s, lane, 6, t);
-      score_round<D>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane, eb, edm, exm);
+      score_round<D, VEC>(T, S, s, ulscript, true, nb, nd, nx, off, next, lane, eb, edm, exm, V);
       if constexpr (D) mark(s, lane, 7, t);
       off = next;
     }
@@ -2085,7 +2384,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
     if constexpr (D) trace(tr, lane, doc, 14, (uint32_t)(nd << 16 | nx));
     if constexpr (D) dbg_round(S, s, off, next, nb, nd, nx, true, lane);
     if constexpr (D) mark(s, lane, 6, t);
-    score_round<D>(T, S, s, ulscript, false, nb, nd, nx, off, next, lane, eb, edm, exm);
+    score_round<D, VEC>(T, S, s, ulscript, false, nb, nd, nx, off, next, lane, eb, edm, exm, V);
     if constexpr (D) mark(s, lane, 7, t);
     off = next;
   }
@@ -2096,10 +2395,29 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s,
 // document: pass 1, and pass 2 with Repeats when pass 1 is not good enough.
 // Returns the number of passes, or -reason (kWhy*) to re-queue.
 enum { kWhyLength = 1, kWhyClassify = 2, kWhySpan = 3, kWhySqueeze = 4, kWhyCapacity = 5 };
-template <bool D>
+// MoveLang1ToLang2's vector half (compact_lang_det_impl.cc:1122-1147), lane 0
+// over the document's vector: relabel lang1 -> lang2, merge neighbours that
+// now share a language.
+__device__ __noinline__ void vec_move_lang(VecState* V, int from_lang, int to_lang, int unk) {
+  int k = 0, prior = unk;
+  for (int i = 0; i < V->n; ++i) {
+    cld_chunk c = V->v[i];
+    if (c.lang1 == (uint16_t)from_lang) c.lang1 = (uint16_t)to_lang;
+    if ((int)c.lang1 == prior && k > 0) {
+      V->v[k - 1].bytes += c.bytes;
+    } else {
+      V->v[k] = c;
+      ++k;
+    }
+    prior = c.lang1;
+  }
+  V->n = k;
+}
+
+template <bool D, bool VEC = false>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
-                      const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf) {
+                      const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf, VecState* V = nullptr) {
   const int unk = (int)T.unknown_lang;
   // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
   if (lane == 0) s.has_pri = pri != nullptr;
@@ -2135,10 +2453,14 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
   // the Squeeze one is fresh per span (pred2).
   bool sq = false;
   int nsp = 0, cur = 0;                          // span cache (pass 1): spans recorded, bytes used
-  bool cache_ok = true;
+  bool cache_ok = !VEC;                          // (vec mode rebuilds pass 2's spans with their offset map)
   for (int pass = 1; pass <= 3; ++pass) {
     const bool rep = pass == 3 || (pass == 2 && !sq);    // Repeats always comes with Finish
     const bool from_cache = pass == 2 && rep && cache_ok;
+    if constexpr (VEC) {                         // each pass starts a new vector (:1730-1732)
+      V->n = 0;
+      V->over = false;
+    }
     if (lane == 0) s.dt.init();
     if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
     uint32_t hcarry = 0, ep = 0;
@@ -2176,7 +2498,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
-        tb = next_span(T, dv, S, lb, next, ul, st, lane);
+        tb = next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {
@@ -2189,6 +2511,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
       if constexpr (D) mark(s, lane, 1, t);
       if (pass == 1) {
         if (tb > 2048 && squeeze_trigger(S, lb, careful, lane)) {   // recursion with Squeeze (:1867-1900)
+          if constexpr (VEC) return -kWhySqueeze;  // (CheapSqueezeInplaceOverwrite: the sequential kernel)
           restart = true;
           cache_ok = false;
           break;
@@ -2205,7 +2528,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         if (sq) tb = squeeze_span(S, s.text, tb, careful, lane);             // in place, as the reference does
         if (rep_inline) {
           bool okr;
-          tb = rep_words(S, s.text, s.text, tb, hcarry, ep, careful, okr, lane);   // in place, as the reference does
+          tb = rep_words<VEC>(S, s.text, s.text, tb, hcarry, ep, careful, okr, lane);   // in place, as the reference does
           if (!okr) return -kWhySpan;
           if constexpr (D) mark(s, lane, 3, t);
         }
@@ -2215,13 +2538,13 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           dbg_words(s, lane, v, 4);
         }
         Win win{nullptr, 0, 16 * n16, 16 * n16};                          // the whole span is in s.text
-        ok = score_span<D>(T, S, s, win, tb, ul, lane, tr, doc, cflags);
+        ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
       } else {
         const uint8_t* text = lb;
         if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
         if (rep_inline) {
           bool okr;
-          tb = rep_words(S, lb, S.lb[1], tb, hcarry, ep, careful, okr, lane);
+          tb = rep_words<VEC>(S, lb, S.lb[1], tb, hcarry, ep, careful, okr, lane);
           if (!okr) return -kWhySpan;
           text = S.lb[1];
           if constexpr (D) mark(s, lane, 3, t);
@@ -2232,7 +2555,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           dbg_words(s, lane, v, 4);
         }
         Win win{text, 0, 0, (tb + 48 + 15) & ~15};                       // windows of it go to s.text
-        ok = score_span<D>(T, S, s, win, tb, ul, lane, tr, doc, cflags);
+        ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
       }
       if (!ok) return -kWhyCapacity;
       t = (D && s.prof) ? (long long)clock64() : 0;
@@ -2242,7 +2565,33 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
       sq = true;
       continue;
     }
-    if (wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0)) return pass;
+    if constexpr (VEC) {
+      auto mv = [&](int from_lang, int to_lang) {
+        if (lane == 0) vec_move_lang(V, from_lang, to_lang, unk);
+        V->n = rdl(V->n, 0);
+      };
+      if (wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0, mv)) {
+        // FinishResultVector(0, buffer_length) (:1688-1702): the first item
+        // starts at 0, the last ends at the document end
+        if (lane == 0 && V->n > 0 && !V->over) {
+          cld_chunk f = V->v[0];
+          if (f.offset > 0) {
+            f.bytes += f.offset;
+            f.offset = 0;
+            V->v[0] = f;
+          }
+          cld_chunk e = V->v[V->n - 1];
+          if (e.offset + e.bytes < L) {
+            e.bytes += L - (e.offset + e.bytes);
+            V->v[V->n - 1] = e;
+          }
+        }
+        gsync();
+        return pass;
+      }
+    } else {
+      if (wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0)) return pass;
+    }
   }
   return 0;
 }

@@ -418,6 +418,7 @@ struct Device {
     uint64_t* pos = nullptr; size_t pos_cap = 0;
     uint32_t* order = nullptr; size_t order_cap = 0;
     cld_chunk* compact = nullptr; size_t compact_cap = 0;
+    uint8_t* vslots = nullptr;   // k_long<VEC>: one VecSlot per slot of d_slots (on first use)
   } vec;
   std::mutex mu;
 };
@@ -1037,6 +1038,14 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     if (hipMalloc(&V.arena, (uint64_t)lanes * V.stride) != hipSuccess) { V.arena = nullptr; return CLD_ENOMEM; }
     V.lanes = lanes;
   }
+  // The parallel kernels build the vectors (k_long<VEC>); documents they
+  // cannot reproduce, and HTML pages, run the sequential kernel.
+  // CLD_VEC_PARALLEL=0: the sequential kernel for every document (A/B).
+  static const bool parallel_env = !(getenv("CLD_VEC_PARALLEL") && atoi(getenv("CLD_VEC_PARALLEL")) == 0);
+  if (parallel_env && d->n_slots > 0 && !V.vslots) {
+    if (hipMalloc(&V.vslots, (uint64_t)d->n_slots * cld_vec_slot_bytes()) != hipSuccess) V.vslots = nullptr;
+  }
+  const bool parallel = parallel_env && V.vslots != nullptr;
   // Sub-batches as large as memory allows: a launch lasts at least as long as
   // its longest document (one wave runs it start to end), so every sub-batch
   // pays that tail once -- 32 MB sub-batches held C5 to 76K docs/s, one launch
@@ -1053,6 +1062,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   // its pool region or an offset map), the vectors to ch in document order.
   std::vector<uint64_t> pool_off, pos;
   std::vector<uint32_t> order, bstart;
+  cld_batch_stats vst{};
   static const bool no_order = getenv("CLD_VEC_ORDER") && atoi(getenv("CLD_VEC_ORDER")) == 0;   // (A/B only)
   auto sub = [&](const uint8_t* b, const uint64_t* o, size_t m, cld_result* res, const uint8_t* sp,
                  const uint32_t* pr, bool big, std::vector<int32_t>& nch, std::vector<cld_chunk>& ch) -> int {
@@ -1071,7 +1081,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     // Longest documents first: a wave runs one document start to end, so with
     // more documents than waves a long one dequeued late sets the batch's end.
     // A counting sort by bit length of the size (descending).
-    const bool ordered = !no_order && m > (size_t)V.lanes;
+    const bool ordered = !parallel && !no_order && m > (size_t)V.lanes;
     if (ordered) {
       if (grow(&V.order, &V.order_cap, m)) return CLD_ENOMEM;
       bstart.assign(66, 0);
@@ -1090,13 +1100,36 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     if (pr) HIP_OK(hipMemcpyAsync(V.pri, pr, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     if (ordered) HIP_OK(hipMemcpyAsync(V.order, order.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
-    HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes, d->d_counters,
-                                  sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off, V.nch,
-                                  ordered ? V.order : nullptr, cflags & kCldFlags, s));
+    if (parallel) {
+      if (grow(&d->d_requeue, &d->requeue_cap, m) || grow(&d->d_requeue2, &d->requeue2_cap, m) ||
+          grow(&d->d_lsorted, &d->lsorted_cap, m) || grow(&d->d_lkey, &d->lkey_cap, m))
+        return CLD_ENOMEM;
+      HIP_OK(cld_launch_route_vec((int)m, sp ? V.sp : nullptr, d->d_counters, d->d_requeue, d->d_requeue2, s));
+      HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
+      HIP_OK(cld_launch_long_vec(d->d_T, V.in - base, V.offs, d->d_lsorted, V.out, d->d_slots, V.vslots, d->n_slots,
+                                 d->d_requeue2, d->d_counters, cflags & kCldFlags, sp ? V.sp : nullptr,
+                                 pr ? V.pri : nullptr, V.pool, V.pool_off, V.nch, s));
+      HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes,
+                                    d->d_counters, sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off,
+                                    V.nch, d->d_requeue2, cflags & kCldFlags, d->d_counters + kCtrRequeue2, s));
+    } else {
+      HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes,
+                                    d->d_counters, sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off,
+                                    V.nch, ordered ? V.order : nullptr, cflags & kCldFlags, nullptr, s));
+    }
     nch.resize(m);
+    uint32_t ctr[kCtrSlots];
+    HIP_OK(hipMemcpyAsync(ctr, d->d_counters, sizeof(ctr), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(res, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    // statistics (cld_last_batch_stats): documents the parallel kernel finished
+    // (long_docs) and those the sequential kernel took (general_docs)
+    vst.docs += m;
+    vst.general_docs += parallel ? ctr[kCtrRequeue2] : m;
+    vst.long_docs += parallel ? m - ctr[kCtrRequeue2] : 0;
+    for (int k = 0; k < 3; ++k) vst.passes[k] += ctr[kCtrPass1 + k];
+    vst.passes[3] += ctr[kCtrError];
     pos.assign(m, 0);
     uint64_t total = 0;
     for (size_t i = 0; i < m; ++i) {
@@ -1172,6 +1205,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     counts->insert(counts->end(), nch.begin(), nch.end());
     a += m;
   }
+  d->last = vst;
+  d->stats_pending = false;
   return failed ? CLD_EIO : CLD_OK;
 }
 
@@ -1383,7 +1418,7 @@ void cld_shutdown(void) {
       (void)hipEventDestroy(h.up); (void)hipEventDestroy(h.comp); (void)hipEventDestroy(h.down);
     }
     (void)hipHostFree(d->h_ctr);
-    for (void* p : {(void*)d->vec.arena, (void*)d->vec.in, (void*)d->vec.offs, (void*)d->vec.out, (void*)d->vec.sp,
+    for (void* p : {(void*)d->vec.arena, (void*)d->vec.vslots, (void*)d->vec.in, (void*)d->vec.offs, (void*)d->vec.out, (void*)d->vec.sp,
                     (void*)d->vec.pri, (void*)d->vec.pool, (void*)d->vec.pool_off, (void*)d->vec.nch,
                     (void*)d->vec.pos, (void*)d->vec.order, (void*)d->vec.compact})
       if (p) (void)hipFree(p);

@@ -1270,7 +1270,13 @@ __device__ __forceinline__ void sort3_regs(SlotRegs& r, int lane) {
 // order, merges into the first later slot of its close set.  The close sets
 // are gathered for all slots at once; the slots that have one (a handful at
 // most) are visited in order on scalars.
-__device__ __forceinline__ void refine_close_pairs_regs(const DevTables& T, SlotRegs& r, int lane) {
+struct NoMove {
+  __device__ __forceinline__ void operator()(int, int) const {}
+};
+// mv(from_lang, to_lang), wave-uniform, for every merge in order: vec mode
+// relabels the chunk vector there (MoveLang1ToLang2, :1122-1147).
+template <class Mv = NoMove>
+__device__ __forceinline__ void refine_close_pairs_regs(const DevTables& T, SlotRegs& r, int lane, Mv&& mv = Mv{}) {
   int cs = lane < 24 ? close_set(T, (int)r.key) : 0;
   uint64_t todo = __ballot(cs != 0);
   while (todo) {
@@ -1284,6 +1290,7 @@ __device__ __forceinline__ void refine_close_pairs_regs(const DevTables& T, Slot
     const bool s_from = rdl(r.val, s) < rdl(r.val, s2);        // the smaller moves into the larger
     const int from = s_from ? s : s2, to = s_from ? s2 : s;
     const int fv = rdl(r.val, from), fs = rdl(r.sc, from), fr = rdl(r.rl, from);
+    mv(rdl((int)r.key, from), rdl((int)r.key, to));
     if (lane == to) { r.val += fv; r.sc += fs; r.rl += fr; }
     if (lane == from) { r.key = kUnusedKey; r.sc = 0; r.rl = 0; cs = 0; }   // (value stays, as there)
   }
@@ -1333,10 +1340,11 @@ __device__ __forceinline__ double rdl_f64(double v, int l) {
 // pass must follow (never when `final`).  best_effort: kCLDFlagBestEffort
 // (:1998-2000, :1493): no unreliable-language removal and no UNKNOWN for a
 // small return percent.
+template <class Mv = NoMove>
 __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, int total, bool final, cld_result* __restrict__ out,
-                               int lane, bool best_effort = false) {
+                               int lane, bool best_effort = false, Mv&& mv = Mv{}) {
   SlotRegs r = load_slots(dt, lane);
-  refine_close_pairs_regs(T, r, lane);
+  refine_close_pairs_regs(T, r, lane, mv);
   sort3_regs(r, lane);
   double ns;
   DocSum x = extract_regs(T, r, total, lane, ns);

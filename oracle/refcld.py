@@ -84,6 +84,9 @@ class RefCLD:
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.refcld_detect_batch_flags.argtypes = lib.refcld_detect_batch.argtypes + [ctypes.c_int]
         lib.refcld_detect_flags.argtypes = lib.refcld_detect.argtypes + [ctypes.c_int]
+        lib.refcld_detect_batch_vec.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.c_int]
         fd, path = tempfile.mkstemp(suffix=".cld2_data_file00")
         with os.fdopen(fd, "wb") as f:
             f.write(cld2_data_file.build(cldt.Blob.load(cldt_path)))
@@ -110,6 +113,29 @@ class RefCLD:
         if rc != 0:
             raise RuntimeError("refcld_detect_batch rc=%d" % rc)
         return out
+
+    def detect_batch_vec(self, buf, offsets, plain=None, threads=1, flags=0):
+        """Vector mode over a batch, `threads` host threads -> (results, chunks, chunk_offsets),
+        document i's vector = chunks[chunk_offsets[i]:chunk_offsets[i + 1]]."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        base = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(np.diff(offsets) + 16, out=base[1:])      # a region of len + 16 chunks per document
+        ch = np.zeros(max(int(base[-1]), 1), dtype=CHUNK_DTYPE)
+        pl = None if plain is None else np.ascontiguousarray(plain, dtype=np.uint8)
+        bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))
+        rc = self.lib.refcld_detect_batch_vec(bptr, offsets.ctypes.data, n, None if pl is None else pl.ctypes.data,
+                                              out.ctypes.data, ch.ctypes.data, base.ctypes.data, threads, int(flags))
+        if rc != 0:
+            raise RuntimeError("refcld_detect_batch_vec rc=%d" % rc)
+        cnt = out["n_chunks"].astype(np.int64)
+        assert np.all(cnt <= np.diff(base).astype(np.int64))
+        coffs = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(cnt, out=coffs[1:])
+        idx = np.repeat(base[:-1].astype(np.int64) - coffs[:-1].astype(np.int64), cnt) + np.arange(int(coffs[-1]))
+        return out, ch[idx], coffs
 
     def detect_vec(self, doc, plain=True, hints=None, flags=0):
         """ExtDetectLanguageSummary with a ResultChunkVector -> (result, chunks)."""

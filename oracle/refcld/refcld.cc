@@ -140,4 +140,37 @@ int refcld_detect_batch(const char* buf, const uint64_t* offs, int n, const uint
   return refcld_detect_batch_flags(buf, offs, n, plain, hints, out, threads, 0);
 }
 
+// Vector mode over `threads` pthreads: document i's chunks go to
+// chunks[chunk_base[i] ..], at most chunk_base[i + 1] - chunk_base[i] of them
+// (out[i].n_chunks is the full count).
+typedef struct {
+  const char* buf; const uint64_t* offs; int lo, hi; const uint8_t* plain; refcld_result* out;
+  refcld_chunk* chunks; const uint64_t* base; int flags;
+} vjob_t;
+
+static void* run_vec(void* a) {
+  vjob_t* j = (vjob_t*)a;
+  std::string s;
+  for (int i = j->lo; i < j->hi; ++i)
+    detect_one(j->buf + j->offs[i], (int)(j->offs[i + 1] - j->offs[i]), j->plain ? j->plain[i] : 1, NULL, &j->out[i],
+               j->chunks + j->base[i], (int)(j->base[i + 1] - j->base[i]), &s, j->flags);
+  return NULL;
+}
+
+int refcld_detect_batch_vec(const char* buf, const uint64_t* offs, int n, const uint8_t* plain, refcld_result* out,
+                            refcld_chunk* chunks, const uint64_t* chunk_base, int threads, int flags) {
+  if (!isDataLoaded()) return -1;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  std::vector<pthread_t> th(threads);
+  std::vector<vjob_t> jobs(threads);
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = vjob_t{buf, offs, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads), plain, out,
+                     chunks, chunk_base, flags};
+    pthread_create(&th[t], NULL, run_vec, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}
+
 }  // extern "C"
