@@ -632,6 +632,18 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   }
   int ss = 0;                                    // the span script: read off q's lane in the first window
   if (lane == 0) lb[0] = ' ';
+  // vec mode: where a scan that reaches the document end stops.  A final
+  // character cut by the end is consumed whole (UTF8OneCharLen) by the
+  // reference's loops, so its claimed bytes run past L.
+  int dend = L;
+  if constexpr (VEC) {
+    int xc = L - 1;
+    while (xc > 0 && xc > L - 4 && (dv.p[xc] & 0xC0) == 0x80) --xc;
+    if (xc >= 0 && L > 0) {
+      const int nc = utf8_len(dv.p[xc]);
+      if (xc + nc > L) dend = xc + nc;
+    }
+  }
   if constexpr (VEC) {
     // map2original_ at the leading space (getonescriptspan.cc:835-848):
     // Delete(offset) Delete(skip) Insert(1) maps it past the skipped bytes, to
@@ -736,7 +748,8 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         // the gap; a gap of one byte makes that a Copy(1) of the gap byte, no
         // gap an Insert at the run end (:955-993)
         const int from = sep ? x : x + n;
-        const int nl = next_stop(S.lsm, from, L);
+        int nl = next_stop(S.lsm, from, L);
+        if (nl >= L) nl = dend;
         omap[lpos + opre + olen] = (uint32_t)(nl - from >= 2 ? nl : from);
       }
     }
@@ -763,7 +776,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     if ((w << 6) + 64 >= L) {                                         // end of document
       if (run && wmax((uint32_t)(cutx + 1)) == 0) {                 // (a cut character brings its own)
         if (lane == 0) lb[lpos] = ' ';
-        if (VEC && lane == 0) omap[lpos] = (uint32_t)L;              // Insert(1) at the document end
+        if (VEC && lane == 0) omap[lpos] = (uint32_t)dend;           // Insert(1) at the document end
         ++lpos;
         ++put;
       }
@@ -782,13 +795,22 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       for (int k = 0; k < nc; ++k) tail[k] = (uint8_t)dv.at(cutx + k);
       for (int k = 0; k < 4; ++k) tail[nc + k] = ' ';                 // separator + "   " (ilen stops before \0)
       filled = lower_tail(T.lower, tail, nc + 4, lb + lpos, kMaxScriptLowerBuffer - lpos);
+      if constexpr (VEC) {
+        // the cut character is copied whole (Copy(n): its missing bytes map
+        // past the document end), then the ' ' and the pads map to where its
+        // claimed bytes end; the lowercaser must leave these bytes as they are
+        for (int k = 0; k < filled; ++k) {
+          omap[lpos + k] = (uint32_t)(cutx + (k < nc ? k : nc));
+          if (k < nc + 4 && lb[lpos + k] != tail[k]) bad = 1;
+        }
+      }
     }
     lpos += rdl(filled, 0);
     for (int k = lane; k < 40; k += 64) lb[lpos + k] = 0;
     lpos -= 3;                                                        // text_bytes = filled - 3
   } else {
     for (int k = lane; k < 40; k += 64) lb[lpos + k] = k < 3 ? ' ' : 0;   // "   " (lowered pads), NULs
-    if (VEC && lane < 4) omap[lpos + lane] = (uint32_t)nxt;            // Insert(4): where the scan stopped
+    if (VEC && lane < 4) omap[lpos + lane] = (uint32_t)(nxt >= L ? dend : nxt);   // Insert(4): where the scan stopped
   }
   // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
   // spans near the 40 KB limit that also grow; re-queue those.

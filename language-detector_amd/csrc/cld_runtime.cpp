@@ -421,6 +421,7 @@ struct Device {
     uint8_t* vslots = nullptr;   // k_long<VEC>: one VecSlot per slot of d_slots (on first use)
   } vec;
   std::mutex mu;
+  std::atomic<int> inflight{0};   // calls routed to this context and not yet returned (pick_context)
 };
 
 std::mutex g_init_mu;
@@ -1308,12 +1309,18 @@ int cld_init(const char* tables_path, int n_devices) {
     }
     if (ids.empty()) return g_init_rc = CLD_EINVAL;
   }
-  for (int id : ids) {
-    Device* d = new Device();
-    d->id = id;
-    if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
-    g_devs.push_back(d);
-  }
+  // CLD_MI355X_CONTEXTS=k: k contexts per GPU (own streams, scratch and k_long
+  // slots), so concurrent request-sized calls run side by side on one GPU
+  // instead of queueing behind each other's longest document (pick_context)
+  int per = 1;
+  if (const char* e = getenv("CLD_MI355X_CONTEXTS")) per = std::max(1, std::min(64, atoi(e)));
+  for (int id : ids)
+    for (int k = 0; k < per; ++k) {
+      Device* d = new Device();
+      d->id = id;
+      if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
+      g_devs.push_back(d);
+    }
   return g_init_rc = CLD_OK;
 }
 
@@ -1448,6 +1455,36 @@ int first_error(const std::vector<int>& rcs) {
 }
 }  // namespace
 
+namespace {
+// Batches below this much text (CLD_SMALL_BATCH_MB, default 16) run whole on
+// one context -- the least busy one -- instead of being split across all of
+// them: a request-sized batch gains nothing from a split (its time is its
+// longest document's), and concurrent callers then each get a context.
+uint64_t small_batch_bytes() {
+  static const uint64_t v = (getenv("CLD_SMALL_BATCH_MB") ? strtoull(getenv("CLD_SMALL_BATCH_MB"), nullptr, 10) : 16ull)
+                            << 20;
+  return v;
+}
+struct Picked {
+  Device* d;
+  explicit Picked(Device* x) : d(x) { d->inflight.fetch_add(1); }
+  ~Picked() { d->inflight.fetch_sub(1); }
+};
+Device* pick_context() {
+  static std::atomic<unsigned> rr{0};
+  const size_t n = g_devs.size();
+  const unsigned start = rr.fetch_add(1);
+  Device* best = g_devs[start % n];
+  int bl = best->inflight.load();
+  for (size_t i = 1; i < n && bl > 0; ++i) {
+    Device* d = g_devs[(start + i) % n];
+    const int l = d->inflight.load();
+    if (l < bl) { bl = l; best = d; }
+  }
+  return best;
+}
+}  // namespace
+
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_result* out, uint32_t flags) {
   if ((flags & ~(kPrepFlags | kPublicFlags)) != 0 || (n > 0 && (!buf || !offsets || !out))) return CLD_EINVAL;
   if (n == 0) return CLD_OK;
@@ -1458,10 +1495,14 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   if (rc) return rc;
   std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   const size_t ndev = g_devs.size();
-  // Shard by byte count (+ a per-document weight) at document boundaries.
+  // Shard by estimated kernel cost at document boundaries (cld_plan_shards).
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
   if (ndev == 1) return run_host_shard_isolating(g_devs[0], buf, offsets, n, out, flags);
+  if (offsets[n] - offsets[0] < small_batch_bytes()) {
+    Picked p(pick_context());
+    return run_host_shard_isolating(p.d, buf, offsets, n, out, flags);
+  }
   FanoutReg reg(ndev, buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;
@@ -1563,6 +1604,10 @@ int cld_detect_batch_ex(const uint8_t* buf, const uint64_t* offsets, size_t n, c
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
   if (ndev == 1) return run_host_shard_isolating(g_devs[0], buf, offsets, n, out, cf, sp, pr, html);
+  if (offsets[n] - offsets[0] < small_batch_bytes()) {
+    Picked p(pick_context());
+    return run_host_shard_isolating(p.d, buf, offsets, n, out, cf, sp, pr, html);
+  }
   FanoutReg reg(ndev, buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;

@@ -106,6 +106,20 @@ for i in range(len(vo) - 1):
     assert [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]] == \
         [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in ch], i
     assert int(res[i]["summary_lang"]) == r.summary_lang, i
+# request-sized batches from concurrent callers: each runs whole on the least
+# busy context (cld_runtime.cpp pick_context), results as the oracle's
+import threading
+sb, so = corpus.c5(4000, seed=125)
+want = o.detect_batch(sb, so, threads=16)
+parts = np.array_split(np.arange(4000), 16)
+got = [None] * 16
+def work(k):
+    lo, hi = int(parts[k][0]), int(parts[k][-1]) + 1
+    got[k] = cld_amd.detect_batch(buf=sb, offsets=so[lo:hi + 1])
+ths = [threading.Thread(target=work, args=(k,)) for k in range(16)]
+for t in ths: t.start()
+for t in ths: t.join()
+assert_same(np.concatenate(got), want, "concurrent small batches")
 print("fan-out ok", docs)
 '''
 
@@ -116,7 +130,8 @@ def test_multi_context_fan_out():
     _ex / _vec) with GPU 0 registered twice (CLD_MI355X_DEVICE_MAP=0,0: two
     contexts with their own streams, tables and scratch), in a child process
     (the runtime's device set is fixed per process).  Both contexts must get
-    documents, and every result must equal the oracle's."""
+    documents, and every result must equal the oracle's; so must 16 concurrent
+    request-sized calls, which each run whole on the least busy context."""
     import os
     import subprocess
     import sys
