@@ -17,6 +17,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -1470,6 +1471,127 @@ struct Picked {
   explicit Picked(Device* x) : d(x) { d->inflight.fetch_add(1); }
   ~Picked() { d->inflight.fetch_sub(1); }
 };
+Device* pick_context();
+
+// Request coalescing (cld_detect_batch below small_batch_bytes()).  A launch
+// lasts as long as its longest document (one wavefront scores it start to
+// end), so request-sized calls queued one after another cost that tail each;
+// run together they pay it once.  The first caller to find a dispatch slot
+// free (one per context) takes the queued requests with its flags, up to
+// kCoalesceBytes of text / kCoalesceDocs documents, copies them into pinned
+// buffers (the GPU reads those directly), runs them as one batch on the least
+// busy context and hands every caller its results and return code.  A lone
+// request runs straight from the caller's buffers.  Results never depend on
+// the company a document keeps.
+constexpr uint64_t kCoalesceBytes = 64ull << 20;
+constexpr size_t kCoalesceDocs = 256 * 1024;
+struct Req {
+  const uint8_t* buf;
+  const uint64_t* offs;
+  size_t n;
+  cld_result* out;
+  uint32_t flags;
+  int rc;
+  bool done;
+};
+std::mutex g_rq_mu;
+std::condition_variable g_rq_cv;
+std::deque<Req*> g_rq;
+int g_rq_active = 0;
+struct Arena {                  // pinned staging of one dispatch (reused)
+  uint8_t* buf = nullptr; size_t buf_cap = 0;
+  uint64_t* offs = nullptr; size_t offs_cap = 0;
+  cld_result* out = nullptr; size_t out_cap = 0;
+};
+std::mutex g_arena_mu;
+std::vector<Arena*> g_arenas;   // free arenas
+
+void run_group(const std::vector<Req*>& grp) {
+  if (grp.size() == 1) {        // nothing to merge: straight from the caller's buffers
+    Req* r = grp[0];
+    Picked p(pick_context());
+    r->rc = run_host_shard_isolating(p.d, r->buf, r->offs, r->n, r->out, r->flags);
+    return;
+  }
+  Arena* a = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_arena_mu);
+    if (!g_arenas.empty()) { a = g_arenas.back(); g_arenas.pop_back(); }
+  }
+  if (!a) a = new Arena();
+  size_t docs = 0;
+  uint64_t bytes = 0;
+  for (Req* r : grp) { docs += r->n; bytes += r->offs[r->n] - r->offs[0]; }
+  int rc = CLD_OK;
+  if (grow_host(&a->buf, &a->buf_cap, std::max<uint64_t>(bytes, 1)) || grow_host(&a->offs, &a->offs_cap, docs + 1) ||
+      grow_host(&a->out, &a->out_cap, docs))
+    rc = CLD_ENOMEM;
+  if (rc == CLD_OK) {
+    size_t k = 0;
+    uint64_t at = 0;
+    for (Req* r : grp) {
+      const uint64_t b0 = r->offs[0], nb = r->offs[r->n] - b0;
+      memcpy(a->buf + at, r->buf + b0, nb);
+      for (size_t i = 0; i < r->n; ++i) a->offs[k + i] = at + (r->offs[i] - b0);
+      k += r->n;
+      at += nb;
+    }
+    a->offs[docs] = at;
+    Picked p(pick_context());
+    rc = run_host_shard_isolating(p.d, a->buf, a->offs, docs, a->out, grp[0]->flags);
+  }
+  size_t k = 0;
+  for (Req* r : grp) {
+    if (rc == CLD_OK || rc == CLD_EIO) {
+      memcpy(r->out, a->out + k, r->n * sizeof(cld_result));
+      bool failed = false;
+      for (size_t i = 0; i < r->n && rc == CLD_EIO; ++i) failed |= r->out[i].summary_lang == CLD_LANG_FAILED;
+      r->rc = failed ? CLD_EIO : CLD_OK;
+    } else {
+      r->rc = rc;
+    }
+    k += r->n;
+  }
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  g_arenas.push_back(a);
+}
+
+int run_coalesced(const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
+  Req me{buf, offs, n, out, flags, CLD_OK, false};
+  std::unique_lock<std::mutex> lk(g_rq_mu);
+  g_rq.push_back(&me);
+  for (;;) {
+    if (me.done) return me.rc;
+    if (g_rq_active < (int)g_devs.size() && !g_rq.empty()) {
+      std::vector<Req*> grp;
+      const uint32_t f = g_rq.front()->flags;
+      uint64_t bytes = 0;
+      size_t docs = 0;
+      for (auto it = g_rq.begin(); it != g_rq.end();) {
+        Req* r = *it;
+        const uint64_t nb = r->offs[r->n] - r->offs[0];
+        if (r->flags != f || (!grp.empty() && (bytes + nb > kCoalesceBytes || docs + r->n > kCoalesceDocs))) {
+          ++it;
+          continue;
+        }
+        grp.push_back(r);
+        bytes += nb;
+        docs += r->n;
+        it = g_rq.erase(it);
+      }
+      ++g_rq_active;
+      lk.unlock();
+      run_group(grp);
+      lk.lock();
+      --g_rq_active;
+      for (Req* r : grp) r->done = true;
+      g_rq_cv.notify_all();
+      continue;
+    }
+    g_rq_cv.wait(lk);
+  }
+}
+
 Device* pick_context() {
   static std::atomic<unsigned> rr{0};
   const size_t n = g_devs.size();
@@ -1498,11 +1620,8 @@ int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n, cld_
   // Shard by estimated kernel cost at document boundaries (cld_plan_shards).
   std::vector<size_t> cut(ndev + 1, 0);
   cld_plan_shards(offsets, n, (int)ndev, cut.data());
+  if (offsets[n] - offsets[0] < small_batch_bytes()) return run_coalesced(buf, offsets, n, out, flags);
   if (ndev == 1) return run_host_shard_isolating(g_devs[0], buf, offsets, n, out, flags);
-  if (offsets[n] - offsets[0] < small_batch_bytes()) {
-    Picked p(pick_context());
-    return run_host_shard_isolating(p.d, buf, offsets, n, out, flags);
-  }
   FanoutReg reg(ndev, buf, offsets, n, out);
   std::vector<int> rcs(ndev, CLD_OK);
   std::vector<std::thread> th;

@@ -141,3 +141,31 @@ def test_multi_context_fan_out():
     r = subprocess.run([sys.executable, "-c", FAN_OUT], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "fan-out ok" in r.stdout
+
+
+def test_concurrent_request_sized_calls_coalesce(gpu, oracle):
+    """Request-sized cld_detect_batch calls from 12 threads at once are run
+    together (cld_runtime.cpp run_coalesced: one GPU batch per dispatch, the
+    documents copied into pinned staging and the results handed back to each
+    caller), with flags kept apart: every caller gets exactly its own results."""
+    import threading
+    from test_gpu_parity import assert_same
+    b, o = corpus.c5(6000, seed=131)
+    want = oracle.detect_batch(b, o, threads=16)
+    want_be = oracle.detect_batch_ex(b, o, threads=16, flags=gpu.FLAG_BEST_EFFORT)
+    parts = np.array_split(np.arange(6000), 24)
+    got = [None] * 24
+
+    def work(k):
+        for rep in range(3):
+            lo, hi = int(parts[k][0]), int(parts[k][-1]) + 1
+            got[k] = gpu.detect_batch(buf=b, offsets=o[lo:hi + 1], flags=gpu.FLAG_BEST_EFFORT if k % 2 else 0)
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(24)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for k in range(24):
+        lo, hi = int(parts[k][0]), int(parts[k][-1]) + 1
+        assert_same(got[k], (want_be if k % 2 else want)[lo:hi], "caller %d" % k)

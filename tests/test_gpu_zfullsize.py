@@ -52,3 +52,34 @@ def test_full_size_equals_reference(gpu, ref_tables, name):
     assert not bad.any(), "%s/%s: %d of %d differ, first %s" % (name, label, bad.sum(), n, np.nonzero(bad)[0][:5])
     assert ub.sum() == 0
     assert st.passes[3] == 0
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+def test_full_size_vectors_equal_reference(gpu, ref_tables, name):
+    """cld_detect_batch_vec on the same corpora: every result field and every
+    ResultChunkVector equal to the reference's ExtDetectLanguageSummary with a
+    vector; plain documents must run the parallel kernels (k_long<VEC>), only
+    the few they hand on (Squeeze pages, length-changing lowercasing) the
+    sequential one."""
+    label, ref = ref_tables
+    buf, offs = fullsize.load(name)
+    n = len(offs) - 1
+    res, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs)
+    st = gpu.last_stats(0)
+    rres, rch, rco = ref.detect_batch_vec(buf, offs, threads=16)
+    bad = np.zeros(n, bool)
+    for f in FIELDS:
+        bad |= (res[f].astype(np.float64) != rres[f].astype(np.float64)).reshape(n, -1).any(axis=1)
+    cnt_bad = np.diff(coffs.astype(np.int64)) != np.diff(rco.astype(np.int64))
+    bad |= cnt_bad
+    if not cnt_bad.any():
+        neq = np.zeros(len(chunks), bool)
+        for f in ("offset", "bytes", "lang1"):
+            neq |= chunks[f] != rch[f]
+        bad[np.searchsorted(coffs, np.nonzero(neq)[0], side="right") - 1] = True
+    bad &= ~ub_docs(buf, offs)
+    print("%s/%s vectors: %d documents, %d chunks, %d differ; parallel kernel %d, sequential %d"
+          % (name, label, n, int(coffs[-1]), int(bad.sum()), st.long_docs, st.general_docs))
+    assert not bad.any(), "%s/%s: %d of %d differ, first %s" % (name, label, bad.sum(), n, np.nonzero(bad)[0][:5])
+    assert st.long_docs >= 0.99 * n, (st.long_docs, st.general_docs)
