@@ -26,7 +26,7 @@ offs.astype(np.uint64).tofile(os.path.join(d, "o.bin"))
 exe = os.path.join(ROOT, "tools", "build", "req_bench")
 if os.environ.get("REQ_RATE_PROF"):   # kernel statistics of the single-caller run (rocprofv3)
     out = os.environ["REQ_RATE_PROF"]
-    subprocess.run(["rocprofv3", "--kernel-trace", "--stats", "-d", out, "-o", "req", "--", exe,
+    subprocess.run(["rocprofv3", "--kernel-trace", "--stats", "-d", out, "-o", "req", "--output-format", "csv", "--", exe,
                     os.path.join(d, "c.bin"), os.path.join(d, "o.bin"), "1", str(1 << 20), "1"], check=True,
                    timeout=600)
 for callers in [int(c) for c in os.environ.get("REQ_RATE_CALLERS", "1,8").split(",")]:
