@@ -135,6 +135,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
                                              const uint8_t* txt, const int L, const uint64_t a, const int i,
                                              const uint8_t sp, uint8_t* __restrict__ special,
                                              uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
+                                             uint32_t* __restrict__ hpos, uint32_t* __restrict__ hgap,
                                              unsigned long long* __restrict__ prof, const uint64_t am0,
                                              const uint64_t am1, const int lane) {
   const DocView dv{txt, L};
@@ -207,7 +208,10 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
   // 3. the output, window by window
   uint8_t* o = hbuf + a;
   uint8_t* f = hflag + a;
-  int q = 0, cb = 0, bad = 0, conts = 0, need = 0;
+  uint32_t* hp = hpos ? hpos + a : nullptr;
+  uint32_t* hg = hpos ? hgap + a : nullptr;
+  int q = 0, cb = 0, bad = 0, conts = 0, need = 0, novec = 0;
+  int drop_run = 0;                                            // dropped '&'s ending the previous window
   uint32_t cover = 0;                                          // end of the last reached candidate so far
   uint32_t drop_prev = 0;                                      // the byte before this window was a dropped '&'
   for (int w0 = 0; w0 < L; w0 += 64) {
@@ -236,9 +240,34 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
     const bool dropped = reached && kind == 2;
     const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
     const int at = q + excl_scan(emit, lane);
+    // vec mode (hpos): every output byte's page offset, as map2original_ maps
+    // it -- a text byte its own, a tag's space the tag start, an entity's k-th
+    // byte start + k (Copy(plen), then Delete(tlen - plen)).  An entity whose
+    // Delete is a single byte, or that grows (Insert), could merge with the
+    // run's closing Insert(1) into a Copy (offsetmap.cc:122-156): such pages
+    // keep the sequential kernel in vec mode (kSpecialNoVec).
+    // the first byte after dropped '&'s also records where they began (hpos
+    // second half, read where hflag bit 1 is set): a run ending there has its
+    // gap start at the first of them (they merge into the gap's Delete)
+    const uint64_t dm = __ballot(dropped);
+    if (hp && dprev) {
+      const uint64_t nd = ~dm & lanemask_lt(lane);             // bytes before this one that were not dropped
+      const int first = nd ? w0 + (63 - __builtin_clzll(nd)) + 1 : w0 - drop_run;
+      hg[at] = (uint32_t)first;
+    }
+    drop_run = dm == ~0ull ? drop_run + 64 : (int)__builtin_clzll(~dm);   // dropped bytes ending the window
+    if (hp) {
+      if (text || (reached && kind == 0)) hp[at] = (uint32_t)p;
+      if (reached && kind == 1) {
+        for (int k = 0; k < plen; ++k) hp[at + k] = (uint32_t)(p + k);
+        const int tl = S.len[j];
+        if (tl - plen == 1 || plen > tl) novec = 1;
+      }
+    }
     if (text) {
       o[at] = (uint8_t)c;
-      f[at] = (uint8_t)dprev;
+      f[at] = (uint8_t)(dprev ? 3 : 0);          // bit 1: the byte after a dropped '&'
+
       // plain characters: well formed, and the same lowering in HTML mode
       if (c < 0x80) {
         bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
@@ -252,7 +281,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
       }
     } else if (reached && kind == 0) {
       o[at] = ' ';
-      f[at] = (uint8_t)dprev;
+      f[at] = (uint8_t)(dprev ? 3 : 0);
     } else if (reached && kind == 1) {
       const uint32_t d = S.dec[j];
       for (int k = 0; k < plen; ++k) {
@@ -270,9 +299,12 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
   for (int p = q + lane; p < L; p += 64) {
     o[p] = ' ';
     f[p] = 0;
+    if (hp) hp[p] = (uint32_t)L;
   }
   bad |= wsum(conts - need) != 0 ? 1 : 0;                      // every continuation byte claimed
-  if (__ballot(bad != 0) == 0 && lane == 0) special[i] = (uint8_t)((sp & ~kSpecialHtml) | kSpecialRewritten);
+  const bool nv = __ballot(novec != 0) != 0;
+  if (__ballot(bad != 0) == 0 && lane == 0)
+    special[i] = (uint8_t)((sp & ~kSpecialHtml) | kSpecialRewritten | (nv ? kSpecialNoVec : 0));
 }
 
 __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables* __restrict__ Tp,
@@ -280,6 +312,7 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
                                                                const uint64_t* __restrict__ offs, int n,
                                                                uint8_t* __restrict__ special,
                                                                uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
+                                                               uint32_t* __restrict__ hpos, uint32_t* __restrict__ hgap,
                                                                unsigned long long* __restrict__ prof) {
   __shared__ HtmlSmem smem[kHtmlWPB];
   __shared__ TagTables tt;
@@ -303,7 +336,7 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
     if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: k_general
     const int L = (int)len64;
     if (L > kHtmlStage) {
-      rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, prof, am0, am1, lane);
+      rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, hpos, hgap, prof, am0, am1, lane);
     } else {
       // the page into LDS (from aligned dwords), NUL padded
       const uint8_t* g = buf + a;
@@ -314,7 +347,7 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
         *reinterpret_cast<uint32_t*>(&S.text[p]) = v;
       }
       wsync();
-      rewrite_page<true>(T, tt, S, S.text, L, a, i, sp, special, hbuf, hflag, prof, am0, am1, lane);
+      rewrite_page<true>(T, tt, S, S.text, L, a, i, sp, special, hbuf, hflag, hpos, hgap, prof, am0, am1, lane);
     }
     wsync();
   }

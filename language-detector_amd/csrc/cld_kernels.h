@@ -25,7 +25,9 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.
-enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2, kSpecialRewritten = 4 };
+// kSpecialNoVec (vec mode): a rewritten page whose offset map the parallel
+// vec kernel cannot reproduce (cld_html.hip); it keeps the sequential kernel.
+enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2, kSpecialRewritten = 4, kSpecialNoVec = 8 };
 // k_long: waves per workgroup
 constexpr int kLongWPB = 4;
 
@@ -53,6 +55,7 @@ hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counter
 hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                                cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
                                uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
+                               const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos, const uint32_t* hgap,
                                cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s);
 hipError_t cld_launch_vec_gather(const cld_chunk* pool, const uint64_t* pool_off, const int32_t* n_chunks,
                                  const uint64_t* pos, int n, cld_chunk* dst, hipStream_t s);
@@ -71,9 +74,11 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
 // text (cld_html.hip): hbuf / hflag are indexed like buf (offs); special is
 // updated in place (kSpecialHtml -> kSpecialRewritten for each rewritten page);
 // prof (nullable, CLD_PROFILE_STAGES=1): cycles of step 2 summed into prof[0].
+// hpos (nullable, vec mode): per rewritten byte, its page offset for MapBack;
+// hgap (with hpos): at a byte that follows dropped '&'s, where they began.
 hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
-                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, unsigned long long* prof,
-                                   hipStream_t s);
+                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, uint32_t* hpos, uint32_t* hgap,
+                                   unsigned long long* prof, hipStream_t s);
 size_t cld_wave_smem_bytes();
 hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,

@@ -237,9 +237,12 @@ __global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restr
                                                   uint32_t* __restrict__ counters, uint32_t* __restrict__ long_list,
                                                   uint32_t* __restrict__ gen_list) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool html = i < n && special && (special[i] & kSpecialHtml);
-  wave_append(html, &counters[kCtrRequeue2], gen_list, (uint32_t)i, nullptr);
-  wave_append(i < n && !html, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
+  // HTML pages the rewrite did not take (still kSpecialHtml) or whose offset
+  // map it flagged (kSpecialNoVec) go to the sequential kernel
+  const uint8_t sp = (i < n && special) ? special[i] : (uint8_t)0;
+  const bool seq = i < n && (sp & (kSpecialHtml | kSpecialNoVec));
+  wave_append(seq, &counters[kCtrRequeue2], gen_list, (uint32_t)i, &counters[kCtrSpecial]);
+  wave_append(i < n && !seq, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
 }
 
 // Routing before k_wave, one thread per document: HTML documents to
@@ -287,7 +290,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   const uint8_t* __restrict__ hbuf, const uint8_t* __restrict__ hflag,
                                                   uint32_t fault_doc, uint8_t* __restrict__ vslots,
                                                   cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
-                                                  int32_t* __restrict__ n_chunks) {
+                                                  int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ hpos,
+                                                  const uint32_t* __restrict__ hgap) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -330,12 +334,15 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
       V.cap = reg > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)reg;
       V.n = 0;
       V.over = false;
-      V.doc = buf + a;
+      V.doc = buf + a;                           // (the page as given: the vector maps into it)
       V.L = (int)len;
       V.last_off = V.last_bytes = V.last_lang = 0;
+      V.hpos = rw ? hpos + a : nullptr;           // a rewritten HTML page: rewritten byte -> page offset
+      V.hgap = rw ? hgap + a : nullptr;
       if (exact && len <= (uint64_t)lng::kDocCap)
-        passes = lng::detect<DIAG, true>(T, buf + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
-                                         (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, &V);
+        passes = lng::detect<DIAG, true>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i,
+                                         cflags, (spi & kSpecialPriors) ? priors + 16ull * i : nullptr,
+                                         rw ? hflag + a : nullptr, &V);
       if (lane == 0 && passes >= 1 && passes <= 3) n_chunks[i] = V.over ? -1 : V.n;
     } else {
       if (exact && len <= (uint64_t)lng::kDocCap)
@@ -510,11 +517,11 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -531,12 +538,13 @@ hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counter
 hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                                cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
                                uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
+                               const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos, const uint32_t* hgap,
                                cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                     requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, nullptr,
-                     nullptr, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks);
+                     requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
+                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap);
   return hipGetLastError();
 }
 
@@ -583,12 +591,12 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
 }
 
 hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
-                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, unsigned long long* prof,
-                                   hipStream_t s) {
+                                   uint8_t* special, uint8_t* hbuf, uint8_t* hflag, uint32_t* hpos, uint32_t* hgap,
+                                   unsigned long long* prof, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int blocks = std::min((n + cld::kHtmlWPB - 1) / cld::kHtmlWPB, 2048);   // persistent: pages by stride
   hipLaunchKernelGGL(cld::k_html_rewrite, dim3(blocks), dim3(64 * cld::kHtmlWPB), 0, s, d_T, buf, offs, n, special,
-                     hbuf, hflag, prof);
+                     hbuf, hflag, hpos, hgap, prof);
   return hipGetLastError();
 }
 

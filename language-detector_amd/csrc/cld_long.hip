@@ -192,6 +192,8 @@ struct VecState {                                      // wave-uniform
   const uint8_t* doc;
   int L;
   int last_off, last_bytes, last_lang;                 // v[n - 1], mirrored
+  const uint32_t* hpos;                                // a rewritten HTML page: byte -> page offset, else null
+  const uint32_t* hgap;                                //   and where dropped '&'s before a byte began
 };
 
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
@@ -614,9 +616,13 @@ __device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
   return r < L ? r : L;
 }
 
+// vec mode: omap receives map2original_'s MapBack per span text byte; hpos
+// (a rewritten HTML page, cld_html.hip) maps each byte of dv to its offset in
+// the page as given -- offsets in omap are always page offsets.
 template <bool VEC = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
-                         int& status, int lane, uint32_t* omap = nullptr) {
+                         int& status, int lane, uint32_t* omap = nullptr, const uint32_t* hpos = nullptr,
+                         const uint32_t* hgap = nullptr) {
   lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
@@ -644,12 +650,15 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       if (xc + nc > L) dend = xc + nc;
     }
   }
+  // position r of dv -> page offset (past the end: where the scan stops)
+  auto orig = [&](int r) -> int { return r >= L ? dend : (hpos ? (int)gld(hpos + r) : r); };
   if constexpr (VEC) {
     // map2original_ at the leading space (getonescriptspan.cc:835-848):
     // Delete(offset) Delete(skip) Insert(1) maps it past the skipped bytes, to
     // the first letter q; skip == 1 is a Copy(1) of the skipped byte; and
     // Delete(1) Insert(1) (offset 1, skip 0) merges into Copy(1) of byte 0
-    if (lane == 0) omap[0] = (uint32_t)((q - next == 1) ? next : (q == 1 ? 0 : q));
+    const int n0 = next == 0 ? 0 : orig(next), q0 = orig(q);
+    if (lane == 0) omap[0] = (uint32_t)((q0 - n0 == 1) ? n0 : (q0 == 1 && n0 == 1 ? 0 : q0));
   }
   int put = 1, lpos = 1, grow = 0, bad = 0, nxt = L, cutx = -1;
   bool run = false;
@@ -742,14 +751,21 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     if constexpr (VEC) {
       if (out_chr && olen != n) bad = 1;         // map2uplow_ not the identity: the sequential kernel maps it
       if (out_chr)
-        for (int k = 0; k < olen; ++k) omap[lpos + opre + k] = (uint32_t)(x + k);   // Copy
+        for (int k = 0; k < olen; ++k) omap[lpos + opre + k] = (uint32_t)orig(x + k);   // Copy
       if (act && (sep || hard_here)) {
         // the run's ' ': Delete(gap) then Insert(1) maps it to the letter after
         // the gap; a gap of one byte makes that a Copy(1) of the gap byte, no
         // gap an Insert at the run end (:955-993)
-        const int from = sep ? x : x + n;
-        int nl = next_stop(S.lsm, from, L);
-        if (nl >= L) nl = dend;
+        const int fr = sep ? x : x + n;
+        const int nl = orig(next_stop(S.lsm, fr, L));
+        int from = orig(fr);
+        // dropped '&'s just before the break (hflag bit 1 on the byte after
+        // them) are deleted in the letter loop, and that Delete merges with
+        // the gap's: the gap starts where they began (hgap)
+        if (dv.hf && fr < L && (gld(dv.hf + fr) & 2)) {
+          if (sep) from = (int)gld(hgap + fr);
+          else bad = 1;                          // (after the hard limit: the sequential kernel)
+        }
         omap[lpos + opre + olen] = (uint32_t)(nl - from >= 2 ? nl : from);
       }
     }
@@ -769,7 +785,13 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
       const int xs = (w << 6) + stop;
       if ((Hm >> stop) & 1) nxt = find_first_g(S.lsm, xs + rdl(n, stop), L);
       else if ((Sm >> stop) & 1) nxt = find_first_g(S.lsm, xs, L);   // the gap scan starts at the break char
-      else nxt = xs;                                                  // another script's letter stop
+      else {
+        nxt = xs;                                                     // another script's letter stop
+        // vec mode: dropped '&'s right before it may stop the reference's scan
+        // at the first of them (a stale script after a foreign letter,
+        // getonescriptspan.cc:876-931), one offset earlier: the sequential kernel
+        if (VEC && dv.hf && (gld(dv.hf + xs) & 2)) bad = 1;
+      }
       break;
     }
     if (evm) run = (Om >> topbit(evm)) & 1;
@@ -810,7 +832,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     lpos -= 3;                                                        // text_bytes = filled - 3
   } else {
     for (int k = lane; k < 40; k += 64) lb[lpos + k] = k < 3 ? ' ' : 0;   // "   " (lowered pads), NULs
-    if (VEC && lane < 4) omap[lpos + lane] = (uint32_t)(nxt >= L ? dend : nxt);   // Insert(4): where the scan stopped
+    if (VEC && lane < 4) omap[lpos + lane] = (uint32_t)orig(nxt);     // Insert(4): where the scan stopped
   }
   // the reference's lowercaser would stop early (kExitDstSpaceFull) only for
   // spans near the 40 KB limit that also grow; re-queue those.
@@ -2520,7 +2542,8 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
-        tb = next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr);
+        tb = next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr, VEC ? V->hpos : nullptr,
+                            VEC ? V->hgap : nullptr);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {

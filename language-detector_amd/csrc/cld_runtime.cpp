@@ -371,6 +371,7 @@ struct Device {
   uint8_t* d_sbuf = nullptr; size_t sbuf_cap = 0;        // prepared text (CLD_FLAG_STRIP_EXTRAS / CSTRING)
   uint8_t* d_hbuf = nullptr; size_t hbuf_cap = 0;        // HTML pages rewritten into plain text (cld_html.hip)
   uint8_t* d_hflag = nullptr; size_t hflag_cap = 0;      //   and their entity lookahead marks
+  uint32_t* d_hpos = nullptr; size_t hpos_cap = 0;       //   and (vec mode) each byte's page offset
   uint64_t* d_soffs = nullptr; size_t soffs_cap = 0;
   uint8_t* d_sscr = nullptr; size_t sscr_cap = 0;
   hipEvent_t ev[4]{};
@@ -644,7 +645,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   HIP_OK(hipEventRecord(ev[0], s));
   if (hbuf)
     HIP_OK(cld_launch_html_rewrite(d->d_T, buf, offs, (int)n, const_cast<uint8_t*>(special), const_cast<uint8_t*>(hbuf),
-                                   const_cast<uint8_t*>(hflag), d->d_prof ? d->d_prof + 7 : nullptr, s));
+                                   const_cast<uint8_t*>(hflag), nullptr, nullptr, d->d_prof ? d->d_prof + 7 : nullptr, s));
   // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
@@ -1106,11 +1107,30 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
       if (grow(&d->d_requeue, &d->requeue_cap, m) || grow(&d->d_requeue2, &d->requeue2_cap, m) ||
           grow(&d->d_lsorted, &d->lsorted_cap, m) || grow(&d->d_lkey, &d->lkey_cap, m))
         return CLD_ENOMEM;
+      // HTML pages: rewritten into plain text with each byte's page offset
+      // (cld_html.hip), then scored by k_long<VEC> like plain documents
+      const uint8_t* hb = nullptr;
+      const uint8_t* hf = nullptr;
+      const uint32_t* hpz = nullptr;
+      const uint32_t* hgz = nullptr;
+      if (sp) {
+        if (grow(&d->d_hbuf, &d->hbuf_cap, std::max<size_t>(bytes, 1)) ||
+            grow(&d->d_hflag, &d->hflag_cap, std::max<size_t>(bytes, 1)) ||
+            grow(&d->d_hpos, &d->hpos_cap, 2 * std::max<size_t>(bytes, 1)))
+          return CLD_ENOMEM;
+        hb = d->d_hbuf - base;
+        hf = d->d_hflag - base;
+        hpz = d->d_hpos - base;
+        hgz = d->d_hpos + std::max<size_t>(bytes, 1) - base;
+        HIP_OK(cld_launch_html_rewrite(d->d_T, V.in - base, V.offs, (int)m, V.sp, const_cast<uint8_t*>(hb),
+                                       const_cast<uint8_t*>(hf), const_cast<uint32_t*>(hpz),
+                                       const_cast<uint32_t*>(hgz), nullptr, s));
+      }
       HIP_OK(cld_launch_route_vec((int)m, sp ? V.sp : nullptr, d->d_counters, d->d_requeue, d->d_requeue2, s));
       HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
       HIP_OK(cld_launch_long_vec(d->d_T, V.in - base, V.offs, d->d_lsorted, V.out, d->d_slots, V.vslots, d->n_slots,
                                  d->d_requeue2, d->d_counters, cflags & kCldFlags, sp ? V.sp : nullptr,
-                                 pr ? V.pri : nullptr, V.pool, V.pool_off, V.nch, s));
+                                 pr ? V.pri : nullptr, hb, hf, hpz, hgz, V.pool, V.pool_off, V.nch, s));
       HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes,
                                     d->d_counters, sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off,
                                     V.nch, d->d_requeue2, cflags & kCldFlags, d->d_counters + kCtrRequeue2, s));
@@ -1417,7 +1437,7 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_blob); (void)hipFree((void*)d->T.cpt); (void)hipFree((void*)d->T.keytab); (void)hipFree((void*)d->T.compat.adds); (void)hipFree(d->d_T); (void)hipFree(d->d_arena); (void)hipFree(d->d_counters);
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
-    (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag);
+    (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag); (void)hipFree(d->d_hpos);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);

@@ -19,13 +19,14 @@ ref = refcld.instance(os.environ["CLD_MI355X_TABLES"])
 cld_amd.init_device(0)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
-buf, offs = corpus.GENERATORS[cfg](n)
-res, chunks, coffs = cld_amd.detect_batch_vec(buf=buf, offsets=offs)
+html = cfg == "html"
+buf, offs = corpus.html(n, seed=78) if html else corpus.GENERATORS[cfg](n)
+res, chunks, coffs = cld_amd.detect_batch_vec(buf=buf, offsets=offs, html=html)
 shown = 0
 kinds = {}
 for i in range(n):
     doc = bytes(buf[offs[i]:offs[i + 1]])
-    rb, cb = ref.detect_vec(doc)
+    rb, cb = ref.detect_vec(doc, plain=not html)
     g = [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]]
     w = [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in cb]
     fd = [f for f in FIELDS if not np.array_equal(np.asarray(res[i][f], np.float64), np.asarray(rb[f], np.float64))]
@@ -38,6 +39,6 @@ for i in range(n):
         print(json.dumps({"doc": i, "len": len(doc), "fields": fd,
                           "gpu": {f: np.asarray(res[i][f]).tolist() for f in FIELDS},
                           "ref": {f: np.asarray(rb[f]).tolist() for f in FIELDS},
-                          "gpu_vec": g[:40], "ref_vec": w[:40], "text": doc[:600].decode("utf-8", "replace")},
+                          "gpu_vec": g[:40], "ref_vec": w[:40], "text": doc[:3000].decode("utf-8", "replace")},
                          ensure_ascii=False), flush=True)
 print(json.dumps({"differing_kinds": kinds}))
