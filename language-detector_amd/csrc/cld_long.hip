@@ -790,7 +790,15 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         // vec mode: dropped '&'s right before it may stop the reference's scan
         // at the first of them (a stale script after a foreign letter,
         // getonescriptspan.cc:876-931), one offset earlier: the sequential kernel
-        if (VEC && dv.hf && (gld(dv.hf + xs) & 2)) bad = 1;
+        if (VEC && dv.hf && (gld(dv.hf + xs) & 2)) {
+          // (only when the run's last character is a letter of another script
+          // -- the single-letter continuation -- is the reference's script
+          // stale there; after a letter of the span's own script it consumes them)
+          int pc = xs - 1;
+          while (pc > 0 && (dv.p[pc] & 0xC0) == 0x80) --pc;
+          const int scp = pc >= 0 ? script_num(T, dv, pc) : 0;
+          if (scp != 0 && scp != common && scp != ss && scp != inherited) bad = 1;
+        }
       }
       break;
     }

@@ -1,6 +1,7 @@
 """Full-size parity against the reference CLD2 itself, on the tree as built:
 every document of BASELINE's C2 (1M tweets), C3 (100K 16 KB pages) and C4
-(1.1M CJK-heavy documents), and 200K documents of C5's stream, through the
+(1.1M CJK-heavy documents), 200K documents of C5's stream, and 100K HTML pages
+(is_plain_text = false, cld_detect_batch_ex), through the
 product's batch entry point (cld_detect_batch: routing, k_wave, k_long,
 k_general) and through oracle/_ref/librefcld2.so (the reference's own sources
 in dynamic-data mode, 16 host threads), every result field compared.  Twice:
@@ -32,14 +33,15 @@ def ub_docs(buf, offs):
 
 
 @pytest.mark.timeout(900)                     # (the first one may wait for its corpus generator)
-@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5", "html"])
 def test_full_size_equals_reference(gpu, ref_tables, name):
     label, ref = ref_tables
     buf, offs = fullsize.load(name)
     n = len(offs) - 1
-    got = gpu.detect_batch(buf=buf, offsets=offs)
+    html = name == "html"                       # is_plain_text = false (cld_detect_batch_ex, CLD_FLAG_HTML)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True) if html else gpu.detect_batch(buf=buf, offsets=offs)
     st = gpu.last_stats(0)
-    want = ref.detect_batch(buf, offs, threads=16)
+    want = ref.detect_batch(buf, offs, plain=np.zeros(n, np.uint8) if html else None, threads=16)
     bad = np.zeros(n, bool)
     for f in FIELDS:
         bad |= (got[f].astype(np.float64) != want[f].astype(np.float64)).reshape(n, -1).any(axis=1)
@@ -55,7 +57,7 @@ def test_full_size_equals_reference(gpu, ref_tables, name):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5", "html"])
 def test_full_size_vectors_equal_reference(gpu, ref_tables, name):
     """cld_detect_batch_vec on the same corpora: every result field and every
     ResultChunkVector equal to the reference's ExtDetectLanguageSummary with a
@@ -65,9 +67,10 @@ def test_full_size_vectors_equal_reference(gpu, ref_tables, name):
     label, ref = ref_tables
     buf, offs = fullsize.load(name)
     n = len(offs) - 1
-    res, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs)
+    html = name == "html"
+    res, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs, html=html)
     st = gpu.last_stats(0)
-    rres, rch, rco = ref.detect_batch_vec(buf, offs, threads=16)
+    rres, rch, rco = ref.detect_batch_vec(buf, offs, plain=np.zeros(n, np.uint8) if html else None, threads=16)
     bad = np.zeros(n, bool)
     for f in FIELDS:
         bad |= (res[f].astype(np.float64) != rres[f].astype(np.float64)).reshape(n, -1).any(axis=1)
