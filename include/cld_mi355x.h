@@ -155,7 +155,7 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * (n entries).  Host buffers; not retained after return.  Blocks until the
  * results are in `out`.  Documents are sharded across the initialised GPUs
  * by estimated cost; each shard streams through the GPU in chunks of <= 64 MB /
- * 256K documents (pinned staging, upload / kernels / download overlapped on
+ * 512K documents (pinned staging, upload / kernels / download overlapped on
  * three streams).  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING and
  * CLD_FLAG_SCORE_AS_QUADS / CLD_FLAG_BEST_EFFORT (above).  Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,

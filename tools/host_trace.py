@@ -21,8 +21,12 @@ pb[:] = buf
 po = cld_amd.host_array(len(offs), np.uint64)
 po[:] = offs
 pout = cld_amd.host_array(n, cld_amd.RESULT_DTYPE)
+pageable = os.environ.get("HOST_TRACE_PAGEABLE") == "1"     # as bench.py's pageable leg: numpy buffers
 for i in range(6):
     t0 = time.perf_counter()
-    rc = cld_amd.lib().cld_detect_batch(pb.ctypes.data, po.ctypes.data, n, pout.ctypes.data, 0)
-    assert rc == 0
+    if pageable:
+        cld_amd.detect_batch(buf=buf, offsets=offs)
+    else:
+        rc = cld_amd.lib().cld_detect_batch(pb.ctypes.data, po.ctypes.data, n, pout.ctypes.data, 0)
+        assert rc == 0
     print("call %d: %.3f ms" % (i, (time.perf_counter() - t0) * 1e3), flush=True)
