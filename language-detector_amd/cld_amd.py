@@ -228,16 +228,21 @@ def pack(docs):
     return buf, offs
 
 
-def detect_batch(docs=None, buf=None, offsets=None, flags=0):
+def detect_batch(docs=None, buf=None, offsets=None, flags=0, out=None):
     """One DetectLanguageSummaryV2 per document; flags = FLAG_STRIP_EXTRAS | FLAG_CSTRING
     prepares each text as POST / does before detecting (handlers.go:150-151);
-    FLAG_SCORE_AS_QUADS / FLAG_BEST_EFFORT are CLD2's own flags."""
+    FLAG_SCORE_AS_QUADS / FLAG_BEST_EFFORT are CLD2's own flags.  out: an
+    existing contiguous RESULT_DTYPE array of n entries to fill (a caller that
+    reuses its result buffer, as a service would), else a new one."""
     if docs is not None:
         buf, offsets = pack(docs)
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = len(offsets) - 1
-    out = np.zeros(n, dtype=RESULT_DTYPE)
+    if out is None:
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+    elif out.dtype != RESULT_DTYPE or out.shape != (n,) or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
+        raise ValueError("out must be a writeable contiguous array of %d RESULT_DTYPE entries" % n)
     if n == 0:
         return out
     bptr = buf.ctypes.data if buf.size else ctypes.addressof(ctypes.c_uint8(0))

@@ -69,7 +69,7 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
                            int special_ctr, uint32_t cflags, const uint32_t* priors, const uint8_t* hbuf,
-                           const uint8_t* hflag, hipStream_t s);
+                           const uint8_t* hflag, uint32_t* hist2, hipStream_t s);
 // HTML documents of the batch (special & kSpecialHtml) rewritten into plain
 // text (cld_html.hip): hbuf / hflag are indexed like buf (offs); special is
 // updated in place (kSpecialHtml -> kSpecialRewritten for each rewritten page);
@@ -85,8 +85,9 @@ hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const ui
                               uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
                               const uint8_t* special, const uint32_t* priors, uint32_t cflags, uint32_t fault_doc,
                               hipStream_t s);
+// (hist2: zeroed by k_route when cld_launch_wave was given it: zeroed = true)
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
-                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s);
+                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, bool zeroed, hipStream_t s);
 size_t cld_long_slot_bytes();
 size_t cld_cpt_entries();
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s);

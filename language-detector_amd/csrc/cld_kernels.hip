@@ -245,15 +245,21 @@ __global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restr
   wave_append(i < n && !seq, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
 }
 
+constexpr int kLenBuckets = 64;
+
 // Routing before k_wave, one thread per document: HTML documents to
 // k_general's list, documents longer than k_wave's CAP to k_long's, each with
 // one atomic per wavefront instead of one per document (a batch of 100K pages
-// used to queue every page through the same counter from k_wave).
+// used to queue every page through the same counter from k_wave).  Block 0
+// also zeroes k_len_hist's histogram and cursors (hist2, nullable): one
+// launch fewer per batch than a memset.
 __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs, int n,
                                               const uint8_t* __restrict__ special, int cap,
                                               uint32_t* __restrict__ counters, uint32_t* __restrict__ requeue_list,
-                                              uint32_t* __restrict__ special_list, int special_ctr) {
+                                              uint32_t* __restrict__ special_list, int special_ctr,
+                                              uint32_t* __restrict__ hist2) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hist2 && blockIdx.x == 0 && threadIdx.x < 2 * kLenBuckets) hist2[threadIdx.x] = 0;
   bool html = false, lng = false;
   if (i < n) {
     html = special && (special[i] & kSpecialHtml);
@@ -370,7 +376,6 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
 // documents a wave picks up are short ones and the grid drains evenly.  The
 // order inside a bucket is whatever the atomics give; a document's result
 // never depends on which wave scored it or when.
-constexpr int kLenBuckets = 64;
 __device__ __forceinline__ uint32_t len_bucket(uint64_t len) {
   const uint64_t b = len >> 10;
   return (uint32_t)(kLenBuckets - 1) - (uint32_t)(b < kLenBuckets - 1 ? b : kLenBuckets - 1);
@@ -492,10 +497,13 @@ hipError_t cld_build_keytab(const DevTables* T, uint64_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
-                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, hipStream_t s) {
+                                 uint8_t* key, uint32_t* hist2, uint32_t* sorted, bool zeroed, hipStream_t s) {
   // hist2: 2 * kLenBuckets u32 (histogram, then scatter cursors), zeroed here
-  hipError_t e = hipMemsetAsync(hist2, 0, 2 * cld::kLenBuckets * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
+  // unless k_route already did (zeroed)
+  if (!zeroed) {
+    hipError_t e = hipMemsetAsync(hist2, 0, 2 * cld::kLenBuckets * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(cld::k_len_hist, dim3(512), dim3(256), 0, s, offs, list, counters, key, hist2);
   hipLaunchKernelGGL(cld::k_len_scatter, dim3(512), dim3(256), 0, s, list, counters, key, hist2,
                      hist2 + cld::kLenBuckets, sorted);
@@ -579,10 +587,10 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
                            cld_result* out, uint32_t* requeue_list, uint32_t* counters,
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
                            int special_ctr, uint32_t cflags, const uint32_t* priors, const uint8_t* hbuf,
-                           const uint8_t* hflag, hipStream_t s) {
+                           const uint8_t* hflag, uint32_t* hist2, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(cld::k_route, dim3((n + 255) / 256), dim3(256), 0, s, offs, n, special, kWaveCap, counters,
-                     requeue_list, special_list, special_ctr);
+                     requeue_list, special_list, special_ctr, hist2);
   const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;   // k_wave's XCD slices
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,

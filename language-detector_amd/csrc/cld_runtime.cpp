@@ -415,6 +415,8 @@ struct Device {
   hipStream_t up_stream = nullptr, down_stream = nullptr;
   uint32_t* h_ctr = nullptr;        // pinned: per-chunk counter snapshots (kCtrSlots each)
   size_t h_ctr_cap = 0;
+  uint32_t* d_ctrs = nullptr;       // device: per-chunk counters of one streamed call (kCtrSlots each)
+  size_t ctrs_cap = 0;
   // ResultChunkVector mode (cld_detect_batch_vec): its own lane arena, made on first use
   struct Vec {
     uint8_t* arena = nullptr; uint64_t stride = 0; int lanes = 0;
@@ -628,7 +630,7 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 // document bytes span [html_base, html_base + html_bytes) of the offsets.
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
             const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0,
-            uint64_t html_base = 0, uint64_t html_bytes = 0) {
+            uint64_t html_base = 0, uint64_t html_bytes = 0, uint32_t* ctr = nullptr) {
   cflags &= kCldFlags;
   const uint8_t *hbuf = nullptr, *hflag = nullptr;
   if (special && html_bytes) {
@@ -649,7 +651,13 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   }
   auto& ev = d->ev_pool[d->ev_used++];
   HIP_OK(hipStreamWaitEvent(s, d->done, 0));   // serialise with the previous batch's scratch use
-  HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
+  // counters: the device's own (zeroed here), or the caller's region (ctr,
+  // kCtrSlots words, zeroed by the caller: the streamed host path zeroes one
+  // region per chunk in a single memset and reads them back in one copy)
+  if (!ctr) {
+    ctr = d->d_counters;
+    HIP_OK(hipMemsetAsync(ctr, 0, kCtrSlots * sizeof(uint32_t), s));
+  }
   if (d->d_dbg) HIP_OK(hipMemsetAsync(d->d_dbg, 0, 4, s));
   HIP_OK(hipEventRecord(ev[0], s));
   if (hbuf)
@@ -658,26 +666,27 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
-  HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, d->d_counters, d->d_prof, special, sp_list,
-                         sp_ctr, cflags, priors, hbuf, hflag, s));
+  HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, ctr, d->d_prof, special, sp_list,
+                         sp_ctr, cflags, priors, hbuf, hflag,
+                         (d->n_slots > 0 && d->long_order) ? d->d_lhist : nullptr, s));
   HIP_OK(hipEventRecord(ev[1], s));
   if (d->n_slots > 0) {
     const uint32_t* list = d->d_requeue;
     if (d->long_order) {
-      HIP_OK(cld_launch_order_long(offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
+      HIP_OK(cld_launch_order_long(offs, d->d_requeue, ctr, d->d_lkey, d->d_lhist, d->d_lsorted, n > 0, s));
       list = d->d_lsorted;
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
-                           d->d_counters, d->h_trace, d->d_dbg, d->dbg_doc,
+                           ctr, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, d->fault_doc,
                            s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
+                              ctr, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
   } else {
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                              d->d_counters, kCtrRequeue, kCtrDequeue, special, priors, cflags, d->fault_doc, s));
+                              ctr, kCtrRequeue, kCtrDequeue, special, priors, cflags, d->fault_doc, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -790,21 +799,82 @@ int grow_host(T** p, size_t* cap, size_t need) {
   return CLD_OK;
 }
 
-// memcpy split over a few host threads: staging into pinned memory runs on the
-// CPU while the GPU works on the previous chunk, and one core copies ~10 GB/s.
-void par_copy(void* dst, const void* src, size_t n) {
-  const size_t kPiece = 8u << 20;
-  const int t = (int)std::min<size_t>(8, (n + kPiece - 1) / kPiece);
-  if (t <= 1) { memcpy(dst, src, n); return; }
-  std::vector<std::thread> th;
-  const size_t per = (n + t - 1) / t;
-  for (int i = 1; i < t; ++i) {
-    const size_t a = per * i, b = std::min(n, a + per);
-    if (a < b) th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
+// Staging copies (pageable caller memory <-> pinned slots) on a persistent
+// pool of host threads: one core copies only a few GB/s, and spawning threads
+// per chunk cost tens of microseconds each.  The caller takes pieces too; one
+// copy runs at a time (they are bandwidth-bound anyway).  CLD_COPY_THREADS
+// sets the pool size (default min(16, hardware threads)).
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();        // never destroyed: its threads are detached
+    return *p;
   }
-  memcpy(dst, src, std::min(n, per));
-  for (auto& x : th) x.join();
-}
+  void copy(void* dst, const void* src, size_t n) {
+    constexpr size_t kPiece = 2u << 20;
+    Job j{(uint8_t*)dst, (const uint8_t*)src, n, kPiece, (n + kPiece - 1) / kPiece};
+    if (j.pieces <= 1 || workers_ == 0) { memcpy(dst, src, n); return; }
+    std::lock_guard<std::mutex> one(job_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      cur_ = &j;
+      ++gen_;
+    }
+    cv_.notify_all();
+    const size_t mine = j.run();
+    std::unique_lock<std::mutex> lk(mu_);
+    j.done += mine;
+    cur_ = nullptr;                             // late wakers find no job
+    done_cv_.wait(lk, [&] { return j.done == j.pieces && j.refs == 0; });
+  }
+
+ private:
+  struct Job {
+    uint8_t* dst; const uint8_t* src; size_t n, piece, pieces;
+    std::atomic<size_t> next{0};
+    size_t done = 0; int refs = 0;              // under mu_
+    Job(uint8_t* d, const uint8_t* s, size_t n_, size_t p, size_t k) : dst(d), src(s), n(n_), piece(p), pieces(k) {}
+    size_t run() {
+      size_t k = 0;
+      for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < pieces; ++k) {
+        const size_t a = i * piece;
+        memcpy(dst + a, src + a, std::min(piece, n - a));
+      }
+      return k;
+    }
+  };
+  CopyPool() {
+    int t = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = getenv("CLD_COPY_THREADS")) t = std::max(1, atoi(e));
+    workers_ = t - 1;
+    for (int i = 0; i < workers_; ++i) std::thread([this] { work(); }).detach();
+  }
+  void work() {
+    uint64_t seen = 0;
+    for (;;) {
+      Job* j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (!(j = cur_)) continue;
+        ++j->refs;
+      }
+      const size_t k = j->run();
+      std::lock_guard<std::mutex> lk(mu_);
+      j->done += k;
+      --j->refs;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  Job* cur_ = nullptr;
+  uint64_t gen_ = 0;
+  int workers_ = 0;
+};
+
+void par_copy(void* dst, const void* src, size_t n) { CopyPool::get().copy(dst, src, n); }
 
 // Host batch on one device, streamed: documents go in chunks through two
 // slots.  Per chunk: stage into pinned memory (skipped when the caller's
@@ -888,6 +958,30 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   }
   const size_t nch = cut.size() - 1;
   if (grow_host(&d->h_ctr, &d->h_ctr_cap, nch * kCtrSlots)) return CLD_ENOMEM;
+  if (grow(&d->d_ctrs, &d->ctrs_cap, nch * kCtrSlots)) return CLD_ENOMEM;
+  // every chunk's counters zeroed at once here, read back at once after the loop
+  HIP_OK(hipMemsetAsync(d->d_ctrs, 0, nch * kCtrSlots * sizeof(uint32_t), d->stream));
+  // both slots sized for the largest chunk up front (the previous call has
+  // drained, so no buffer is reallocated under a running copy or kernel)
+  size_t max_m = 0;
+  uint64_t max_bytes = 1;
+  for (size_t c = 0; c < nch; ++c) {
+    max_m = std::max(max_m, cut[c + 1] - cut[c]);
+    max_bytes = std::max<uint64_t>(max_bytes, offs[cut[c + 1]] - offs[cut[c]]);
+  }
+  for (Device::Slot& h : d->hs) {
+    int r = grow(&h.d_in, &h.d_in_cap, max_bytes);
+    if (!r) r = grow(&h.d_offs, &h.d_offs_cap, max_m + 1);
+    if (!r) r = grow(&h.d_out, &h.d_out_cap, max_m);
+    if (!r && !in_pinned) r = grow_host(&h.h_in, &h.h_in_cap, max_bytes);
+    if (!r && !in_pinned) r = grow_host(&h.h_offs, &h.h_offs_cap, max_m + 1);
+    if (!r && !out_pinned) r = grow_host(&h.h_out, &h.h_out_cap, max_m);
+    if (!r && special) r = grow(&h.d_sp, &h.d_sp_cap, max_m);
+    if (!r && special) r = grow_host(&h.h_sp, &h.h_sp_cap, max_m);
+    if (!r && priors) r = grow(&h.d_pri, &h.d_pri_cap, 16 * max_m);
+    if (!r && priors) r = grow_host(&h.h_pri, &h.h_pri_cap, 16 * max_m);
+    if (r) return r;
+  }
   int rc = CLD_OK;
   auto deliver = [&](Device::Slot& h) -> int {
     if (!h.busy) return CLD_OK;
@@ -896,34 +990,26 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     h.busy = false;
     return CLD_OK;
   };
+  // Per chunk c in slot c&1: once chunk c-2's UPLOAD is done its pinned
+  // staging is free, so chunk c is staged while the GPU still runs c-2 and
+  // c-1; c-2's results are handed over just before c's download reuses h_out.
   for (size_t c = 0; c < nch && rc == CLD_OK; ++c) {
     Device::Slot& h = d->hs[c & 1];
-    if ((rc = deliver(h))) break;                      // chunk c-2: its results, and its buffers free
+    if (h.busy) HIP_BRK(hipEventSynchronize(h.up))
     const size_t a = cut[c], m = cut[c + 1] - a;
     const uint64_t base = offs[a], bytes = offs[a + m] - base;
-    if ((rc = grow(&h.d_in, &h.d_in_cap, std::max<size_t>(bytes, 1))) ||
-        (rc = grow(&h.d_offs, &h.d_offs_cap, m + 1)) || (rc = grow(&h.d_out, &h.d_out_cap, m)))
-      break;
     const uint8_t* src_in = buf + base;
     const uint64_t* src_offs = offs + a;
     if (!in_pinned) {
-      if ((rc = grow_host(&h.h_in, &h.h_in_cap, std::max<size_t>(bytes, 1))) ||
-          (rc = grow_host(&h.h_offs, &h.h_offs_cap, m + 1)))
-        break;
       par_copy(h.h_in, src_in, bytes);
       memcpy(h.h_offs, src_offs, (m + 1) * sizeof(uint64_t));
       src_in = h.h_in;
       src_offs = h.h_offs;
     }
     cld_result* dst = out + a;
-    if (!out_pinned && (rc = grow_host(&h.h_out, &h.h_out_cap, m))) break;
     if (special) {           // per-document routing bits (and priors) for this chunk, staged pinned
-      if ((rc = grow(&h.d_sp, &h.d_sp_cap, m)) || (rc = grow_host(&h.h_sp, &h.h_sp_cap, m))) break;
       memcpy(h.h_sp, special + a, m);
-      if (priors) {
-        if ((rc = grow(&h.d_pri, &h.d_pri_cap, 16 * m)) || (rc = grow_host(&h.h_pri, &h.h_pri_cap, 16 * m))) break;
-        memcpy(h.h_pri, priors + 16 * a, 16 * m * sizeof(uint32_t));
-      }
+      if (priors) memcpy(h.h_pri, priors + 16 * a, 16 * m * sizeof(uint32_t));
     }
     // upload (after the slot's previous kernels stopped reading its device buffers)
     HIP_BRK(hipStreamWaitEvent(d->up_stream, h.comp, 0))
@@ -940,16 +1026,17 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     const uint8_t* kbuf = h.d_in - base;
     if (flags & kPrepFlags) {
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
-      rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream, nullptr, nullptr, flags);
+      rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream, nullptr, nullptr, flags, 0, 0,
+                   d->d_ctrs + c * kCtrSlots);
     } else {
       rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream, special ? h.d_sp : nullptr,
-                   (special && priors) ? h.d_pri : nullptr, flags, base, (special && html) ? bytes : 0);
+                   (special && priors) ? h.d_pri : nullptr, flags, base, (special && html) ? bytes : 0,
+                   d->d_ctrs + c * kCtrSlots);
     }
     if (rc) break;
-    HIP_BRK(hipMemcpyAsync(d->h_ctr + c * kCtrSlots, d->d_counters, kCtrSlots * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, d->stream))
     HIP_BRK(hipEventRecord(h.comp, d->stream))
-    // download
+    // download (chunk c-2's results out of h_out first)
+    if ((rc = deliver(h))) break;
     HIP_BRK(hipStreamWaitEvent(d->down_stream, h.comp, 0))
     HIP_BRK(hipMemcpyAsync(out_pinned ? dst : h.h_out, h.d_out, m * sizeof(cld_result), hipMemcpyDeviceToHost,
                           d->down_stream))
@@ -959,6 +1046,9 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
     h.busy = true;
   }
   if (rc == CLD_OK && d->h_trace) watch_trace(d, d->stream);
+  if (rc == CLD_OK && hipMemcpyAsync(d->h_ctr, d->d_ctrs, nch * kCtrSlots * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     d->stream) != hipSuccess)
+    rc = CLD_EFAULT;
   for (auto& h : d->hs) {                              // drain (also after an error: no DMA may outlive the call)
     int r = deliver(h);
     if (rc == CLD_OK) rc = r;
@@ -1141,7 +1231,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
                                        const_cast<uint32_t*>(hgz), nullptr, s));
       }
       HIP_OK(cld_launch_route_vec((int)m, sp ? V.sp : nullptr, d->d_counters, d->d_requeue, d->d_requeue2, s));
-      HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, s));
+      HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, false, s));
       HIP_OK(cld_launch_long_vec(d->d_T, V.in - base, V.offs, d->d_lsorted, V.out, d->d_slots, V.vslots, d->n_slots,
                                  d->d_requeue2, d->d_counters, cflags & kCldFlags, sp ? V.sp : nullptr,
                                  pr ? V.pri : nullptr, hb, hf, hpz, hgz, V.pool, V.pool_off, V.nch, s));
@@ -1460,6 +1550,7 @@ void cld_shutdown(void) {
       (void)hipEventDestroy(h.up); (void)hipEventDestroy(h.comp); (void)hipEventDestroy(h.down);
     }
     (void)hipHostFree(d->h_ctr);
+    (void)hipFree(d->d_ctrs);
     for (void* p : {(void*)d->vec.arena, (void*)d->vec.vslots, (void*)d->vec.in, (void*)d->vec.offs, (void*)d->vec.out, (void*)d->vec.sp,
                     (void*)d->vec.pri, (void*)d->vec.pool, (void*)d->vec.pool_off, (void*)d->vec.nch,
                     (void*)d->vec.pos, (void*)d->vec.order, (void*)d->vec.compact})

@@ -22,10 +22,12 @@ po = cld_amd.host_array(len(offs), np.uint64)
 po[:] = offs
 pout = cld_amd.host_array(n, cld_amd.RESULT_DTYPE)
 pageable = os.environ.get("HOST_TRACE_PAGEABLE") == "1"     # as bench.py's pageable leg: numpy buffers
+out = np.zeros(n, dtype=cld_amd.RESULT_DTYPE)
+fresh = os.environ.get("HOST_TRACE_FRESH_OUT") == "1"       # a new result array per call (its page faults)
 for i in range(6):
     t0 = time.perf_counter()
     if pageable:
-        cld_amd.detect_batch(buf=buf, offsets=offs)
+        cld_amd.detect_batch(buf=buf, offsets=offs, out=None if fresh else out)
     else:
         rc = cld_amd.lib().cld_detect_batch(pb.ctypes.data, po.ctypes.data, n, pout.ctypes.data, 0)
         assert rc == 0
