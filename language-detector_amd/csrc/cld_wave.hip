@@ -1230,14 +1230,6 @@ __device__ __forceinline__ SlotRegs load_slots(const DocTote& dt, int lane) {
   r.rl = in ? dt.rel[j] : 0;
   return r;
 }
-__device__ __forceinline__ void store_slots(DocTote& dt, const SlotRegs& r, int lane) {
-  if (lane < 24) {
-    dt.key[lane] = (uint16_t)r.key;
-    dt.value[lane] = r.val;
-    dt.score[lane] = r.sc;
-    dt.rel[lane] = r.rl;
-  }
-}
 
 // DocTote::Sort(3) (tote.cc:221-250) across lanes 0-23, one lane per slot.
 // Pass s of the reference's partial bubble sort swaps slot s with every later
@@ -1293,6 +1285,50 @@ __device__ __forceinline__ void refine_close_pairs_regs(const DevTables& T, Slot
     mv(rdl((int)r.key, from), rdl((int)r.key, to));
     if (lane == to) { r.val += fv; r.sc += fs; r.rl += fr; }
     if (lane == from) { r.key = kUnusedKey; r.sc = 0; r.rl = 0; cs = 0; }   // (value stays, as there)
+  }
+}
+
+// RemoveUnreliableLanguages (compact_lang_det_impl.cc:997-1101) on the slot
+// registers.  todo = the slots unreliable on entry: only they can act, since a
+// merge leaves its target reliable (np >= 41 over at least its own bytes) and
+// empties its source.  They are visited in slot order on scalars and rechecked
+// as the reference does (an earlier merge may have emptied or fixed one); the
+// second loop (drop what is still unreliable) runs across lanes.  The
+// reference's Find on the sorted tote is a linear scan: the first slot whose
+// key matches.  As there, a merge moves reliability and bytes into the score
+// field and leaves value alone.
+__device__ __forceinline__ void remove_unreliable_regs(const DevTables& T, SlotRegs& r, uint64_t todo, int lane) {
+  const int unk = (int)T.unknown_lang;
+  while (todo) {
+    const int s = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int lang = rdl((int)r.key, s);
+    if (lang == kUnusedKey) continue;
+    const int bytes = rdl(r.val, s), reli = rdl(r.rl, s);
+    if (bytes == 0) continue;
+    const int rp = reli / bytes;
+    if (rp >= 41) continue;
+    int alt = unk;
+    if ((uint32_t)lang <= T.hawaiian && (uint32_t)lang < T.n_closest) alt = gld(T.closest + lang);
+    if (alt == unk) continue;
+    const uint64_t am = __ballot(lane < 24 && (int)r.key == alt);
+    if (!am) continue;
+    const int as = __builtin_ctzll(am);
+    const int bytes2 = rdl(r.val, as), reli2 = rdl(r.rl, as);
+    if (bytes2 == 0) continue;
+    const int rp2 = reli2 / bytes2;
+    int to = as, from = s;
+    if (rp2 < rp || (rp2 == rp && lang < alt)) { to = s; from = as; }
+    int np = rp > rp2 ? rp : rp2;
+    if (np < 41) np = 41;
+    const int nbytes = bytes + bytes2;
+    if (lane == from) { r.key = kUnusedKey; r.sc = 0; r.rl = 0; }
+    if (lane == to) { r.sc = nbytes; r.rl = np * nbytes; }
+  }
+  if (lane < 24 && r.key != kUnusedKey && r.val != 0 && r.rl / (r.val ? r.val : 1) < 41) {
+    r.key = kUnusedKey;
+    r.sc = 0;
+    r.rl = 0;
   }
 }
 
@@ -1354,13 +1390,8 @@ __device__ __forceinline__ int finish_document(const DevTables& T, DocTote& dt, 
   if (!best_effort) {
     // RemoveUnreliableLanguages (:997-1101) only when some slot is unreliable
     const bool unrel = lane < 24 && r.key != kUnusedKey && r.val != 0 && r.rl / (r.val ? r.val : 1) < 41;
-    if (__ballot(unrel)) {
-      store_slots(dt, r, lane);
-      if (lane == 0) dt.sorted = 1;                            // (DocTote::Find then scans linearly)
-      wsync();
-      if (lane == 0) remove_unreliable_languages(T, dt);
-      wsync();
-      r = load_slots(dt, lane);
+    if (const uint64_t todo = __ballot(unrel)) {
+      remove_unreliable_regs(T, r, todo, lane);
       sort3_regs(r, lane);
       x = extract_regs(T, r, total, lane, ns);
     }
