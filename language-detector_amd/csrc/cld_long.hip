@@ -122,9 +122,9 @@ struct Slot {
   uint16_t d_hoff[kHB];                  // delta / distinct hit offsets (debug dump only)
   uint16_t x_hoff[kHB];
   uint16_t be_off[kEB];
-  uint64_t be_add[kEB];                  // tote adds per emission (tote_adds), base / delta / distinct
-  uint64_t d_add[kHB];
-  uint64_t x_add[kHB];
+  uint32_t be_ai[kEB];                   // per emission: its tote adds' index in the per-GPU adds
+  uint32_t d_ai[kHB];                    //   table (adds_index), base / delta / distinct
+  uint32_t x_ai[kHB];
 };
 
 // Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4).  The
@@ -1385,25 +1385,48 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
 // The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
 __device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? gld(t.adds + i) : 0ull; }
 
+// Emissions keep 32-bit indices, not the 8-byte adds: the seven tables' adds
+// sit back to back in one per-GPU array that starts at compat's
+// (cld_build_adds), so entry i of table t is adds_index(T, t, i) there, and an
+// emission stream costs 4 bytes of slot per entry instead of 8 (the streams
+// were ~45% of k_long's HBM writes at C3, profiles/round4f_emission_index.txt).
+__device__ __forceinline__ uint32_t adds_index(const DevTables& T, const DevTbl& t, uint32_t i) {
+  return (uint32_t)(t.adds - T.compat.adds) + i;
+}
+__device__ __forceinline__ uint64_t adds_by_index(const DevTables& T, uint32_t g) { return gld(T.compat.adds + g); }
+// A chunk's add before its gather (chunk_ref / resolve_ref): bit 62 marks an
+// index into the adds array; anything else is the add itself (the seed, a
+// prior or a ring boost: tote adds use bits 0-47 and 63, never 62).
+constexpr uint64_t kRefIndex = 1ull << 62;
+__device__ __forceinline__ uint64_t resolve_ref(const DevTables& T, uint64_t r) {
+  return (r & kRefIndex) ? adds_by_index(T, (uint32_t)r) : r;
+}
+
 // Base emissions of one base hit (LinearizeAll, scoreonescriptspan.cc:856-960):
 // one or two langprobs as tote adds, zero langprobs dropped.  ind bit 31
 // selects the second quad table.
-__device__ __forceinline__ void base_adds(const DevTbl& t1, const DevTbl& t2, uint32_t ind, uint64_t& l1, uint64_t& l2) {
+__device__ __forceinline__ void base_adds(const DevTables& T, const DevTbl& t1, const DevTbl& t2, uint32_t ind,
+                                          uint64_t& l1, uint64_t& l2, uint32_t& g1, uint32_t& g2) {
   const DevTbl* lb = &t1;
   if (ind & 0x80000000u) {
     lb = &t2;
     ind &= ~0x80000000u;
   }
   l2 = 0;
+  g2 = 0;
   if (ind < lb->size_one) {
     l1 = adds_at(*lb, ind);
+    g1 = adds_index(T, *lb, ind);
   } else {
     ind += ind - lb->size_one;
     l1 = adds_at(*lb, ind);
     l2 = adds_at(*lb, ind + 1);
+    g1 = adds_index(T, *lb, ind);
+    g2 = g1 + 1;
     if (!(l1 >> 63)) {
       l1 = l2;
       l2 = 0;
+      g1 = g2;
     }
   }
 }
@@ -1504,7 +1527,7 @@ __device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, 
 
 // GetQuadHits for one round from chain entry c0 (cldutil.cc:315-405): probes
 // per entry, the "not one of the last two hits" filter, the 1000-hit cut.
-// Each kept hit's base emissions go straight to be_off / be_add (eb of
+// Each kept hit's base emissions go straight to be_off / be_ai (eb of
 // them), so score_round does not read the hits back; the hit list itself is
 // kept only for the debug dump (D).  Returns the round end (the reference's
 // `next`); c0 advances.
@@ -1587,17 +1610,18 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm
     nb += __popcll(keep);
     {
       uint64_t l1 = 0, l2 = 0;
-      if (kept) base_adds(T.quad, T.quad2, ind, l1, l2);
+      uint32_t g1 = 0, g2 = 0;
+      if (kept) base_adds(T, T.quad, T.quad2, ind, l1, l2, g1, g2);
       const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
       const int o = eb + excl_scan(c, lane);
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)p;
-        S.be_add[o] = l1;
+        S.be_ai[o] = g1;
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)p;
-        S.be_add[o + 1] = l2;
+        S.be_ai[o + 1] = g2;
       }
     }
     if (lastl < 64) {
@@ -1720,16 +1744,16 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& s
       edm = rdl(od + md, 63);
       if (in && (apx >> 63)) {
         S.x_off[ox] = (uint16_t)pws;
-        S.x_add[ox] = apx;
+        S.x_ai[ox] = adds_index(T, T.distinctocta, pp & xm);
         ++ox;
       }
       if (in && (axp >> 63)) {
         S.x_off[ox] = (uint16_t)a;
-        S.x_add[ox] = axp;
+        S.x_ai[ox] = adds_index(T, T.distinctocta, xp & xm);
       }
       if (in && (adp >> 63)) {
         S.d_off[od] = (uint16_t)a;
-        S.d_add[od] = adp;
+        S.d_ai[od] = adds_index(T, T.deltaocta, dp & dmk);
       }
     }
     if (D && lane <= cut) {
@@ -1806,17 +1830,18 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
     nb += __popcll(hm);
     {
       uint64_t l1 = 0, l2 = 0;
-      if (kept) base_adds(T.compat, T.compat, (uint32_t)prop, l1, l2);
+      uint32_t g1 = 0, g2 = 0;
+      if (kept) base_adds(T, T.compat, T.compat, (uint32_t)prop, l1, l2, g1, g2);
       const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
       const int o = eb + excl_scan(c, lane);
       eb = rdl(o + c, 63);
       if (l1 >> 63) {
         S.be_off[o] = (uint16_t)(x + len);
-        S.be_add[o] = l1;
+        S.be_ai[o] = g1;
       }
       if (l2 >> 63) {
         S.be_off[o + 1] = (uint16_t)(x + len);
-        S.be_add[o + 1] = l2;
+        S.be_ai[o + 1] = g2;
       }
     }
     if (lastl < 64) {
@@ -1856,11 +1881,11 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
       exm = rdl(ox + mx, 63);
       if (md) {
         S.d_off[od] = (uint16_t)x;
-        S.d_add[od] = adp;
+        S.d_ai[od] = adds_index(T, T.deltabi, dp & ~T.deltabi.key_mask);
       }
       if (mx) {
         S.x_off[ox] = (uint16_t)x;
-        S.x_add[ox] = axp;
+        S.x_ai[ox] = adds_index(T, T.distinctbi, xp & ~T.distinctbi.key_mask);
       }
     }
     if (D && lane <= cut) {
@@ -1906,20 +1931,22 @@ __device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
 
 // Chunk k's adds (score_round): t < seedn the seed, then its base, delta and
 // distinct emissions, then the four boosts (the last four distinct langprobs
-// so far).  Plain functions rather than lambdas: a captured reference loses
-// its address space, and the slot / LDS reads would become FLAT.
-__device__ __forceinline__ uint64_t chunk_add(const Slot& S, const Smem& s, uint64_t seed, int rs, int t, int k, int tot,
+// so far) -- as refs (kRefIndex): the emissions' gathers are issued later
+// (resolve_ref), once their indices are in.  Plain functions rather than
+// lambdas: a captured reference loses its address space, and the slot / LDS
+// reads would become FLAT.
+__device__ __forceinline__ uint64_t chunk_ref(const Slot& S, const Smem& s, uint64_t seed, int rs, int t, int k, int tot,
                                               int bs, int nB, int ds, int nD, int xs, int nX, int xe) {
   if (t >= tot) return 0ull;
   int u = t;
   const int seedn = k == 0 ? 1 : 0;
   if (u < seedn) return seed;
-  if ((u -= seedn) < nB) return S.be_add[bs + u];
-  if ((u -= nB) < nD) return S.d_add[ds + u];
-  if ((u -= nD) < nX) return S.x_add[xs + u];
+  if ((u -= seedn) < nB) return kRefIndex | S.be_ai[bs + u];
+  if ((u -= nB) < nD) return kRefIndex | S.d_ai[ds + u];
+  if ((u -= nD) < nX) return kRefIndex | S.x_ai[xs + u];
   if (u - nX >= kMaxBoosts) return s.pri_add[rs][u - nX - kMaxBoosts];   // prior boosts (has_pri)
   const int v = xe - kMaxBoosts + (u - nX);
-  return v < 0 ? s.ring[rs][v + kMaxBoosts] : gld(&S.x_add[v]);   // (gld: no LDS/global pointer select)
+  return v < 0 ? s.ring[rs][v + kMaxBoosts] : (kRefIndex | gld(&S.x_ai[v]));   // (gld: no LDS/global pointer select)
 }
 // Chunk plan of k: emission ranges and the number of adds.
 __device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
@@ -2126,24 +2153,27 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
   const uint64_t seed = tote_adds(T, (uint32_t)per_script_number_latin(T, default_language(T, ulscript)) << 8);
   const int rs = ((uint32_t)ulscript == T.latin) ? 0 : 1;
   int ck1 = -1, ck2 = -1, cs1 = 0, cs2 = 0, cgr = 0;   // chunk `lane`: top keys, scores, grams
-  // the first 128 adds of chunk k + 1 are loaded while chunk k is scored
+  // the first 128 adds of chunk k + 1 are loaded while chunk k is scored: their
+  // indices at the top of chunk k, their gathers at its end
   int pbs, pnB, pds, pnD, pxs, pnX, pxe;
   int ptot = chunk_plan(s, K, eb, 0, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-  uint64_t n0 = chunk_add(S, s, seed, rs, lane, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-  uint64_t n1 = chunk_add(S, s, seed, rs, lane + 64, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+  uint64_t n0 = resolve_ref(T, chunk_ref(S, s, seed, rs, lane, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe));
+  uint64_t n1 = resolve_ref(T, chunk_ref(S, s, seed, rs, lane + 64, 0, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe));
   for (int k = 0; k < K; ++k) {
     const int bs = pbs, nB = pnB, ds = pds, nD = pnD, xs = pxs, nX = pnX, xe = pxe, tot = ptot;
     const uint64_t a0 = n0, a1 = n1;
+    uint64_t r0 = 0, r1 = 0;
     if (k + 1 < K) {
       ptot = chunk_plan(s, K, eb, k + 1, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-      n0 = chunk_add(S, s, seed, rs, lane, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
-      n1 = chunk_add(S, s, seed, rs, lane + 64, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      r0 = chunk_ref(S, s, seed, rs, lane, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
+      r1 = chunk_ref(S, s, seed, rs, lane + 64, k + 1, ptot, pbs, pnB, pds, pnD, pxs, pnX, pxe);
     }
     reinterpret_cast<uint4*>(s.tote)[lane] = make_uint4(0, 0, 0, 0);
     wsync();
     const int seedn = k == 0 ? 1 : 0;
     for (int t = lane; t < tot; t += 64) {
-      const uint64_t a = t < 128 ? (t < 64 ? a0 : a1) : chunk_add(S, s, seed, rs, t, k, tot, bs, nB, ds, nD, xs, nX, xe);
+      const uint64_t a = t < 128 ? (t < 64 ? a0 : a1)
+                                 : resolve_ref(T, chunk_ref(S, s, seed, rs, t, k, tot, bs, nB, ds, nD, xs, nX, xe));
       const uint32_t k1 = (uint32_t)a & 0xFF, k2 = (uint32_t)(a >> 16) & 0xFF, k3 = (uint32_t)(a >> 32) & 0xFF;
       // the low half sums the score (read with the reference's uint16 wrap), the
       // high half counts the adds: a group (the 4 keys of one lane) is in use
@@ -2153,6 +2183,10 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       if (k3) atomicAdd(&s.tote[k3], ((uint32_t)(a >> 40) & 0xFF) | 0x10000u);
     }
     const int score_count = nB + seedn;
+    if (k + 1 < K) {
+      n0 = resolve_ref(T, r0);
+      n1 = resolve_ref(T, r1);
+    }
     wsync();
     if (s.has_pri) {                         // the prior whacks zero their key's score (ZeroPSLang :39-42)
       const int wk = lane < 4 ? s.pri_wk[rs][lane] : 0;
@@ -2232,19 +2266,19 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
       const int o = S.be_off[t];
       const int r = 1 + t + count_upto(S.d_off, ed, o, true) + count_upto(S.x_off, ex, o, true);
       vs->lin_off[r] = (uint32_t)o;
-      vs->lin_add[r] = S.be_add[t];
+      vs->lin_add[r] = adds_by_index(T, S.be_ai[t]);
     }
     for (int j = lane; j < ed; j += 64) {
       const int o = S.d_off[j];
       const int r = 1 + j + count_upto(S.x_off, ex, o, false) + count_upto(S.be_off, eb, o, false);
       vs->lin_off[r] = (uint32_t)o;
-      vs->lin_add[r] = S.d_add[j];
+      vs->lin_add[r] = adds_by_index(T, S.d_ai[j]);
     }
     for (int j = lane; j < ex; j += 64) {
       const int o = S.x_off[j];
       const int r = 1 + j + count_upto(S.d_off, ed, o, true) + count_upto(S.be_off, eb, o, false);
       vs->lin_off[r] = (uint32_t)o;
-      vs->lin_add[r] = S.x_add[j];
+      vs->lin_add[r] = adds_by_index(T, S.x_ai[j]);
     }
     gsync();
     // chunk k's first linear entry (chunk_start): the seed and every earlier
@@ -2347,7 +2381,7 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
     uint64_t r4[4];
     for (int i = 0; i < 4; ++i) {
       const int u = ex - kMaxBoosts + i;
-      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : gld(&S.x_add[u]);
+      r4[i] = u < 0 ? s.ring[rs][u + kMaxBoosts] : adds_by_index(T, gld(&S.x_ai[u]));
     }
     for (int i = 0; i < 4; ++i) s.ring[rs][i] = r4[i];
   }
