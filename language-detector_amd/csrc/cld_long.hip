@@ -1382,9 +1382,6 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
   return dst;
 }
 
-// The tote adds of indirect entry i (k_build_adds), as ind_at bounds it.
-__device__ __forceinline__ uint64_t adds_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? gld(t.adds + i) : 0ull; }
-
 // Emissions keep 32-bit indices, not the 8-byte adds: the seven tables' adds
 // sit back to back in one per-GPU array that starts at compat's
 // (cld_build_adds), so entry i of table t is adds_index(T, t, i) there, and an
@@ -1405,8 +1402,11 @@ __device__ __forceinline__ uint64_t resolve_ref(const DevTables& T, uint64_t r) 
 // Base emissions of one base hit (LinearizeAll, scoreonescriptspan.cc:856-960):
 // one or two langprobs as tote adds, zero langprobs dropped.  ind bit 31
 // selects the second quad table.
+// The emission test is the langprob itself (ind_at, 4 bytes): a zero
+// langprob is exactly a zero add (k_build_adds); the adds are gathered only
+// when the chunk is scored (chunk_ref / resolve_ref).
 __device__ __forceinline__ void base_adds(const DevTables& T, const DevTbl& t1, const DevTbl& t2, uint32_t ind,
-                                          uint64_t& l1, uint64_t& l2, uint32_t& g1, uint32_t& g2) {
+                                          uint32_t& l1, uint32_t& l2, uint32_t& g1, uint32_t& g2) {
   const DevTbl* lb = &t1;
   if (ind & 0x80000000u) {
     lb = &t2;
@@ -1415,15 +1415,15 @@ __device__ __forceinline__ void base_adds(const DevTables& T, const DevTbl& t1, 
   l2 = 0;
   g2 = 0;
   if (ind < lb->size_one) {
-    l1 = adds_at(*lb, ind);
+    l1 = ind_at(*lb, ind);
     g1 = adds_index(T, *lb, ind);
   } else {
     ind += ind - lb->size_one;
-    l1 = adds_at(*lb, ind);
-    l2 = adds_at(*lb, ind + 1);
+    l1 = ind_at(*lb, ind);
+    l2 = ind_at(*lb, ind + 1);
     g1 = adds_index(T, *lb, ind);
     g2 = g1 + 1;
-    if (!(l1 >> 63)) {
+    if (!l1) {
       l1 = l2;
       l2 = 0;
       g1 = g2;
@@ -1609,17 +1609,16 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm
     }
     nb += __popcll(keep);
     {
-      uint64_t l1 = 0, l2 = 0;
-      uint32_t g1 = 0, g2 = 0;
+      uint32_t l1 = 0, l2 = 0, g1 = 0, g2 = 0;
       if (kept) base_adds(T, T.quad, T.quad2, ind, l1, l2, g1, g2);
-      const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
+      const int c = (l1 != 0) + (l2 != 0);
       const int o = eb + excl_scan(c, lane);
       eb = rdl(o + c, 63);
-      if (l1 >> 63) {
+      if (l1) {
         S.be_off[o] = (uint16_t)p;
         S.be_ai[o] = g1;
       }
-      if (l2 >> 63) {
+      if (l2) {
         S.be_off[o + 1] = (uint16_t)p;
         S.be_ai[o + 1] = g2;
       }
@@ -1728,30 +1727,30 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& s
     }
     // tote adds of the hits (issued before the cap arithmetic they do not depend on)
     const uint32_t xm = ~T.distinctocta.key_mask, dmk = ~T.deltaocta.key_mask;
-    const uint64_t apx = pp ? adds_at(T.distinctocta, pp & xm) : 0ull;
-    const uint64_t axp = xp ? adds_at(T.distinctocta, xp & xm) : 0ull;
-    const uint64_t adp = dp ? adds_at(T.deltaocta, dp & dmk) : 0ull;
+    const uint32_t apx = pp ? ind_at(T.distinctocta, pp & xm) : 0u;
+    const uint32_t axp = xp ? ind_at(T.distinctocta, xp & xm) : 0u;
+    const uint32_t adp = dp ? ind_at(T.deltaocta, dp & dmk) : 0u;
     const int cx = (pp != 0) + (xp != 0), cd = (dp != 0);
     const int ex = excl_scan(cx, lane), ed = excl_scan(cd, lane);
     const uint64_t capm = __ballot(v && (nx + ex + cx >= kMaxScoringHits - 1 || nd + ed + cd >= kMaxScoringHits));
     const int cut = capm ? __builtin_ctzll(capm) : 64;
     {
       const bool in = lane <= cut;
-      const int mx = in ? (int)(apx >> 63) + (int)(axp >> 63) : 0, md = in ? (int)(adp >> 63) : 0;
+      const int mx = in ? (apx != 0) + (axp != 0) : 0, md = in ? (adp != 0) : 0;
       int ox = exm + excl_scan(mx, lane);
       const int od = edm + excl_scan(md, lane);
       exm = rdl(ox + mx, 63);
       edm = rdl(od + md, 63);
-      if (in && (apx >> 63)) {
+      if (in && apx) {
         S.x_off[ox] = (uint16_t)pws;
         S.x_ai[ox] = adds_index(T, T.distinctocta, pp & xm);
         ++ox;
       }
-      if (in && (axp >> 63)) {
+      if (in && axp) {
         S.x_off[ox] = (uint16_t)a;
         S.x_ai[ox] = adds_index(T, T.distinctocta, xp & xm);
       }
-      if (in && (adp >> 63)) {
+      if (in && adp) {
         S.d_off[od] = (uint16_t)a;
         S.d_ai[od] = adds_index(T, T.deltaocta, dp & dmk);
       }
@@ -1829,17 +1828,16 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
     }
     nb += __popcll(hm);
     {
-      uint64_t l1 = 0, l2 = 0;
-      uint32_t g1 = 0, g2 = 0;
+      uint32_t l1 = 0, l2 = 0, g1 = 0, g2 = 0;
       if (kept) base_adds(T, T.compat, T.compat, (uint32_t)prop, l1, l2, g1, g2);
-      const int c = (int)(l1 >> 63) + (int)(l2 >> 63);
+      const int c = (l1 != 0) + (l2 != 0);
       const int o = eb + excl_scan(c, lane);
       eb = rdl(o + c, 63);
-      if (l1 >> 63) {
+      if (l1) {
         S.be_off[o] = (uint16_t)(x + len);
         S.be_ai[o] = g1;
       }
-      if (l2 >> 63) {
+      if (l2) {
         S.be_off[o + 1] = (uint16_t)(x + len);
         S.be_ai[o + 1] = g2;
       }
@@ -1867,15 +1865,15 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm,
         xp = quad_lookup(T.distinctbi, bh);
       }
     }
-    const uint64_t adp = dp ? adds_at(T.deltabi, dp & ~T.deltabi.key_mask) : 0ull;
-    const uint64_t axp = xp ? adds_at(T.distinctbi, xp & ~T.distinctbi.key_mask) : 0ull;
+    const uint32_t adp = dp ? ind_at(T.deltabi, dp & ~T.deltabi.key_mask) : 0u;
+    const uint32_t axp = xp ? ind_at(T.distinctbi, xp & ~T.distinctbi.key_mask) : 0u;
     const int cd = dp != 0, cx = xp != 0;
     const int ed = excl_scan(cd, lane), ex = excl_scan(cx, lane);
     const uint64_t capm = __ballot(v && (nd + ed + cd >= kMaxScoringHits || nx + ex + cx >= kMaxScoringHits - 1));
     const int cut = capm ? __builtin_ctzll(capm) : 64;
     {
       const bool in = lane <= cut;
-      const int md = in ? (int)(adp >> 63) : 0, mx = in ? (int)(axp >> 63) : 0;
+      const int md = in ? (adp != 0) : 0, mx = in ? (axp != 0) : 0;
       const int od = edm + excl_scan(md, lane), ox = exm + excl_scan(mx, lane);
       edm = rdl(od + md, 63);
       exm = rdl(ox + mx, 63);
