@@ -21,7 +21,8 @@ constexpr int kMaxLgProbScore = 16;
 // kCtrSpecial: HTML / hinted documents the wave kernel sent straight to k_general.
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
        kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
-       kCtrSpecial = 16, kCtrSlots = 32 };
+       kCtrSpecial = 16, kCtrSpecTake = 17 /* k_long: speculative pass-2 results taken */,
+       kCtrSpecDone = 18 /* k_long: waves finished (speculating launches) */, kCtrSlots = 32 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.
@@ -114,6 +115,10 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           hipStream_t s);
+                           cld_result* spec_out, uint32_t* spec_take, hipStream_t s);
+// spec_out / spec_take (nullable: no speculation): cld_long_spec_docs(n_slots)
+// results and u32 entries, k_long's speculative pass-2 results for the
+// longest documents of a small batch.
+size_t cld_long_spec_docs(int n_slots);
 }
 #endif

@@ -281,6 +281,11 @@ __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs
 #ifndef LNG_WPS
 #define LNG_WPS 4
 #endif
+// Speculation for small batches (k_long below): up to nwaves / kSpecShare of
+// the longest documents get a second wave, when the batch has at most
+// kSpecBatchWaves documents per resident wave (a full batch is throughput-
+// bound and keeps one wave per document).
+constexpr uint32_t kSpecShare = 8, kSpecBatchWaves = 4;
 template <int WPB, bool DIAG, bool VEC>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __restrict__ Tp,
                                                   const uint8_t* __restrict__ buf,
@@ -297,7 +302,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   uint32_t fault_doc, uint8_t* __restrict__ vslots,
                                                   cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
                                                   int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ hpos,
-                                                  const uint32_t* __restrict__ hgap) {
+                                                  const uint32_t* __restrict__ hgap, cld_result* __restrict__ spec_out,
+                                                  uint32_t* __restrict__ spec_take) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -308,6 +314,16 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (total == 0) return;                       // empty re-queue list: no dequeue atomics at all
+  // Speculation (small batches only, so full batches keep their throughput):
+  // the first nspec documents of the longest-first list -- the ones a small
+  // launch waits for -- get two waves, one running pass 1 (kPassFirstOnly)
+  // and one pass 2 (kPassRepeatsOnly, into spec_out).  Entries 2q / 2q + 1
+  // are document q's two roles, entries from 2 * nspec on one document each.
+  // The last wave to leave takes pass 2's result for every document whose
+  // pass 1 was not good enough (spec_take).
+  const uint32_t nwaves = gridDim.x * WPB;
+  const uint32_t nspec = (!VEC && spec_out && total <= kSpecBatchWaves * nwaves) ? min(total, nwaves / kSpecShare) : 0u;
+  const uint32_t entries = total + nspec;
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 98, exact);
@@ -315,8 +331,10 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
     // A lane-0-only atomic feeding readfirstlane at the loop head let the
     // compiler split the loop so the other lanes re-read k = 0 forever.
-    const uint32_t k = wave::uflu(atomicAdd(&counters[kCtrDequeue], lane == 0 ? 1u : 0u));
-    if (k >= total) break;
+    const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrDequeue], lane == 0 ? 1u : 0u));
+    if (e >= entries) break;
+    const uint32_t k = e < 2 * nspec ? e >> 1 : e - nspec;      // list position
+    const int mode = e < 2 * nspec ? ((e & 1) ? lng::kPassRepeatsOnly : lng::kPassFirstOnly) : lng::kPassesAll;
     const uint32_t i = list[k];
     const uint64_t a = offs[i], b = offs[i + 1];
     const uint64_t len = b - a;
@@ -351,13 +369,26 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                          rw ? hflag + a : nullptr, &V);
       if (lane == 0 && passes >= 1 && passes <= 3) n_chunks[i] = V.over ? -1 : V.n;
     } else {
+      cld_result* o = mode == lng::kPassRepeatsOnly ? spec_out + k : &out[i];
       if (exact && len <= (uint64_t)lng::kDocCap)
-        passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i, cflags,
-                                   (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr);
+        passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, o, tr, i, cflags,
+                                   (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr,
+                                   nullptr, mode);
     }
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
     if (i == fault_doc) passes = -lng::kWhyLength;   // fault injection (CLD_FAULT_DOC): on to k_general
+    if (mode == lng::kPassRepeatsOnly) {            // pass 2 in spec_out[k]; taken or not by its pass-1 wave
+      if (lane == 0 && !(passes >= 1 && passes <= 3)) {
+        spec_out[k].summary_lang = CLD_LANG_FAILED;
+        spec_out[k].text_bytes = min(max(-passes, 0), 7);   // the re-queue reason
+      }
+      continue;
+    }
+    if (passes == lng::kNeedsRepeats) {
+      if (lane == 0) spec_take[atomicAdd(&counters[kCtrSpecTake], 1u)] = k;
+      continue;
+    }
     if (lane == 0) {
       if (passes >= 1 && passes <= 3) {
         atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
@@ -365,6 +396,28 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
         const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);
         requeue2[q] = i;
         atomicAdd(&counters[kCtrWhy + min(max(-passes, 0), 7)], 1u);
+      }
+    }
+  }
+  if (nspec) {
+    // the last wave out hands over the speculative pass-2 results (every
+    // wave's stores released before its count, acquired by the last)
+    __threadfence();
+    const uint32_t done = wave::uflu(atomicAdd(&counters[kCtrSpecDone], lane == 0 ? 1u : 0u));
+    if (done == nwaves - 1) {
+      __threadfence();
+      const uint32_t nt = __hip_atomic_load(&counters[kCtrSpecTake], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t p = lane; p < nt; p += 64) {
+        const uint32_t k = spec_take[p], i = list[k];
+        const cld_result r = spec_out[k];
+        if (r.summary_lang == CLD_LANG_FAILED) {      // pass 2 could not run here: k_general redoes it all
+          const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);
+          requeue2[q] = i;
+          atomicAdd(&counters[kCtrWhy + r.text_bytes], 1u);
+        } else {
+          out[i] = r;
+          atomicAdd(&counters[kCtrPass2], 1u);
+        }
       }
     }
   }
@@ -517,7 +570,7 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           hipStream_t s) {
+                           cld_result* spec_out, uint32_t* spec_take, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
@@ -525,13 +578,14 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take);
   return hipGetLastError();
 }
+size_t cld_long_spec_docs(int n_slots) { return (size_t)n_slots / cld::kSpecShare; }
 
 size_t cld_vec_slot_bytes() { return sizeof(cld::lng::VecSlot); }
 
@@ -552,7 +606,7 @@ hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const u
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                      requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
-                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap);
+                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap, nullptr, nullptr);
   return hipGetLastError();
 }
 

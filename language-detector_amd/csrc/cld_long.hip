@@ -2498,10 +2498,21 @@ __device__ __noinline__ void vec_move_lang(VecState* V, int from_lang, int to_la
   V->n = k;
 }
 
+// Pass modes (k_long's speculation for the longest documents of a small
+// batch): kPassesAll runs compact_lang_det_impl.cc:1848-2105's passes in
+// order; kPassFirstOnly stops after a pass 1 that is not good enough and
+// returns kNeedsRepeats (a Squeeze restart still runs its passes here);
+// kPassRepeatsOnly starts at pass 2 = Repeats|Finish, what a pass 1 without
+// the Squeeze restart is followed by.  Pass 2 reads nothing pass 1 computed
+// (the DocTote, the boost ring and the predictor start fresh), so the two can
+// run on two waves at once and the document costs the longer, not the sum.
+constexpr int kPassesAll = 0, kPassFirstOnly = 1, kPassRepeatsOnly = 2;
+constexpr int kNeedsRepeats = 4;
 template <bool D, bool VEC = false>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
-                      const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf, VecState* V = nullptr) {
+                      const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf, VecState* V = nullptr,
+                      int mode = kPassesAll) {
   const int unk = (int)T.unknown_lang;
   // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
   if (lane == 0) s.has_pri = pri != nullptr;
@@ -2537,8 +2548,8 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
   // the Squeeze one is fresh per span (pred2).
   bool sq = false;
   int nsp = 0, cur = 0;                          // span cache (pass 1): spans recorded, bytes used
-  bool cache_ok = !VEC;                          // (vec mode rebuilds pass 2's spans with their offset map)
-  for (int pass = 1; pass <= 3; ++pass) {
+  bool cache_ok = !VEC && mode != kPassRepeatsOnly;   // (vec mode rebuilds pass 2's spans with their offset map)
+  for (int pass = mode == kPassRepeatsOnly ? 2 : 1; pass <= 3; ++pass) {
     const bool rep = pass == 3 || (pass == 2 && !sq);    // Repeats always comes with Finish
     const bool from_cache = pass == 2 && rep && cache_ok;
     if constexpr (VEC) {                         // each pass starts a new vector (:1730-1732)
@@ -2676,6 +2687,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
       }
     } else {
       if (wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0)) return pass;
+      if (mode == kPassFirstOnly && pass == 1) return kNeedsRepeats;   // the speculative wave has pass 2
     }
   }
   return 0;

@@ -358,6 +358,8 @@ struct Device {
   uint64_t stride = 0;
   int lanes = 0;
   uint8_t* d_slots = nullptr; // k_long per-wave slots (0 slots: CLD_LONG=0, long documents go to k_general)
+  cld_result* d_spec_out = nullptr;   // k_long's speculative pass-2 results (small batches; CLD_LONG_SPEC=0: off)
+  uint32_t* d_spec_take = nullptr;
   int n_slots = 0;
   uint32_t* d_requeue2 = nullptr;
   size_t requeue2_cap = 0;
@@ -584,6 +586,12 @@ int init_device(Device* d) {
     HIP_OK(hipMalloc(&d->d_slots, (uint64_t)n_slots * slot));
     HIP_OK(hipMemset(d->d_slots, 0, (uint64_t)n_slots * slot));   // predictor epochs start at 0
     d->n_slots = n_slots;
+    const char* sp = getenv("CLD_LONG_SPEC");
+    if (!sp || atoi(sp) != 0) {
+      const size_t m = std::max<size_t>(1, cld_long_spec_docs(n_slots));
+      HIP_OK(hipMalloc(&d->d_spec_out, m * sizeof(cld_result)));
+      HIP_OK(hipMalloc(&d->d_spec_take, m * sizeof(uint32_t)));
+    }
   }
   if (const char* e = getenv("CLD_FAULT_DOC")) d->fault_doc = (uint32_t)strtoul(e, nullptr, 10);
   if (const char* e = getenv("CLD_DEBUG_DOC")) {
@@ -679,7 +687,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            ctr, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, d->fault_doc,
-                           s));
+                           d->d_spec_out, d->d_spec_take, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               ctr, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
@@ -943,11 +951,19 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   // nothing runs until chunk 0 is uploaded, and an upload (~53 GB/s) outruns
   // the kernels (~28 GB/s at C2), so a small first chunk shortens the fill
   // while the next, larger upload still finishes before its kernels are due.
+  // A batch whose mean document is longer than k_wave takes is bound by
+  // k_long's longest document per launch (one wave scores it start to end),
+  // and every chunk pays that tail again: such batches go in chunks four
+  // times as large and without the ramp (a coalesced batch of requests is
+  // then one launch; C5 requests: 8 callers 193K -> 299K, 64 callers
+  // 404K -> 863K docs/s).
+  const bool tail_bound = offs[n] - offs[0] > (uint64_t)n * kWaveCap;
   std::vector<size_t> cut{0};
   while (cut.back() < n) {
     const size_t a = cut.back();
     const size_t ci = cut.size() - 1;
-    const uint64_t kChunkBytes = std::max<uint64_t>(1u << 20, chunk_bytes() >> (ci < 3 ? 3 - ci : 0));
+    const uint64_t kChunkBytes = tail_bound ? 4 * chunk_bytes()
+                                            : std::max<uint64_t>(1u << 20, chunk_bytes() >> (ci < 3 ? 3 - ci : 0));
     const size_t kChunkDocs = (size_t)(kChunkBytes >> 7);    // 8K documents per MB
     size_t lo = a + 1, hi = std::min(n, a + kChunkDocs);     // largest b <= hi with bytes <= kChunkBytes (>= 1 doc)
     while (lo < hi) {
@@ -1542,6 +1558,7 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_requeue); (void)hipFree(d->d_requeue2); (void)hipFree(d->d_lsorted); (void)hipFree(d->d_lkey); (void)hipFree(d->d_lhist); (void)hipFree(d->d_slots); (void)hipFree(d->d_buf); (void)hipFree(d->d_offs); (void)hipFree(d->d_out);
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag); (void)hipFree(d->d_hpos);
+    (void)hipFree(d->d_spec_out); (void)hipFree(d->d_spec_take);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);
