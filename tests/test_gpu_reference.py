@@ -77,3 +77,30 @@ def test_gpu_equals_reference_with_flags(gpu, ref, ref_tables, golden, flags):
     hints = random_hints(gpu, 5000, 512)
     same(gpu.detect_batch_ex(buf=cb, offsets=co, hints=hints, flags=flags),
          ref.detect_batch(cb, co, hints=hints, threads=16, flags=flags), "hints flags %#x" % flags)
+
+
+def test_small_batches_speculate_and_equal_reference(gpu, ref):
+    """Small batches of long documents: k_long gives the longest of them a
+    pass-1 wave and a pass-2 wave (speculation; the launch turns it on when the
+    long list has at most 4 documents per resident wave, which every batch here
+    has), and takes pass 2's result only where pass 1 was not good enough.
+    Pages that need pass 2 (Repeats), ones that stop after pass 1, hinted and
+    HTML pages, each equal to the reference; request-sized C5 batches too."""
+    b3, o3 = corpus.c3(600, seed=811)
+    got = gpu.detect_batch(buf=b3, offsets=o3)
+    st = gpu.last_stats(0)
+    assert st.long_docs == 600 and st.general_docs == 0
+    assert st.passes[1] > 100 and st.passes[0] > 50      # both outcomes of the pass-1 wave occur
+    same(got, ref.detect_batch(b3, o3, threads=16), "c3 600")
+    for seed in (812, 813, 814):                         # ~1 MiB requests, each with ~180 long documents
+        b5, o5 = corpus.c5(1000, seed=seed)
+        same(gpu.detect_batch(buf=b5, offsets=o5), ref.detect_batch(b5, o5, threads=16), "c5 request %d" % seed)
+    from test_gpu_html_hints import random_hints
+    hb, ho = corpus.html(300, seed=815)
+    n = len(ho) - 1
+    same(gpu.detect_batch_ex(buf=hb, offsets=ho, html=True),
+         ref.detect_batch(hb, ho, plain=np.zeros(n, np.uint8), threads=16), "html 300")
+    cb, co = corpus.c3(200, seed=816)
+    hints = random_hints(gpu, 200, 817)
+    same(gpu.detect_batch_ex(buf=cb, offsets=co, hints=hints), ref.detect_batch(cb, co, hints=hints, threads=16),
+         "c3 hints")
