@@ -71,6 +71,14 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
                            unsigned long long* prof, const uint8_t* special, uint32_t* special_list,
                            int special_ctr, uint32_t cflags, const uint32_t* priors, const uint8_t* hbuf,
                            const uint8_t* hflag, uint32_t* hist2, hipStream_t s);
+// k_wave alone, without k_route: the caller guarantees every document is at
+// most kWaveCap bytes (run_tiny's request-sized batches).  Documents the wave
+// kernel cannot finish are listed under counters[kCtrRequeue], or, with
+// requeue_list == nullptr (counters unused), marked in their result:
+// summary_lang = kWaveRequeued.
+constexpr uint16_t kWaveRequeued = 0xFFFE;
+hipError_t cld_launch_wave_only(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n, cld_result* out,
+                                uint32_t* requeue_list, uint32_t* counters, uint32_t cflags, hipStream_t s);
 // HTML documents of the batch (special & kSpecialHtml) rewritten into plain
 // text (cld_html.hip): hbuf / hflag are indexed like buf (offs); special is
 // updated in place (kSpecialHtml -> kSpecialRewritten for each rewritten page);

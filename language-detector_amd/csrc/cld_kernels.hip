@@ -213,8 +213,12 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   const bool rq = !wave::detect<CAP>(T, (rw ? hbuf : buf) + a, (int)len, smem[wv], lane, &out[i],
                                      (i & 63) == 0 ? prof : nullptr, cflags, pri, rw ? hflag + a : nullptr);
   if (rq && lane == 0) {                       // rare (state-machine or capacity cases)
-    uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
-    requeue_list[k] = (uint32_t)i;
+    if (requeue_list) {
+      uint32_t k = atomicAdd(&counters[kCtrRequeue], 1u);
+      requeue_list[k] = (uint32_t)i;
+    } else {                                   // run_tiny: the mark travels with the results
+      out[i].summary_lang = kWaveRequeued;
+    }
   }
 }
 
@@ -649,6 +653,15 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
   dim3 grid(8 * per), block(64 * kWaveWPB);
   hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), grid, block, 0, s, *T, buf, offs, n, out,
                      requeue_list, counters, prof, special, special_list, special_ctr, cflags, priors, hbuf, hflag);
+  return hipGetLastError();
+}
+
+hipError_t cld_launch_wave_only(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n, cld_result* out,
+                                uint32_t* requeue_list, uint32_t* counters, uint32_t cflags, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int per = ((n + kWaveWPB - 1) / kWaveWPB + 7) / 8;
+  hipLaunchKernelGGL((cld::k_wave<kWaveCap, kWaveWPB>), dim3(8 * per), dim3(64 * kWaveWPB), 0, s, *T, buf, offs, n,
+                     out, requeue_list, counters, nullptr, nullptr, nullptr, 0, cflags, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 

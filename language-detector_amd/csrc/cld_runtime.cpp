@@ -348,6 +348,24 @@ DevTables device_tables(const DevTables& o, const uint8_t* d) {
 }
 
 // ------------------------------------------------------------ per-GPU context
+// Request-sized batches of short documents (run_tiny): at most kTinyDocs
+// documents of at most kWaveCap bytes.  One pinned block and its device twin
+// per tiny slot, laid out so that one upload and one download carry a call:
+//   [results (n x 40 B, ending at kTinyCtrOff) | (unused) | offsets | text]
+constexpr size_t kTinyDocs = 1024;
+constexpr size_t kTinyCtrOff = kTinyDocs * sizeof(cld_result);
+constexpr size_t kTinyOffsOff = kTinyCtrOff + kCtrSlots * sizeof(uint32_t);
+constexpr size_t kTinyBlock = kTinyOffsOff + (kTinyDocs + 1) * sizeof(uint64_t) + kTinyDocs * kWaveCap + 256;
+constexpr int kTinySlots = 2;   // calls in flight per context (each its own stream)
+struct TinySlot {
+  hipStream_t s = nullptr;
+  uint8_t* h = nullptr;          // pinned
+  uint8_t* hd = nullptr;         // the pinned block's device address (zero-copy mode)
+  uint8_t* dv = nullptr;         // device
+  uint32_t* d_rq = nullptr;      // k_wave's re-queue list
+  std::mutex mu;
+};
+
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
@@ -435,6 +453,8 @@ struct Device {
     cld_chunk* compact = nullptr; size_t compact_cap = 0;
     uint8_t* vslots = nullptr;   // k_long<VEC>: one VecSlot per slot of d_slots (on first use)
   } vec;
+  TinySlot tiny[kTinySlots];      // run_tiny: k_wave-only calls, independent of the scratch above
+  std::atomic<unsigned> tiny_rr{0};
   std::mutex mu;
   std::atomic<int> inflight{0};   // calls routed to this context and not yet returned (pick_context)
 };
@@ -447,6 +467,7 @@ std::mutex g_init_mu;
 // same table set.  Order: g_init_mu, then g_swap_mu, then a device's mu.
 std::shared_mutex g_swap_mu;
 bool g_inited = false;
+std::atomic<bool> g_ready{false};   // g_inited with g_init_rc == CLD_OK (the lock-free check of every call)
 int g_init_rc = CLD_ENODEV;
 HostTables g_tab;
 std::vector<Device*> g_devs;
@@ -557,6 +578,13 @@ int init_device(Device* d) {
     HIP_OK(hipEventCreateWithFlags(&h.down, hipEventDisableTiming));
   }
   if (int rc = upload_tables(d, g_tab)) return rc;
+  for (TinySlot& t : d->tiny) {
+    HIP_OK(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
+    HIP_OK(hipHostMalloc((void**)&t.h, kTinyBlock, hipHostMallocDefault));
+    HIP_OK(hipHostGetDevicePointer((void**)&t.hd, t.h, 0));
+    HIP_OK(hipMalloc(&t.dv, kTinyBlock));
+    HIP_OK(hipMalloc(&t.d_rq, kTinyDocs * sizeof(uint32_t)));
+  }
   HIP_OK(hipMalloc(&d->d_counters, kCtrSlots * sizeof(uint32_t)));
   HIP_OK(hipMalloc(&d->d_lhist, 256 * sizeof(uint32_t)));
   if (const char* e = getenv("CLD_LONG_ORDER")) d->long_order = atoi(e) != 0;
@@ -931,8 +959,8 @@ struct HostReg {
 // marked them); internal, never returned to a caller.
 constexpr int kDocsFailed = 1;
 
-int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
-                   const uint8_t* special = nullptr, const uint32_t* priors = nullptr, bool html = false) {
+int run_host_stream(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
+                    const uint8_t* special = nullptr, const uint32_t* priors = nullptr, bool html = false) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   d->ev_used = 0;
@@ -1037,8 +1065,12 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
         HIP_BRK(hipMemcpyAsync(h.d_pri, h.h_pri, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, d->up_stream))
     }
     HIP_BRK(hipEventRecord(h.up, d->up_stream))
-    // kernels: buffer base biased so that the caller's offsets index it directly
+    // kernels: buffer base biased so that the caller's offsets index it directly.
+    // They write h.d_out, which chunk c-2's download may still be reading on
+    // down_stream: wait for that copy on the device (the host hand-over of its
+    // results, deliver() below, comes later and keeps the overlap).
     HIP_BRK(hipStreamWaitEvent(d->stream, h.up, 0))
+    if (h.busy) HIP_BRK(hipStreamWaitEvent(d->stream, h.down, 0))
     const uint8_t* kbuf = h.d_in - base;
     if (flags & kPrepFlags) {
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
@@ -1103,25 +1135,158 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
   return err ? kDocsFailed : CLD_OK;
 }
 
+// Request-sized batches of short documents: the per-call cost the reference's
+// per-document wrapper call (wrapper.cc:7-16, handlers.go:132-151) would
+// otherwise pay in full -- the streamed path's six launches, three streams,
+// chunk events and counter copies -- is cut to one upload, one k_wave launch,
+// one download and one synchronisation, on a tiny slot of its own (its own
+// stream, pinned block and re-queue list; none of the context's scratch, so
+// it needs neither the context lock nor the `done` chain).  Documents k_wave
+// re-queues (a second script span, a second hit round, ...) are redone on the
+// streamed path; results are the same whichever path finishes a document.
+// CLD_TINY=0 turns it off (A/B).
+bool tiny_enabled() {
+  static const bool v = !(getenv("CLD_TINY") && atoi(getenv("CLD_TINY")) == 0);
+  return v;
+}
+
+bool tiny_batch(const Device* d, const uint64_t* offs, size_t n, uint32_t flags, const uint8_t* special,
+                const uint32_t* priors) {
+  if (n == 0 || n > kTinyDocs || special || priors || (flags & kPrepFlags) || !tiny_enabled()) return false;
+  if (d->d_dbg || d->h_trace || d->d_prof || d->fault_doc != 0xFFFFFFFFu) return false;   // diagnostics
+  uint64_t bad = 0;
+  for (size_t i = 0; i < n; ++i) bad |= (uint64_t)(offs[i + 1] - offs[i] > (uint64_t)kWaveCap);
+  return bad == 0;
+}
+
+// CLD_TINY_ZC=1: k_wave reads the documents from the pinned block and
+// writes the results into it over PCIe (no DMA at all: one launch and one
+// synchronisation per call); default: one upload and one download.
+bool tiny_zero_copy() {
+  static const bool v = getenv("CLD_TINY_ZC") && atoi(getenv("CLD_TINY_ZC")) != 0;
+  return v;
+}
+
+int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
+  TinySlot* t = nullptr;
+  std::unique_lock<std::mutex> lk;
+  for (TinySlot& x : d->tiny) {
+    std::unique_lock<std::mutex> l(x.mu, std::try_to_lock);
+    if (l.owns_lock()) { t = &x; lk = std::move(l); break; }
+  }
+  if (!t) {
+    t = &d->tiny[d->tiny_rr.fetch_add(1) % kTinySlots];
+    lk = std::unique_lock<std::mutex>(t->mu);
+  }
+  HIP_OK(hipSetDevice(d->id));
+  const uint64_t base = offs[0], bytes = offs[n] - base;
+  const size_t text_off = kTinyOffsOff + (n + 1) * sizeof(uint64_t);
+  const size_t out_off = kTinyCtrOff - n * sizeof(cld_result);
+  uint64_t* ho = (uint64_t*)(t->h + kTinyOffsOff);
+  for (size_t i = 0; i <= n; ++i) ho[i] = offs[i] - base;
+  memcpy(t->h + text_off, buf + base, bytes);
+  // documents k_wave cannot finish come back marked (kWaveRequeued), no counters
+  if (tiny_zero_copy()) {
+    HIP_OK(cld_launch_wave_only(&d->T, t->hd + text_off, (const uint64_t*)(t->hd + kTinyOffsOff), (int)n,
+                                (cld_result*)(t->hd + out_off), nullptr, nullptr, flags & kCldFlags, t->s));
+  } else {
+    HIP_OK(hipMemcpyAsync(t->dv + kTinyOffsOff, t->h + kTinyOffsOff, text_off - kTinyOffsOff + bytes,
+                          hipMemcpyHostToDevice, t->s));
+    HIP_OK(cld_launch_wave_only(&d->T, t->dv + text_off, (const uint64_t*)(t->dv + kTinyOffsOff), (int)n,
+                                (cld_result*)(t->dv + out_off), nullptr, nullptr, flags & kCldFlags, t->s));
+    HIP_OK(hipMemcpyAsync(t->h + out_off, t->dv + out_off, n * sizeof(cld_result), hipMemcpyDeviceToHost, t->s));
+  }
+  HIP_OK(hipStreamSynchronize(t->s));
+  memcpy(out, t->h + out_off, n * sizeof(cld_result));
+  lk.unlock();
+  std::vector<uint32_t> list;
+  for (size_t i = 0; i < n; ++i)
+    if (out[i].summary_lang == kWaveRequeued) list.push_back((uint32_t)i);
+  const uint32_t rq = (uint32_t)list.size();
+  cld_batch_stats st{};
+  st.docs = n;
+  st.short_docs = n - rq;
+  st.passes[0] = n - rq;
+  if (rq == 0) {
+    std::unique_lock<std::mutex> dl(d->mu, std::try_to_lock);   // best effort: diagnostics only
+    if (dl.owns_lock()) { d->last = st; d->stats_pending = false; }
+    return CLD_OK;
+  }
+  // the re-queued documents, gathered, on the streamed path
+  std::vector<uint8_t> gb;
+  std::vector<uint64_t> go{0};
+  for (uint32_t i : list) {
+    gb.insert(gb.end(), buf + offs[i], buf + offs[i + 1]);
+    go.push_back(gb.size());
+  }
+  std::vector<cld_result> gout(rq);
+  const int rc = run_host_stream(d, gb.data(), go.data(), rq, gout.data(), flags);
+  if (rc != CLD_OK && rc != kDocsFailed) return rc;
+  for (uint32_t k = 0; k < rq; ++k) out[list[k]] = gout[k];
+  std::lock_guard<std::mutex> dl(d->mu);
+  const cld_batch_stats s2 = d->last;                  // the streamed call's counts for the re-queued documents
+  st.long_docs = s2.long_docs;
+  st.general_docs = s2.general_docs;
+  st.short_docs += s2.short_docs;
+  for (int k = 0; k < 4; ++k) st.passes[k] += s2.passes[k];
+  for (int k = 0; k < 8; ++k) st.long_requeue[k] = s2.long_requeue[k];
+  st.short_ms = s2.short_ms; st.long_ms = s2.long_ms; st.general_ms = s2.general_ms;
+  d->last = st;
+  return rc;
+}
+
+// One device's share of a host batch: run_tiny when it qualifies, else the streamed path.
+int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags,
+                   const uint8_t* special = nullptr, const uint32_t* priors = nullptr, bool html = false) {
+  if (tiny_batch(d, offs, n, flags, special, priors)) return run_tiny(d, buf, offs, n, out, flags);
+  return run_host_stream(d, buf, offs, n, out, flags, special, priors, html);
+}
+
 // Documents the kernels could not score come back marked CLD_LANG_FAILED
 // (k_general, kDocsFailed above); each is redone alone, so one bad document
 // never costs the batch.  CLD_EIO only if one still fails on its own.
+// The failed documents are retried together, as one gathered batch (scoring
+// is deterministic: outside fault injection a document that failed fails
+// again, so a batch with many marked documents must not turn into one GPU
+// round trip per document).  Only when the gathered retry itself reports
+// failures, and at most kIsolateAlone of them, is each such document run
+// alone, so one document cannot take another's result with it.
+constexpr size_t kIsolateAlone = 16;
 int run_host_shard_isolating(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out,
                              uint32_t flags, const uint8_t* special = nullptr, const uint32_t* priors = nullptr,
                              bool html = false) {
   int rc = run_host_shard(d, buf, offs, n, out, flags, special, priors, html);
   if (rc != kDocsFailed) return rc;
-  bool left = false;
-  for (size_t i = 0; i < n; ++i) {
-    if (out[i].summary_lang != CLD_LANG_FAILED) continue;
-    const int r = run_host_shard(d, buf, offs + i, 1, out + i, flags, special ? special + i : nullptr,
-                                 priors ? priors + 16 * i : nullptr, html);
-    if (r != CLD_OK) {
-      left = true;
-      if (r != kDocsFailed) return r;          // a device error, not a document
-    }
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < n; ++i)
+    if (out[i].summary_lang == CLD_LANG_FAILED) idx.push_back(i);
+  // gather the failed documents (with their routing bits and priors) into one batch
+  std::vector<uint8_t> gb;
+  std::vector<uint64_t> go{0};
+  std::vector<uint8_t> gsp;
+  std::vector<uint32_t> gpr;
+  for (size_t i : idx) {
+    gb.insert(gb.end(), buf + offs[i], buf + offs[i + 1]);
+    go.push_back(gb.size());
+    if (special) gsp.push_back(special[i]);
+    if (priors) gpr.insert(gpr.end(), priors + 16 * i, priors + 16 * i + 16);
   }
-  if (left) fprintf(stderr, "cld_mi355x: documents without a result after a retry (summary CLD_LANG_FAILED)\n");
+  std::vector<cld_result> gout(idx.size());
+  int r = run_host_shard(d, gb.data(), go.data(), idx.size(), gout.data(), flags, special ? gsp.data() : nullptr,
+                         priors ? gpr.data() : nullptr, html);
+  if (r != CLD_OK && r != kDocsFailed) return r;          // a device error, not a document
+  size_t left = 0;
+  for (size_t k = 0; k < idx.size(); ++k) {
+    out[idx[k]] = gout[k];
+    if (gout[k].summary_lang != CLD_LANG_FAILED) continue;
+    if (++left > kIsolateAlone) continue;                 // stays marked: CLD_EIO below
+    const size_t i = idx[k];
+    r = run_host_shard(d, buf, offs + i, 1, out + i, flags, special ? special + i : nullptr,
+                       priors ? priors + 16 * i : nullptr, html);
+    if (r != CLD_OK && r != kDocsFailed) return r;
+    if (r == CLD_OK) --left;
+  }
+  if (left) fprintf(stderr, "cld_mi355x: %zu document(s) without a result after a retry (summary CLD_LANG_FAILED)\n", left);
   return left ? CLD_EIO : CLD_OK;
 }
 
@@ -1404,22 +1569,13 @@ int swap_tables_all(const HostTables& nt) {
   return CLD_OK;
 }
 
-struct Pending {
-  const char* text;
-  size_t len;
-  cld_result res;
-  bool done = false;
-};
-std::mutex g_q_mu;
-std::condition_variable g_q_cv;
-std::vector<Pending*> g_queue;
-bool g_dispatching = false;
 
 }  // namespace
 
 extern "C" {
 
 int cld_init(const char* tables_path, int n_devices) {
+  if (g_ready.load(std::memory_order_acquire)) return CLD_OK;
   std::lock_guard<std::mutex> lk(g_init_mu);
   if (g_inited) return g_init_rc;
   g_inited = true;
@@ -1462,6 +1618,7 @@ int cld_init(const char* tables_path, int n_devices) {
       if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
       g_devs.push_back(d);
     }
+  g_ready.store(true, std::memory_order_release);
   return g_init_rc = CLD_OK;
 }
 
@@ -1477,6 +1634,7 @@ int cld_init_device(const char* tables_path, int device) {
   d->id = device;
   if ((rc = init_device(d)) != CLD_OK) return g_init_rc = rc;
   g_devs.push_back(d);
+  g_ready.store(true, std::memory_order_release);
   return g_init_rc = CLD_OK;
 }
 
@@ -1572,6 +1730,11 @@ void cld_shutdown(void) {
                     (void*)d->vec.pri, (void*)d->vec.pool, (void*)d->vec.pool_off, (void*)d->vec.nch,
                     (void*)d->vec.pos, (void*)d->vec.order, (void*)d->vec.compact})
       if (p) (void)hipFree(p);
+    for (TinySlot& t : d->tiny) {
+      if (t.s) (void)hipStreamSynchronize(t.s);
+      (void)hipHostFree(t.h); (void)hipFree(t.dv); (void)hipFree(t.d_rq);
+      if (t.s) (void)hipStreamDestroy(t.s);
+    }
     (void)hipEventDestroy(d->done);
     (void)hipStreamDestroy(d->up_stream);
     (void)hipStreamDestroy(d->down_stream);
@@ -1582,6 +1745,7 @@ void cld_shutdown(void) {
   g_tab = HostTables();
   g_dynamic = false;
   g_inited = false;
+  g_ready.store(false, std::memory_order_release);
   g_init_rc = CLD_ENODEV;
 }
 
@@ -1633,11 +1797,41 @@ struct Req {
   size_t n;
   cld_result* out;
   uint32_t flags;
-  int rc;
-  bool done;
+  bool tiny;                    // run_tiny-sized: every document <= kWaveCap, n <= kTinyDocs, no preparation
+  int rc = CLD_OK;
+  // Parking: a queued caller sleeps on its own condition variable until its
+  // group is done (kDone) or it is promoted to form the next group (kLead).
+  // One shared condition variable woke all of them at every dispatch, and
+  // their re-acquiring the queue lock one by one cost ~1 ms per dispatch at
+  // 256 callers.  Done callers are woken as a binary tree: each wakes `kid`
+  // before returning, so no thread issues more than two wake-ups.
+  enum { kWaiting = 0, kDone = 1, kLead = 2 };
+  std::mutex m;
+  std::condition_variable cv;
+  int state = kWaiting;
+  bool promoted = false;        // under g_rq_mu: already asked to lead
+  Req* kid[2] = {nullptr, nullptr};
+  Req(const uint8_t* b, const uint64_t* o, size_t n_, cld_result* r, uint32_t f, bool t)
+      : buf(b), offs(o), n(n_), out(r), flags(f), tiny(t) {}
+  void post(int st) {
+    { std::lock_guard<std::mutex> l(m); state = st; }
+    cv.notify_one();
+  }
+  int park() {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [&] { return state != kWaiting; });
+    const int st = state;
+    if (st == kLead) state = kWaiting;
+    return st;
+  }
 };
+bool tiny_request(const uint64_t* offs, size_t n, uint32_t flags) {
+  if (n > kTinyDocs || (flags & kPrepFlags) || !tiny_enabled()) return false;
+  uint64_t bad = 0;
+  for (size_t i = 0; i < n; ++i) bad |= (uint64_t)(offs[i + 1] - offs[i] > (uint64_t)kWaveCap);
+  return bad == 0;
+}
 std::mutex g_rq_mu;
-std::condition_variable g_rq_cv;
 std::deque<Req*> g_rq;
 int g_rq_active = 0;
 struct Arena {                  // pinned staging of one dispatch (reused)
@@ -1698,39 +1892,90 @@ void run_group(const std::vector<Req*>& grp) {
   g_arenas.push_back(a);
 }
 
+// Dispatch slots: one per context for any group, and up to kTinySlots per
+// context while the extra ones carry tiny groups (run_tiny: each tiny slot has
+// its own stream and buffers, so two such calls overlap on one GPU -- one
+// uploads or synchronises while the other's kernel runs).  A group whose
+// first request is tiny takes only tiny requests, up to kTinyDocs documents,
+// so it stays on run_tiny.  Caller holds g_rq_mu.
+bool form_group(std::vector<Req*>* grp) {
+  const int ndev = (int)g_devs.size();
+  const bool any_slot = g_rq_active < ndev;
+  if (g_rq.empty() || !(any_slot || g_rq_active < ndev * kTinySlots)) return false;
+  const Req* first = nullptr;
+  for (Req* r : g_rq)
+    if (any_slot || r->tiny) { first = r; break; }
+  if (!first) return false;
+  const uint32_t f = first->flags;
+  const bool tiny = first->tiny;
+  uint64_t bytes = 0;
+  size_t docs = 0;
+  grp->clear();
+  for (auto it = g_rq.begin(); it != g_rq.end();) {
+    Req* r = *it;
+    const uint64_t nb = r->offs[r->n] - r->offs[0];
+    const bool fits = tiny ? r->tiny && docs + r->n <= kTinyDocs
+                           : grp->empty() || (bytes + nb <= kCoalesceBytes && docs + r->n <= kCoalesceDocs);
+    if (r->flags != f || !fits) {
+      ++it;
+      continue;
+    }
+    grp->push_back(r);
+    bytes += nb;
+    docs += r->n;
+    it = g_rq.erase(it);
+  }
+  ++g_rq_active;
+  return true;
+}
+
 int run_coalesced(const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
-  Req me{buf, offs, n, out, flags, CLD_OK, false};
+  Req me(buf, offs, n, out, flags, tiny_request(offs, n, flags));
+  std::vector<Req*> grp;
   std::unique_lock<std::mutex> lk(g_rq_mu);
   g_rq.push_back(&me);
   for (;;) {
-    if (me.done) return me.rc;
-    if (g_rq_active < (int)g_devs.size() && !g_rq.empty()) {
-      std::vector<Req*> grp;
-      const uint32_t f = g_rq.front()->flags;
-      uint64_t bytes = 0;
-      size_t docs = 0;
-      for (auto it = g_rq.begin(); it != g_rq.end();) {
-        Req* r = *it;
-        const uint64_t nb = r->offs[r->n] - r->offs[0];
-        if (r->flags != f || (!grp.empty() && (bytes + nb > kCoalesceBytes || docs + r->n > kCoalesceDocs))) {
-          ++it;
-          continue;
-        }
-        grp.push_back(r);
-        bytes += nb;
-        docs += r->n;
-        it = g_rq.erase(it);
+    {  // a promoted caller whose request another dispatcher has meanwhile run
+      std::lock_guard<std::mutex> l(me.m);
+      if (me.state == Req::kDone) {
+        lk.unlock();
+        for (Req* k : me.kid) if (k) k->post(Req::kDone);
+        return me.rc;
       }
-      ++g_rq_active;
+    }
+    if (!form_group(&grp)) {
       lk.unlock();
-      run_group(grp);
-      lk.lock();
-      --g_rq_active;
-      for (Req* r : grp) r->done = true;
-      g_rq_cv.notify_all();
+      if (me.park() == Req::kDone) {
+        for (Req* k : me.kid) if (k) k->post(Req::kDone);
+        return me.rc;
+      }
+      lk.lock();                               // promoted: form the next group
+      me.promoted = false;
       continue;
     }
-    g_rq_cv.wait(lk);
+    lk.unlock();
+    run_group(grp);
+    // wake-up tree over the other members (set before any wake-up: a woken
+    // member returns, and its Req with it)
+    std::vector<Req*> others;
+    bool mine = false;
+    for (Req* r : grp) {
+      if (r == &me) mine = true;
+      else others.push_back(r);
+    }
+    for (size_t j = 0; j < others.size(); ++j)
+      for (int c = 0; c < 2; ++c) {
+        const size_t k = 2 * j + 2 + c;
+        others[j]->kid[c] = k < others.size() ? others[k] : nullptr;
+      }
+    lk.lock();
+    --g_rq_active;
+    for (Req* r : g_rq)                        // the next group's dispatcher
+      if (!r->promoted && r != &me) { r->promoted = true; r->post(Req::kLead); break; }
+    lk.unlock();
+    for (size_t j = 0; j < 2 && j < others.size(); ++j) others[j]->post(Req::kDone);
+    if (mine) return me.rc;
+    lk.lock();
   }
 }
 
@@ -2093,69 +2338,42 @@ int cld_convert_data_file(const char* data_file, const char* base_cldt, const ch
   return (fclose(f) == 0 && w == out.size()) ? CLD_OK : CLD_EIO;
 }
 
-// wrapper.cc:7-16.  Concurrent callers are coalesced: the first caller to
-// find no dispatch in flight becomes the dispatcher and runs every queued
-// document as one batch; the others wait for their slot to be filled.
+// wrapper.cc:7-16.  One document through cld_detect_batch: concurrent
+// callers are coalesced there (run_coalesced) into micro-batches, and a batch
+// of short documents takes run_tiny (one upload, one k_wave launch, one
+// download).
+//
+// Failures.  The reference has no error channel here and neither does
+// wrapper.h, so:
+//  * a document the kernels could not score (CLD_EIO: marked
+//    CLD_LANG_FAILED after the batch path's own retry) gets the reference's
+//    answer for "no language", UNKNOWN -> "en" (compact_lang_det.cc:91-93),
+//    with a line on stderr -- one document never costs the process;
+//  * no usable GPU or tables at the first call, or a device error (CLD_EFAULT,
+//    CLD_ENOMEM, ...), aborts with a message: answering "en" to every caller
+//    of a broken GPU would turn a deployment fault into confident wrong
+//    answers (a service checks cld_init() at start).
 const char* detect_language(const char* text) {
   if (cld_init(nullptr, 0) != CLD_OK) {
-    // a deployment without a usable GPU (or tables): there is no CPU fallback,
-    // and wrapper.h has no error channel, so the process stops loudly
     fprintf(stderr, "cld_mi355x: detect_language: GPU runtime unavailable\n");
     abort();
   }
-  Pending p;
-  p.text = text ? text : "";
-  p.len = strlen(p.text);
-  std::unique_lock<std::mutex> lk(g_q_mu);
-  g_queue.push_back(&p);
-  for (;;) {
-    if (p.done) break;
-    if (!g_dispatching) {
-      g_dispatching = true;
-      std::vector<Pending*> batch;
-      batch.swap(g_queue);
-      lk.unlock();
-      std::vector<uint64_t> offs(batch.size() + 1, 0);
-      std::string bytes;
-      for (size_t i = 0; i < batch.size(); ++i) {
-        bytes.append(batch[i]->text, batch[i]->len);
-        offs[i + 1] = bytes.size();
-      }
-      std::vector<cld_result> res(batch.size());
-      int rc = cld_detect_batch((const uint8_t*)bytes.data(), offs.data(), batch.size(), res.data(), 0);
-      if (rc != CLD_OK) {
-        // One caller's document never costs the others their answers.  After
-        // CLD_EIO only the documents marked CLD_LANG_FAILED lack a result;
-        // after any other error every document is retried on its own.  A
-        // document that still fails gets the reference's answer for "no
-        // language" (UNKNOWN -> "en", compact_lang_det.cc:91-93) and a line
-        // on stderr: wrapper.h has no error channel to carry it.
-        for (size_t i = 0; i < batch.size(); ++i) {
-          if (rc == CLD_EIO && res[i].summary_lang != CLD_LANG_FAILED) continue;
-          const uint64_t one[2] = {offs[i], offs[i + 1]};
-          int r = cld_detect_batch((const uint8_t*)bytes.data(), one, 1, &res[i], 0);
-          if (r != CLD_OK || res[i].summary_lang == CLD_LANG_FAILED) {
-            fprintf(stderr, "cld_mi355x: detect_language: no result for a document (%d); answering \"en\"\n", r);
-            std::shared_lock<std::shared_mutex> tl(g_swap_mu);
-            res[i].summary_lang = (uint16_t)g_tab.meta.unknown_language;
-          }
-        }
-      }
-      lk.lock();
-      for (size_t i = 0; i < batch.size(); ++i) { batch[i]->res = res[i]; batch[i]->done = true; }
-      g_dispatching = false;
-      g_q_cv.notify_all();
-      continue;
-    }
-    g_q_cv.wait(lk);
+  const char* t = text ? text : "";
+  const uint64_t offs[2] = {0, (uint64_t)strlen(t)};
+  cld_result res{};
+  const int rc = cld_detect_batch((const uint8_t*)t, offs, 1, &res, 0);
+  std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+  if (rc == CLD_EIO && res.summary_lang == CLD_LANG_FAILED) {
+    fprintf(stderr, "cld_mi355x: detect_language: no result for a document; answering \"en\"\n");
+    res.summary_lang = (uint16_t)g_tab.meta.unknown_language;
+  } else if (rc != CLD_OK) {
+    fprintf(stderr, "cld_mi355x: detect_language: device error %d\n", rc);
+    abort();
   }
-  lk.unlock();
-  int lang = p.res.summary_lang;
-  {
-    std::shared_lock<std::shared_mutex> tl(g_swap_mu);
-    if (lang == (int)g_tab.meta.unknown_language) lang = (int)g_tab.meta.english;  // compact_lang_det.cc:91-93
-  }
-  return cld_language_code(lang);
+  int lang = res.summary_lang;
+  if (lang == (int)g_tab.meta.unknown_language) lang = (int)g_tab.meta.english;  // compact_lang_det.cc:91-93
+  if (lang < 0 || (size_t)lang >= g_tab.codes.size()) lang = (int)g_tab.meta.unknown_language;
+  return (size_t)lang < g_tab.codes.size() ? g_tab.codes[lang] : "un";
 }
 
 }  // extern "C"

@@ -169,3 +169,103 @@ def test_concurrent_request_sized_calls_coalesce(gpu, oracle):
     for k in range(24):
         lo, hi = int(parts[k][0]), int(parts[k][-1]) + 1
         assert_same(got[k], (want_be if k % 2 else want)[lo:hi], "caller %d" % k)
+
+
+CHUNKED = r'''
+import numpy as np
+import cld_amd, corpus
+from oracle import Oracle
+from test_gpu_parity import assert_same
+cld_amd.init()
+o = Oracle()
+# 1 MB chunks: C2 streams through ~9 chunks in two alternating slots, C5
+# (tail-bound: 4 MB chunks) through several; pageable and pinned result arrays
+for name, (b, off) in (("c2", corpus.c2(60000, seed=141)), ("c5", corpus.c5(20000, seed=142))):
+    want = o.detect_batch(b, off, threads=16)
+    for rep in range(3):
+        assert_same(cld_amd.detect_batch(buf=b, offsets=off), want, "%s chunked rep %d" % (name, rep))
+print("chunked ok")
+'''
+
+
+def test_streamed_chunks_reuse_slots_safely():
+    """The streamed host path alternates two chunk slots, so chunk c writes the
+    device results of chunk c-2's slot while c-2's download may still be
+    queued (cld_runtime.cpp run_host_stream: the kernels of chunk c wait for
+    that download on the device).  With CLD_CHUNK_MB=1 every batch here is
+    many chunks; every result must equal the oracle's, three times over."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CLD_CHUNK_MB="1",
+               PYTHONPATH=os.pathsep.join(os.path.join(root, p) for p in ("language-detector_amd", "oracle", "tests")))
+    r = subprocess.run([sys.executable, "-c", CHUNKED], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "chunked ok" in r.stdout
+
+
+def test_tiny_batches_equal_the_oracle(gpu, oracle):
+    """Request-sized batches of short documents take run_tiny (one upload, one
+    k_wave launch, one download; cld_runtime.cpp).  Batches of 1..1024
+    documents -- tweets, CJK, and short documents k_wave hands on (several
+    script spans), which the tiny path redoes on the streamed path -- must
+    equal the oracle, alone and from 16 concurrent callers; a clean tweet batch
+    must have run on the tiny path (no kernel events: short_ms == 0)."""
+    import threading
+    from test_gpu_parity import EDGE
+    b2, o2 = corpus.c2(3000, seed=151)
+    b4, o4 = corpus.c4(2000, seed=152)
+    docs = [bytes(b2[o2[i]:o2[i + 1]]) for i in range(3000)] + [bytes(b4[o4[i]:o4[i + 1]]) for i in range(2000)]
+    docs = [d for d in docs if len(d) <= 256]
+    mixed = [("abc рус %d العربية ok " % k).encode() for k in range(40)] + [e for e in EDGE if len(e) <= 256]
+    rng = np.random.default_rng(153)
+    batches = []
+    for size in (1, 2, 7, 64, 255, 1000, 1024):
+        pick = [docs[int(i)] for i in rng.integers(0, len(docs), size)]
+        if size in (7, 255):
+            for j, m in zip(range(0, size, 3), mixed):
+                pick[j] = m
+        batches.append(pick)
+    for pick in batches:
+        pb, po = gpu.pack(pick)
+        assert_same(gpu.detect_batch(buf=pb, offsets=po), oracle.detect_batch(pb, po, threads=8), "tiny %d" % len(pick))
+    pb, po = gpu.pack(docs[:500])
+    gpu.detect_batch(buf=pb, offsets=po)
+    st = gpu.last_stats(0)
+    assert st.short_docs == 500 and st.short_ms == 0, (st.short_docs, st.short_ms)
+    got = [None] * 16
+    packed = [gpu.pack(batches[k % len(batches)]) for k in range(16)]
+
+    def work(k):
+        for rep in range(4):
+            got[k] = gpu.detect_batch(buf=packed[k][0], offsets=packed[k][1])
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(16)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for k in range(16):
+        assert_same(got[k], oracle.detect_batch(*packed[k], threads=8), "concurrent tiny %d" % k)
+
+
+def test_detect_language_many_callers(gpu, oracle):
+    """wrapper.h detect_language from 64 threads at once over tweets, CJK and
+    long pages (coalesced micro-batches: tiny groups on run_tiny, the rest on
+    the streamed path) equals the oracle's DetectLanguage answer per document."""
+    import threading
+    b2, o2 = corpus.c2(1500, seed=161)
+    b5, o5 = corpus.c5(500, seed=162)
+    texts = [bytes(b2[o2[i]:o2[i + 1]]) for i in range(1500)]
+    texts += [bytes(b5[o5[i]:o5[i + 1]]) for i in range(500)]
+    want = [oracle.detect_language(t) for t in texts]
+    got = [None] * len(texts)
+
+    def worker(lo):
+        for i in range(lo, len(texts), 64):
+            got[i] = gpu.detect_language(texts[i])
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(64)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    bad = [i for i in range(len(texts)) if got[i] != want[i]]
+    assert not bad, (len(bad), bad[:5], [got[i] for i in bad[:5]], [want[i] for i in bad[:5]])
