@@ -26,6 +26,7 @@
 #include <thread>
 #include <vector>
 
+#include "cld_coalesce.h"
 #include "cld_device.h"
 #include "cld_dynamic_data.h"
 #include "cld_hints.h"
@@ -1791,49 +1792,13 @@ Device* pick_context();
 // the company a document keeps.
 constexpr uint64_t kCoalesceBytes = 64ull << 20;
 constexpr size_t kCoalesceDocs = 256 * 1024;
-struct Req {
-  const uint8_t* buf;
-  const uint64_t* offs;
-  size_t n;
-  cld_result* out;
-  uint32_t flags;
-  bool tiny;                    // run_tiny-sized: every document <= kWaveCap, n <= kTinyDocs, no preparation
-  int rc = CLD_OK;
-  // Parking: a queued caller sleeps on its own condition variable until its
-  // group is done (kDone) or it is promoted to form the next group (kLead).
-  // One shared condition variable woke all of them at every dispatch, and
-  // their re-acquiring the queue lock one by one cost ~1 ms per dispatch at
-  // 256 callers.  Done callers are woken as a binary tree: each wakes `kid`
-  // before returning, so no thread issues more than two wake-ups.
-  enum { kWaiting = 0, kDone = 1, kLead = 2 };
-  std::mutex m;
-  std::condition_variable cv;
-  int state = kWaiting;
-  bool promoted = false;        // under g_rq_mu: already asked to lead
-  Req* kid[2] = {nullptr, nullptr};
-  Req(const uint8_t* b, const uint64_t* o, size_t n_, cld_result* r, uint32_t f, bool t)
-      : buf(b), offs(o), n(n_), out(r), flags(f), tiny(t) {}
-  void post(int st) {
-    { std::lock_guard<std::mutex> l(m); state = st; }
-    cv.notify_one();
-  }
-  int park() {
-    std::unique_lock<std::mutex> l(m);
-    cv.wait(l, [&] { return state != kWaiting; });
-    const int st = state;
-    if (st == kLead) state = kWaiting;
-    return st;
-  }
-};
+using cld::CoReq;
 bool tiny_request(const uint64_t* offs, size_t n, uint32_t flags) {
   if (n > kTinyDocs || (flags & kPrepFlags) || !tiny_enabled()) return false;
   uint64_t bad = 0;
   for (size_t i = 0; i < n; ++i) bad |= (uint64_t)(offs[i + 1] - offs[i] > (uint64_t)kWaveCap);
   return bad == 0;
 }
-std::mutex g_rq_mu;
-std::deque<Req*> g_rq;
-int g_rq_active = 0;
 struct Arena {                  // pinned staging of one dispatch (reused)
   uint8_t* buf = nullptr; size_t buf_cap = 0;
   uint64_t* offs = nullptr; size_t offs_cap = 0;
@@ -1842,11 +1807,11 @@ struct Arena {                  // pinned staging of one dispatch (reused)
 std::mutex g_arena_mu;
 std::vector<Arena*> g_arenas;   // free arenas
 
-void run_group(const std::vector<Req*>& grp) {
+void run_group(const std::vector<CoReq*>& grp, void*) {
   if (grp.size() == 1) {        // nothing to merge: straight from the caller's buffers
-    Req* r = grp[0];
+    CoReq* r = grp[0];
     Picked p(pick_context());
-    r->rc = run_host_shard_isolating(p.d, r->buf, r->offs, r->n, r->out, r->flags);
+    r->rc = run_host_shard_isolating(p.d, r->buf, r->offs, r->n, (cld_result*)r->out, r->flags);
     return;
   }
   Arena* a = nullptr;
@@ -1857,7 +1822,7 @@ void run_group(const std::vector<Req*>& grp) {
   if (!a) a = new Arena();
   size_t docs = 0;
   uint64_t bytes = 0;
-  for (Req* r : grp) { docs += r->n; bytes += r->offs[r->n] - r->offs[0]; }
+  for (CoReq* r : grp) { docs += r->n; bytes += r->offs[r->n] - r->offs[0]; }
   int rc = CLD_OK;
   if (grow_host(&a->buf, &a->buf_cap, std::max<uint64_t>(bytes, 1)) || grow_host(&a->offs, &a->offs_cap, docs + 1) ||
       grow_host(&a->out, &a->out_cap, docs))
@@ -1865,7 +1830,7 @@ void run_group(const std::vector<Req*>& grp) {
   if (rc == CLD_OK) {
     size_t k = 0;
     uint64_t at = 0;
-    for (Req* r : grp) {
+    for (CoReq* r : grp) {
       const uint64_t b0 = r->offs[0], nb = r->offs[r->n] - b0;
       memcpy(a->buf + at, r->buf + b0, nb);
       for (size_t i = 0; i < r->n; ++i) a->offs[k + i] = at + (r->offs[i] - b0);
@@ -1877,11 +1842,12 @@ void run_group(const std::vector<Req*>& grp) {
     rc = run_host_shard_isolating(p.d, a->buf, a->offs, docs, a->out, grp[0]->flags);
   }
   size_t k = 0;
-  for (Req* r : grp) {
+  for (CoReq* r : grp) {
+    cld_result* ro = (cld_result*)r->out;
     if (rc == CLD_OK || rc == CLD_EIO) {
-      memcpy(r->out, a->out + k, r->n * sizeof(cld_result));
+      memcpy(ro, a->out + k, r->n * sizeof(cld_result));
       bool failed = false;
-      for (size_t i = 0; i < r->n && rc == CLD_EIO; ++i) failed |= r->out[i].summary_lang == CLD_LANG_FAILED;
+      for (size_t i = 0; i < r->n && rc == CLD_EIO; ++i) failed |= ro[i].summary_lang == CLD_LANG_FAILED;
       r->rc = failed ? CLD_EIO : CLD_OK;
     } else {
       r->rc = rc;
@@ -1892,91 +1858,31 @@ void run_group(const std::vector<Req*>& grp) {
   g_arenas.push_back(a);
 }
 
-// Dispatch slots: one per context for any group, and up to kTinySlots per
-// context while the extra ones carry tiny groups (run_tiny: each tiny slot has
-// its own stream and buffers, so two such calls overlap on one GPU -- one
-// uploads or synchronises while the other's kernel runs).  A group whose
-// first request is tiny takes only tiny requests, up to kTinyDocs documents,
-// so it stays on run_tiny.  Caller holds g_rq_mu.
-bool form_group(std::vector<Req*>* grp) {
-  const int ndev = (int)g_devs.size();
-  const bool any_slot = g_rq_active < ndev;
-  if (g_rq.empty() || !(any_slot || g_rq_active < ndev * kTinySlots)) return false;
-  const Req* first = nullptr;
-  for (Req* r : g_rq)
-    if (any_slot || r->tiny) { first = r; break; }
-  if (!first) return false;
-  const uint32_t f = first->flags;
-  const bool tiny = first->tiny;
-  uint64_t bytes = 0;
-  size_t docs = 0;
-  grp->clear();
-  for (auto it = g_rq.begin(); it != g_rq.end();) {
-    Req* r = *it;
-    const uint64_t nb = r->offs[r->n] - r->offs[0];
-    const bool fits = tiny ? r->tiny && docs + r->n <= kTinyDocs
-                           : grp->empty() || (bytes + nb <= kCoalesceBytes && docs + r->n <= kCoalesceDocs);
-    if (r->flags != f || !fits) {
-      ++it;
-      continue;
-    }
-    grp->push_back(r);
-    bytes += nb;
-    docs += r->n;
-    it = g_rq.erase(it);
-  }
-  ++g_rq_active;
-  return true;
+// Dispatch slots (cld_coalesce.h): one per context for any group, and up to
+// kTinySlots per context while the extra ones carry tiny groups (run_tiny:
+// each tiny slot has its own stream and buffers, so two such calls overlap on
+// one GPU -- one uploads or synchronises while the other's kernel runs).
+// Waiters spin CLD_COALESCE_SPIN_US (default 50) before they sleep: a tiny
+// round trip is ~35 us.
+cld::Coalescer* coalescer() {
+  static cld::Coalescer* c = [] {
+    cld::Coalescer* x = new cld::Coalescer();   // never destroyed (callers may be parked at exit)
+    x->run = run_group;
+    x->tiny_docs = kTinyDocs;
+    x->max_bytes = kCoalesceBytes;
+    x->max_docs = kCoalesceDocs;
+    x->spin_us = getenv("CLD_COALESCE_SPIN_US") ? atoi(getenv("CLD_COALESCE_SPIN_US")) : 50;
+    return x;
+  }();
+  return c;
 }
 
 int run_coalesced(const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
-  Req me(buf, offs, n, out, flags, tiny_request(offs, n, flags));
-  std::vector<Req*> grp;
-  std::unique_lock<std::mutex> lk(g_rq_mu);
-  g_rq.push_back(&me);
-  for (;;) {
-    {  // a promoted caller whose request another dispatcher has meanwhile run
-      std::lock_guard<std::mutex> l(me.m);
-      if (me.state == Req::kDone) {
-        lk.unlock();
-        for (Req* k : me.kid) if (k) k->post(Req::kDone);
-        return me.rc;
-      }
-    }
-    if (!form_group(&grp)) {
-      lk.unlock();
-      if (me.park() == Req::kDone) {
-        for (Req* k : me.kid) if (k) k->post(Req::kDone);
-        return me.rc;
-      }
-      lk.lock();                               // promoted: form the next group
-      me.promoted = false;
-      continue;
-    }
-    lk.unlock();
-    run_group(grp);
-    // wake-up tree over the other members (set before any wake-up: a woken
-    // member returns, and its Req with it)
-    std::vector<Req*> others;
-    bool mine = false;
-    for (Req* r : grp) {
-      if (r == &me) mine = true;
-      else others.push_back(r);
-    }
-    for (size_t j = 0; j < others.size(); ++j)
-      for (int c = 0; c < 2; ++c) {
-        const size_t k = 2 * j + 2 + c;
-        others[j]->kid[c] = k < others.size() ? others[k] : nullptr;
-      }
-    lk.lock();
-    --g_rq_active;
-    for (Req* r : g_rq)                        // the next group's dispatcher
-      if (!r->promoted && r != &me) { r->promoted = true; r->post(Req::kLead); break; }
-    lk.unlock();
-    for (size_t j = 0; j < 2 && j < others.size(); ++j) others[j]->post(Req::kDone);
-    if (mine) return me.rc;
-    lk.lock();
-  }
+  cld::Coalescer& co = *coalescer();
+  co.slots_any.store((int)g_devs.size(), std::memory_order_relaxed);   // (fixed while g_swap_mu is held)
+  co.slots_tiny.store((int)g_devs.size() * kTinySlots, std::memory_order_relaxed);
+  CoReq me(buf, offs, n, out, flags, tiny_request(offs, n, flags));
+  return co.submit(&me);
 }
 
 Device* pick_context() {
