@@ -357,7 +357,11 @@ constexpr size_t kTinyDocs = 1024;
 constexpr size_t kTinyCtrOff = kTinyDocs * sizeof(cld_result);
 constexpr size_t kTinyOffsOff = kTinyCtrOff + kCtrSlots * sizeof(uint32_t);
 constexpr size_t kTinyBlock = kTinyOffsOff + (kTinyDocs + 1) * sizeof(uint64_t) + kTinyDocs * kWaveCap + 256;
-constexpr int kTinySlots = 2;   // calls in flight per context (each its own stream)
+constexpr int kTinySlotsMax = 4;   // calls in flight per context (each its own stream); CLD_TINY_SLOTS, default 4
+int tiny_slots() {
+  static const int v = getenv("CLD_TINY_SLOTS") ? std::max(1, std::min(kTinySlotsMax, atoi(getenv("CLD_TINY_SLOTS")))) : 4;
+  return v;
+}
 struct TinySlot {
   hipStream_t s = nullptr;
   uint8_t* h = nullptr;          // pinned
@@ -454,7 +458,7 @@ struct Device {
     cld_chunk* compact = nullptr; size_t compact_cap = 0;
     uint8_t* vslots = nullptr;   // k_long<VEC>: one VecSlot per slot of d_slots (on first use)
   } vec;
-  TinySlot tiny[kTinySlots];      // run_tiny: k_wave-only calls, independent of the scratch above
+  TinySlot tiny[kTinySlotsMax];   // run_tiny: k_wave-only calls, independent of the scratch above (tiny_slots() used)
   std::atomic<unsigned> tiny_rr{0};
   std::mutex mu;
   std::atomic<int> inflight{0};   // calls routed to this context and not yet returned (pick_context)
@@ -568,6 +572,16 @@ int swap_tables_all(const HostTables& nt);
 
 int init_device(Device* d) {
   HIP_OK(hipSetDevice(d->id));
+  // CLD_SYNC=block|spin|yield: how host threads wait for the GPU (HIP's
+  // default decides by itself).  Waiting callers burn CPU when they spin,
+  // which a CPU-quota'd service may not have to spare.
+  if (const char* e = getenv("CLD_SYNC")) {
+    const unsigned f = !strcmp(e, "block") ? hipDeviceScheduleBlockingSync
+                       : !strcmp(e, "spin") ? hipDeviceScheduleSpin
+                       : !strcmp(e, "yield") ? hipDeviceScheduleYield : hipDeviceScheduleAuto;
+    (void)hipSetDeviceFlags(f);
+    (void)hipGetLastError();
+  }
   HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&d->up_stream, hipStreamNonBlocking));
   HIP_OK(hipStreamCreateWithFlags(&d->down_stream, hipStreamNonBlocking));
@@ -579,7 +593,8 @@ int init_device(Device* d) {
     HIP_OK(hipEventCreateWithFlags(&h.down, hipEventDisableTiming));
   }
   if (int rc = upload_tables(d, g_tab)) return rc;
-  for (TinySlot& t : d->tiny) {
+  for (int k = 0; k < tiny_slots(); ++k) {
+    TinySlot& t = d->tiny[k];
     HIP_OK(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc((void**)&t.h, kTinyBlock, hipHostMallocDefault));
     HIP_OK(hipHostGetDevicePointer((void**)&t.hd, t.h, 0));
@@ -1171,12 +1186,13 @@ bool tiny_zero_copy() {
 int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
   TinySlot* t = nullptr;
   std::unique_lock<std::mutex> lk;
-  for (TinySlot& x : d->tiny) {
-    std::unique_lock<std::mutex> l(x.mu, std::try_to_lock);
-    if (l.owns_lock()) { t = &x; lk = std::move(l); break; }
+  const int ns = tiny_slots();
+  for (int k = 0; k < ns; ++k) {
+    std::unique_lock<std::mutex> l(d->tiny[k].mu, std::try_to_lock);
+    if (l.owns_lock()) { t = &d->tiny[k]; lk = std::move(l); break; }
   }
   if (!t) {
-    t = &d->tiny[d->tiny_rr.fetch_add(1) % kTinySlots];
+    t = &d->tiny[d->tiny_rr.fetch_add(1) % ns];
     lk = std::unique_lock<std::mutex>(t->mu);
   }
   HIP_OK(hipSetDevice(d->id));
@@ -1859,11 +1875,13 @@ void run_group(const std::vector<CoReq*>& grp, void*) {
 }
 
 // Dispatch slots (cld_coalesce.h): one per context for any group, and up to
-// kTinySlots per context while the extra ones carry tiny groups (run_tiny:
+// tiny_slots() per context while the extra ones carry tiny groups (run_tiny:
 // each tiny slot has its own stream and buffers, so two such calls overlap on
 // one GPU -- one uploads or synchronises while the other's kernel runs).
-// Waiters spin CLD_COALESCE_SPIN_US (default 50) before they sleep: a tiny
-// round trip is ~35 us.
+// Waiters sleep at once (CLD_COALESCE_SPIN_US: spin that long first): on a
+// CPU-quota'd host (16 cores on the GPU box), spinning callers used up the
+// quota and the cgroup throttled the whole process for the rest of its
+// 100 ms period (gpurun_out/r5d).
 cld::Coalescer* coalescer() {
   static cld::Coalescer* c = [] {
     cld::Coalescer* x = new cld::Coalescer();   // never destroyed (callers may be parked at exit)
@@ -1871,7 +1889,10 @@ cld::Coalescer* coalescer() {
     x->tiny_docs = kTinyDocs;
     x->max_bytes = kCoalesceBytes;
     x->max_docs = kCoalesceDocs;
-    x->spin_us = getenv("CLD_COALESCE_SPIN_US") ? atoi(getenv("CLD_COALESCE_SPIN_US")) : 50;
+    x->spin_us = getenv("CLD_COALESCE_SPIN_US") ? atoi(getenv("CLD_COALESCE_SPIN_US")) : 0;
+    // the dispatcher wakes every member itself (CLD_COALESCE_WAKE=tree: members
+    // wake each other): 256 callers 146K -> 263K docs/s, p99 74 -> 20 ms (r5d)
+    x->tree_wake = getenv("CLD_COALESCE_WAKE") && !strcmp(getenv("CLD_COALESCE_WAKE"), "tree");
     return x;
   }();
   return c;
@@ -1880,7 +1901,7 @@ cld::Coalescer* coalescer() {
 int run_coalesced(const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
   cld::Coalescer& co = *coalescer();
   co.slots_any.store((int)g_devs.size(), std::memory_order_relaxed);   // (fixed while g_swap_mu is held)
-  co.slots_tiny.store((int)g_devs.size() * kTinySlots, std::memory_order_relaxed);
+  co.slots_tiny.store((int)g_devs.size() * tiny_slots(), std::memory_order_relaxed);
   CoReq me(buf, offs, n, out, flags, tiny_request(offs, n, flags));
   return co.submit(&me);
 }
