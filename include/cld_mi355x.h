@@ -156,7 +156,14 @@ int cld_stage_cycles(int ctx, uint64_t* cycles16);
  * results are in `out`.  Documents are sharded across the initialised GPUs
  * by estimated cost; each shard streams through the GPU in chunks of <= 64 MB /
  * 512K documents (pinned staging, upload / kernels / download overlapped on
- * three streams).  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING and
+ * three streams).  A batch whose mean document is longer than 256 bytes goes
+ * in chunks of <= 256 MB / 2M documents instead: each of a context's two chunk
+ * slots then holds up to 256 MB of text plus 48 B per document in device
+ * memory, and as much pinned host staging unless the caller's buffers are
+ * pinned (CLD_CHUNK_MB scales both).  Request-sized calls (< 16 MB of text)
+ * from concurrent callers are coalesced into one GPU batch; a batch of at
+ * most 1024 documents of <= 256 bytes takes one upload, one kernel and one
+ * download.  flags: 0 or CLD_FLAG_STRIP_EXTRAS / CLD_FLAG_CSTRING and
  * CLD_FLAG_SCORE_AS_QUADS / CLD_FLAG_BEST_EFFORT (above).  Thread-safe. */
 int cld_detect_batch(const uint8_t* buf, const uint64_t* offsets, size_t n,
                      cld_result* out, uint32_t flags);
