@@ -22,7 +22,11 @@ constexpr int kMaxLgProbScore = 16;
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
        kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
        kCtrSpecial = 16, kCtrSpecTake = 17 /* k_long: speculative pass-2 results taken */,
-       kCtrSpecDone = 18 /* k_long: waves finished (speculating launches) */, kCtrSlots = 32 };
+       kCtrSpecDone = 18 /* k_long: waves finished (speculating launches) */,
+       // staged long-document path (k_lspan / k_lscore / k_lrep): list counts and dequeue cursors
+       kCtrStFall = 19 /* to the fused k_long */, kCtrStDqSpan = 20, kCtrStOk = 21 /* spans stored */,
+       kCtrStDqS1 = 22, kCtrStP2 = 23 /* pass 2 */, kCtrStDqRep = 24, kCtrStDqS2 = 25, kCtrStDqFall = 26,
+       kCtrStPool = 27 /* store 256-byte units taken */, kCtrSlots = 32 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.
@@ -123,10 +127,26 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           cld_result* spec_out, uint32_t* spec_take, hipStream_t s);
+                           cld_result* spec_out, uint32_t* spec_take, int ctr_total, int ctr_deq, hipStream_t s);
 // spec_out / spec_take (nullable: no speculation): cld_long_spec_docs(n_slots)
 // results and u32 entries, k_long's speculative pass-2 results for the
 // longest documents of a small batch.
 size_t cld_long_spec_docs(int n_slots);
+// Staged long-document path (cld_long.hip, "staged long-document path"):
+// k_lspan over `list` (counters[kCtrRequeue] documents) stores pass 1's spans
+// in `pool` (meta[k]: the region of list entry k) and lists the entries it
+// took (ok_list) and the documents it did not (fall_list, for the fused
+// k_long: cld_launch_long with kCtrStFall / kCtrStDqFall); k_lscore scores
+// pass 1 (to p2_list when not good enough), k_lrep runs Repeats over those,
+// k_lscore<pass 2> finishes them.  small_total: a list this short goes whole
+// to the fused kernel, in order (its speculation is for small batches).
+// n_waves: resident waves the staged kernels may use (slots).
+int cld_staged_waves_per_simd();
+hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                             cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
+                             uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
+                             uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
+                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
+                             uint32_t small_total, hipStream_t s);
 }
 #endif

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
                                                   cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
                                                   int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ hpos,
                                                   const uint32_t* __restrict__ hgap, cld_result* __restrict__ spec_out,
-                                                  uint32_t* __restrict__ spec_take) {
+                                                  uint32_t* __restrict__ spec_take, int ctr_total, int ctr_deq) {
   __shared__ lng::Smem smem[WPB];
   const DevTables& T = *Tp;
   // wave index through readfirstlane: the slot pointer (and every S.field
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
   uint32_t* tr = (DIAG && trace) ? trace + 4 * (blockIdx.x * WPB + wv) : nullptr;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::Slot));
   const uint32_t total =
-      wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      wave::uflu(__hip_atomic_load(&counters[ctr_total], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (total == 0) return;                       // empty re-queue list: no dequeue atomics at all
   // Speculation (small batches only, so full batches keep their throughput):
   // the first nspec documents of the longest-first list -- the ones a small
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     // Whole-wave atomic (lane 0 adds 1, the others 0) read back from lane 0.
     // A lane-0-only atomic feeding readfirstlane at the loop head let the
     // compiler split the loop so the other lanes re-read k = 0 forever.
-    const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrDequeue], lane == 0 ? 1u : 0u));
+    const uint32_t e = wave::uflu(atomicAdd(&counters[ctr_deq], lane == 0 ? 1u : 0u));
     if (e >= entries) break;
     const uint32_t k = e < 2 * nspec ? e >> 1 : e - nspec;      // list position
     const int mode = e < 2 * nspec ? ((e & 1) ? lng::kPassRepeatsOnly : lng::kPassFirstOnly) : lng::kPassesAll;
@@ -426,6 +426,144 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     }
   }
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 100, total);
+}
+
+// ------------------------------------------------ staged long-document path
+// (cld_long.hip, st_spans / st_score / st_rep).  Persistent grids, one wave
+// per document at a time, each with its own occupancy: LNG_ST_WPS waves per
+// SIMD for k_lspan / k_lscore (their registers fit 96 VGPRs; k_lscore's LDS is
+// the LNG_ST_TEXT text window without the Repeats predictor), LNG_REP_WPS for
+// k_lrep (one wave per workgroup, 8 KB of LDS predictor each).
+#ifndef LNG_ST_WPS
+#define LNG_ST_WPS 5
+#endif
+#ifndef LNG_REP_WPS
+#define LNG_REP_WPS 5
+#endif
+#ifndef LNG_ST_TEXT
+#define LNG_ST_TEXT 5120
+#endif
+constexpr int kStWPB = 4;
+using StSmem = lng::SmemT<LNG_ST_TEXT, false>;
+static_assert(kStWPB * sizeof(StSmem) * (4 * LNG_ST_WPS / kStWPB) <= 160 * 1024, "k_lscore LDS per CU");
+
+__global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lspan(
+    const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
+    uint64_t* __restrict__ meta, uint32_t* __restrict__ ok_list, uint32_t* __restrict__ fall_list,
+    uint32_t* __restrict__ counters, const uint8_t* __restrict__ special, const uint8_t* __restrict__ hbuf,
+    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total) {
+  const DevTables& T = *Tp;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
+  const uint32_t total =
+      wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (total == 0) return;
+  if (total <= small_total) {                    // a small batch: the fused kernel takes it all, in list order
+    if (blockIdx.x == 0) {
+      for (uint32_t k = threadIdx.x; k < total; k += blockDim.x) fall_list[k] = list[k];
+      if (threadIdx.x == 0) counters[kCtrStFall] = total;
+    }
+    return;
+  }
+  const bool exact = lng::space_lowers_to_space(T);
+  const uint64_t units = pool_bytes >> 8;
+  for (;;) {
+    const uint32_t k = wave::uflu(atomicAdd(&counters[kCtrStDqSpan], lane == 0 ? 1u : 0u));
+    if (k >= total) break;                       // every wave reaches this exit
+    const uint32_t i = list[k];
+    const uint64_t a = offs[i], L = offs[i + 1] - a;
+    const uint8_t spi = special ? special[i] : (uint8_t)0;
+    const bool rw = (spi & kSpecialRewritten) != 0;
+    bool ok = exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc;
+    uint64_t at = 0;
+    const uint64_t need = lng::st_region_bytes(L);
+    if (ok) {
+      const uint32_t u = (uint32_t)((need + 255) >> 8);
+      uint32_t got = 0;
+      if (lane == 0) got = atomicAdd(&counters[kCtrStPool], u);
+      got = wave::uflu(__shfl((int)got, 0, 64));
+      ok = (uint64_t)got + u <= units;
+      at = (uint64_t)got << 8;
+    }
+    if (ok) {
+      const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
+      ok = lng::st_spans(T, dv, S, pool + at, need, lane);
+    }
+    if (lane == 0) {
+      if (ok) {
+        meta[k] = at;
+        ok_list[atomicAdd(&counters[kCtrStOk], 1u)] = k;
+      } else {
+        fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
+      }
+    }
+  }
+}
+
+template <bool P2>
+__global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
+    const DevTables* __restrict__ Tp, const uint32_t* __restrict__ list, cld_result* __restrict__ out,
+    uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, const uint64_t* __restrict__ meta,
+    const uint32_t* __restrict__ in_list, uint32_t* __restrict__ p2_list, uint32_t* __restrict__ requeue2,
+    uint32_t* __restrict__ counters, uint32_t cflags, const uint8_t* __restrict__ special,
+    const uint32_t* __restrict__ priors) {
+  __shared__ StSmem smem[kStWPB];
+  const DevTables& T = *Tp;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
+  const uint32_t total = wave::uflu(
+      __hip_atomic_load(&counters[P2 ? kCtrStP2 : kCtrStOk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (total == 0) return;
+  if (lane == 0) {
+    smem[wv].dbg = nullptr;
+    smem[wv].dbg_pos = 0;
+    smem[wv].prof = nullptr;
+  }
+  for (;;) {
+    const uint32_t e = wave::uflu(atomicAdd(&counters[P2 ? kCtrStDqS2 : kCtrStDqS1], lane == 0 ? 1u : 0u));
+    if (e >= total) break;                       // every wave reaches this exit
+    const uint32_t k = in_list[e];
+    const uint64_t at = meta[k];
+    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
+    const uint32_t i = list[k];
+    const uint8_t spi = special ? special[i] : (uint8_t)0;
+    const int r = lng::st_score(T, S, smem[wv], pool + at, P2, &out[i], cflags,
+                                (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, lane);
+    if (lane == 0) {
+      if (r == 1) {
+        atomicAdd(&counters[P2 ? kCtrPass2 : kCtrPass1], 1u);
+      } else if (r == 0 && !P2) {
+        p2_list[atomicAdd(&counters[kCtrStP2], 1u)] = k;
+      } else {                                   // capacity (or a pass 2 that did not finish): k_general
+        requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = i;
+        atomicAdd(&counters[kCtrWhy + lng::kWhyCapacity], 1u);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __restrict__ list,
+                                                         uint8_t* __restrict__ slots, uint8_t* __restrict__ pool,
+                                                         uint64_t* __restrict__ meta,
+                                                         const uint32_t* __restrict__ p2_list,
+                                                         uint32_t* __restrict__ requeue2,
+                                                         uint32_t* __restrict__ counters) {
+  __shared__ __attribute__((aligned(16))) uint16_t pred[kPredictionTableSize];
+  const int lane = threadIdx.x & 63;
+  lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)blockIdx.x * sizeof(lng::Slot));
+  const uint32_t total =
+      wave::uflu(__hip_atomic_load(&counters[kCtrStP2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (;;) {
+    const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrStDqRep], lane == 0 ? 1u : 0u));
+    if (e >= total) break;                       // every wave reaches this exit
+    const uint32_t k = p2_list[e];
+    if (!lng::st_rep(pred, S, pool + meta[k], lane) && lane == 0) {
+      meta[k] = lng::kStNone;
+      requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = list[k];
+      atomicAdd(&counters[kCtrWhy + lng::kWhySpan], 1u);
+    }
+  }
 }
 
 // Longest-first order for k_long's persistent grid (LPT list scheduling):
@@ -574,7 +712,7 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           cld_result* spec_out, uint32_t* spec_take, hipStream_t s) {
+                           cld_result* spec_out, uint32_t* spec_take, int ctr_total, int ctr_deq, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
@@ -582,14 +720,40 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take, ctr_total,
+                       ctr_deq);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take);
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take, ctr_total,
+                       ctr_deq);
   return hipGetLastError();
 }
 size_t cld_long_spec_docs(int n_slots) { return (size_t)n_slots / cld::kSpecShare; }
+
+int cld_staged_waves_per_simd() { return LNG_ST_WPS > LNG_REP_WPS ? LNG_ST_WPS : LNG_REP_WPS; }
+
+hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
+                             cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
+                             uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
+                             uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
+                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
+                             uint32_t small_total, hipStream_t s) {
+  // n_waves: the slots (resident waves) of the widest launch below
+  const int per_simd = cld_staged_waves_per_simd();
+  const int cus = n_waves / (4 * per_simd);
+  if (cus < 1) return hipErrorInvalidValue;
+  const dim3 gst(cus * 4 * LNG_ST_WPS / cld::kStWPB), bst(64 * cld::kStWPB);
+  hipLaunchKernelGGL(cld::k_lspan, gst, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
+                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total);
+  hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
+                     requeue2, counters, cflags, special, priors);
+  hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,
+                     requeue2, counters);
+  hipLaunchKernelGGL(cld::k_lscore<true>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, p2_list, p2_list,
+                     requeue2, counters, cflags, special, priors);
+  return hipGetLastError();
+}
 
 size_t cld_vec_slot_bytes() { return sizeof(cld::lng::VecSlot); }
 
@@ -610,7 +774,8 @@ hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const u
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                      requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
-                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap, nullptr, nullptr);
+                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap, nullptr, nullptr, kCtrRequeue,
+                     kCtrDequeue);
   return hipGetLastError();
 }
 

@@ -130,11 +130,14 @@ struct Slot {
 // Per-wave LDS (16-byte aligned: the tote is zeroed and read as uint4).  The
 // scoring state and the Repeats predictor are never live together (pass 2
 // runs CheapRepWordsInplace over every cached span before scoring any, see
-// rep_all), so they share the first 8 KB.
-struct alignas(16) Smem {
+// rep_all), so they share the first 8 KB.  The staged kernels (k_lspan /
+// k_lscore / k_lrep) score without the predictor and with a smaller text
+// window: SmemT<TEXT, false> (the stage functions take either layout).
+template <int TEXT, bool PRED>
+struct alignas(16) SmemT {
   union {
     struct {
-      uint8_t text[kLdsText];            // a window of the current span's lowered text (Win)
+      uint8_t text[TEXT];                // a window of the current span's lowered text (Win)
       uint32_t tote[256];                // chunk tote, one key per word (uint16 wrap applied at read)
       uint32_t lo[kMaxCh];               // first offset of chunk k
       union {
@@ -146,7 +149,7 @@ struct alignas(16) Smem {
         };
       };
     };
-    uint16_t pred[kPredictionTableSize]; // Repeats predictor, 16-bit codes (pred_code)
+    uint16_t pred[PRED ? kPredictionTableSize : 1];   // Repeats predictor, 16-bit codes (pred_code)
   };
   uint64_t ring[2][4];                   // distinct boosts (as tote adds), latn / othr, oldest first
   uint64_t pri_add[2][4];                // ApplyHints prior boosts (as tote adds), latn / othr (has_pri)
@@ -157,6 +160,7 @@ struct alignas(16) Smem {
   uint32_t dbg_pos;
   unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
 };
+using Smem = SmemT<kLdsText, true>;
 static_assert(sizeof(Smem) <= 10240, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
 
 // ------------------------------------------------ ResultChunkVector (vec mode)
@@ -205,7 +209,8 @@ constexpr bool kProfSub = true;
 #else
 constexpr bool kProfSub = false;
 #endif
-__device__ __forceinline__ void mark(Smem& s, int lane, int stage, long long& t) {
+template <class SM>
+__device__ __forceinline__ void mark(SM& s, int lane, int stage, long long& t) {
   if (kProfSub && stage != 7) stage = 6;
   if (s.prof) {
     const long long now = (long long)clock64();
@@ -213,7 +218,8 @@ __device__ __forceinline__ void mark(Smem& s, int lane, int stage, long long& t)
     t = now;
   }
 }
-__device__ __forceinline__ void mark_sub(Smem& s, int lane, int stage, long long& t) {
+template <class SM>
+__device__ __forceinline__ void mark_sub(SM& s, int lane, int stage, long long& t) {
   if (kProfSub && s.prof) {
     const long long now = (long long)clock64();
     if (lane == 0) atomicAdd(&s.prof[stage], (unsigned long long)(now - t));
@@ -224,7 +230,8 @@ __device__ __forceinline__ void mark_sub(Smem& s, int lane, int stage, long long
 // Debug dump records (u32 words): 'S' span {ul, tb, pass}; 'R' round {off, next,
 // nb, nd, nx, then nb+nd+nx (offset, indirect) pairs}; 'C' chunk {lo, hi, lang1,
 // lang2, score1, score2, grams, rel_delta, rel_score}.
-__device__ void dbg_words(Smem& s, int lane, const uint32_t* v, int n) {
+template <class SM>
+__device__ void dbg_words(SM& s, int lane, const uint32_t* v, int n) {
   if (!s.dbg) return;
   if (lane == 0) {
     for (int i = 0; i < n; ++i) s.dbg[1 + s.dbg_pos + i] = v[i];
@@ -1436,7 +1443,8 @@ __device__ __forceinline__ void base_adds(const DevTables& T, const DevTbl& t1, 
 // at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
 // else mid (+1 on a vowel).  It never jumps over a space, so it enters every
 // word at its first byte and a word's entries depend on that word alone.
-__device__ __forceinline__ bool word_lists(Win& win, Smem& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+template <class SM>
+__device__ __forceinline__ bool word_lists(Win& win, SM& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
   lane = wave::lane_here();
   nws = 0;
   nsp = 0;
@@ -1492,7 +1500,8 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
   return cnt;
 }
 
-__device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, int nws, int lane) {
+template <class SM>
+__device__ __forceinline__ int build_chain(Win& win, SM& sm, int tb, Slot& S, int nws, int lane) {
   lane = wave::lane_here();
   int nch = 0;
   int sn = (LNG_PF & 1) && lane < nws ? S.wst[lane] : 0;       // word starts one block ahead
@@ -1531,8 +1540,8 @@ __device__ __forceinline__ int build_chain(Win& win, Smem& sm, int tb, Slot& S, 
 // them), so score_round does not read the hits back; the hit list itself is
 // kept only for the debug dump (D).  Returns the round end (the reference's
 // `next`); c0 advances.
-template <bool D>
-__device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int nch, int& c0, int& nb,
+template <bool D, class SM>
+__device__ __forceinline__ int quad_round(const DevTables& T, Win& win, SM& sm, int tb, Slot& S, int nch, int& c0, int& nb,
                           int& eb, bool& ok, int lane) {
   lane = wave::lane_here();
   nb = 0;
@@ -1642,8 +1651,8 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, Smem& sm
 // hits.  As in quad_round, the hits become emissions here (ed delta / ex
 // distinct with non-zero langprobs, in hit order); the hit lists are kept
 // only for the debug dump (D).
-template <bool D>
-__device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& sm, Slot& S, int nsp, int& j0, int off, int next,
+template <bool D, class SM>
+__device__ __forceinline__ void octa_round(const DevTables& T, Win& win, SM& sm, Slot& S, int nsp, int& j0, int off, int next,
                            int& nd, int& nx, int& edm, int& exm, bool& ok, int lane) {
   lane = wave::lane_here();
   edm = 0;
@@ -1792,8 +1801,8 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, Smem& s
 // GetUniHits + GetBiHits (cldutil.cc:201-310) for one round from off.
 // As in quad_round / octa_round, the hits become emissions here (eb base,
 // edm delta, exm distinct); the hit lists are kept only for the debug dump.
-template <bool D>
-__device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, Smem& sm, int tb, Slot& S, int off, int& nb, int& nd,
+template <bool D, class SM>
+__device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, SM& sm, int tb, Slot& S, int off, int& nb, int& nd,
                          int& nx, int& eb, int& edm, int& exm, bool& ok, int lane) {
   lane = wave::lane_here();
   const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
@@ -1933,7 +1942,8 @@ __device__ uint64_t keytab_eval(const DevTables& T, int ulscript, int k) {
 // (resolve_ref), once their indices are in.  Plain functions rather than
 // lambdas: a captured reference loses its address space, and the slot / LDS
 // reads would become FLAT.
-__device__ __forceinline__ uint64_t chunk_ref(const Slot& S, const Smem& s, uint64_t seed, int rs, int t, int k, int tot,
+template <class SM>
+__device__ __forceinline__ uint64_t chunk_ref(const Slot& S, const SM& s, uint64_t seed, int rs, int t, int k, int tot,
                                               int bs, int nB, int ds, int nD, int xs, int nX, int xe) {
   if (t >= tot) return 0ull;
   int u = t;
@@ -1947,7 +1957,8 @@ __device__ __forceinline__ uint64_t chunk_ref(const Slot& S, const Smem& s, uint
   return v < 0 ? s.ring[rs][v + kMaxBoosts] : (kRefIndex | gld(&S.x_ai[v]));   // (gld: no LDS/global pointer select)
 }
 // Chunk plan of k: emission ranges and the number of adds.
-__device__ __forceinline__ int chunk_plan(const Smem& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
+template <class SM>
+__device__ __forceinline__ int chunk_plan(const SM& s, int K, int eb, int k, int& bs, int& nB, int& ds, int& nD,
                                           int& xs, int& nX, int& xe) {
   bs = s.bst[k];
   const int be = k == K - 1 ? eb : s.bst[k + 1];
@@ -2060,8 +2071,8 @@ __device__ int better_boundary_w(VecSlot* vs, uint32_t ps0, uint32_t ps1, int li
 // entries and lands in the first chunk k with that count < E_k, i.e. with
 // o <= theta_k = be_off[E_k - 2].  Every chunk is therefore one contiguous
 // range of each stream.
-template <bool D, bool VEC = false>
-LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, bool cjk, int nb, int nd, int nx,
+template <bool D, bool VEC = false, class SM = Smem>
+LNG_SR_INL void score_round(const DevTables& T, Slot& S, SM& s, int ulscript, bool cjk, int nb, int nd, int nx,
                             int lowest, int dummy_off, int lane, int eb, int ed, int ex, VecState* V = nullptr) {
   lane = wave::lane_here();
   // The hit rounds (quad_round / octa_round / cjk_round) already turned their
@@ -2388,7 +2399,8 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, Smem& s, int ulscript, 
 }
 
 
-__device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int nd, int nx, bool octa, int lane) {
+template <class SM>
+__device__ void dbg_round(const Slot& S, SM& s, int off, int next, int nb, int nd, int nx, bool octa, int lane) {
   if (!s.dbg) return;
   const uint32_t h[6] = {'R', (uint32_t)off, (uint32_t)next, (uint32_t)nb, (uint32_t)nd, (uint32_t)nx};
   dbg_words(s, lane, h, 6);
@@ -2408,8 +2420,8 @@ __device__ void dbg_round(const Slot& S, Smem& s, int off, int next, int nb, int
 
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
-template <bool D, bool VEC = false>
-__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, Smem& s, Win& win, int tb,
+template <bool D, bool VEC = false, class SM = Smem>
+__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, SM& s, Win& win, int tb,
                                            int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags,
                                            VecState* V = nullptr) {
   int rt = rtype_of(T, ulscript);
@@ -2691,6 +2703,129 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
     }
   }
   return 0;
+}
+
+// ------------------------------------------------ staged long-document path
+// k_long runs every stage of a document in one kernel, so the kernel carries
+// the registers of its largest stage (128 VGPRs with spills: 4 waves/SIMD)
+// and the LDS of the union of the text window and the Repeats predictor, and
+// k_long's time follows its resident waves (round4d_waves.txt).  The staged
+// path splits pass 1 and pass 2 into kernels of their own (cld_kernels.hip):
+//   k_lspan   classify + GetOneScriptSpan/LowerScriptSpan + the Squeeze
+//             trigger test: pass 1's lowered spans into the document's region
+//             of a per-batch store (st_spans)
+//   k_lscore  ScoreOneScriptSpan over the stored spans, DocTote, the document
+//             level (st_score): pass 1, or pass 2 (Repeats|Finish)
+//   k_lrep    CheapRepWordsInplace over the stored spans, in place, predictor
+//             in LDS (st_rep): what pass 2 scores
+// each with its own register and LDS budget.  The stages are the very
+// functions detect() calls, in the same order, on the same span text (pass 2
+// from the span cache), so results are the same.  A document the staged path
+// does not take -- the Squeeze restart, a re-queued span, more than kStSpans
+// spans, no room in the store -- goes to the fused k_long whole, from scratch.
+constexpr int kStSpans = 32;
+struct StHdr {                                   // at the start of a document's region
+  uint32_t nsp, careful, rsv0, rsv1;
+  uint64_t span[kStSpans];                       // offset in the region | tb << 32 | ulscript << 56
+};
+constexpr int kStHdr = (int)sizeof(StHdr);       // (272: the span text after it stays 16-byte aligned)
+constexpr uint64_t kStNone = ~0ull;
+// A document's region: its header, then the worst case of its spans -- at
+// most 4 lowered bytes per raw byte (olen <= 4 per character), a ' ' per run
+// and per span 128 bytes of pads, NULs and hash read slack.
+__device__ __forceinline__ uint64_t st_region_bytes(uint64_t L) { return (4 * L + 4096 + 15) & ~15ull; }
+
+// Pass 1's spans of one document into its region (detect()'s pass-1 span
+// loop up to the scoring).  False: the fused kernel takes the document.
+__device__ bool st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* region, uint64_t cap, int lane) {
+  bool careful;
+  if (!classify(T, dv, S, careful, lane)) return false;
+  const int L = dv.len;
+  int next = 0, nsp = 0;
+  uint64_t cur = kStHdr;
+  StHdr* h = reinterpret_cast<StHdr*>(region);
+  for (;;) {
+    // room for the worst case of the span to come (st_region_bytes): never
+    // written past the region
+    if (cur + 4ull * (uint64_t)(L - next) + 128 > cap) return false;
+    int ul = 0, st = 0;
+    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane);
+    if (st == 0) break;
+    if (st < 0 || nsp == kStSpans) return false;
+    if (tb > 2048 && squeeze_trigger(S, region + cur, careful, lane)) return false;   // the Squeeze restart
+    if (lane == 0) h->span[nsp] = cur | ((uint64_t)(uint32_t)tb << 32) | ((uint64_t)(uint32_t)ul << 56);
+    ++nsp;
+    cur += (uint64_t)((tb + 64 + 15) & ~15);     // text, pads, hash read slack (as detect()'s cache)
+  }
+  if (lane == 0) {
+    h->nsp = (uint32_t)nsp;
+    h->careful = careful ? 1u : 0u;
+  }
+  gsync();
+  return true;
+}
+
+// One pass over a document's stored spans: detect()'s span loop (scoring
+// part) and the document level.  rep: pass 2 (Repeats|Finish), the spans
+// already through st_rep.  Returns 1 (result written), 0 (pass 1 not good
+// enough: pass 2 follows) or -kWhyCapacity.
+template <class SM>
+__device__ int st_score(const DevTables& T, Slot& S, SM& s, const uint8_t* region, bool rep, cld_result* out,
+                        uint32_t cflags, const uint32_t* __restrict__ pri, int lane) {
+  if (lane == 0) s.has_pri = pri != nullptr;
+  if (lane < 16) {
+    const uint32_t lp = pri ? gld(pri + lane) : 0u;
+    if (lane < 8) s.pri_add[lane >> 2][lane & 3] = lp ? tote_adds(T, lp) : 0ull;
+    else s.pri_wk[(lane - 8) >> 2][lane & 3] = (uint8_t)((lp >> 8) & 0xFF);
+  }
+  if (lane == 0) s.dt.init();
+  if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
+  wsync();
+  const StHdr* h = reinterpret_cast<const StHdr*>(region);
+  const int nsp = (int)uflu(gld(&h->nsp));
+  int total = 0;
+  for (int j = 0; j < nsp; ++j) {
+    const uint64_t e = ufl64(gld(&h->span[j]));
+    const uint8_t* lb = region + (uint32_t)e;
+    const int tb = (int)((e >> 32) & 0xFFFFFF), ul = (int)(e >> 56);
+    bool ok;
+    if (tb + 48 <= (int)sizeof(s.text)) {
+      const int n16 = (tb + 48 + 15) >> 4;
+      for (int i = lane; i < n16; i += 64)
+        reinterpret_cast<uint4*>(s.text)[i] = gld4(reinterpret_cast<const uint32_t*>(lb) + 4 * i);
+      wsync();
+      Win win{nullptr, 0, 16 * n16, 16 * n16};
+      ok = score_span<false, false>(T, S, s, win, tb, ul, lane, nullptr, 0, cflags, nullptr);
+    } else {
+      Win win{lb, 0, 0, (tb + 48 + 15) & ~15};
+      ok = score_span<false, false>(T, S, s, win, tb, ul, lane, nullptr, 0, cflags, nullptr);
+    }
+    if (!ok) return -kWhyCapacity;
+    total += tb;
+  }
+  return wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0);
+}
+
+// CheapRepWordsInplace over a document's stored spans, in order, one
+// predictor for the document (detect()'s from_cache pass 2).  False: a span
+// the in-place formulation cannot take (k_general redoes the document).
+__device__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, int lane) {
+  StHdr* h = reinterpret_cast<StHdr*>(region);
+  const int nsp = (int)uflu(gld(&h->nsp));
+  const bool careful = uflu(gld(&h->careful)) != 0;
+  for (int i = lane; i < kPredictionTableSize / 8; i += 64) reinterpret_cast<uint4*>(tbl)[i] = make_uint4(0, 0, 0, 0);
+  wsync();
+  uint32_t hcarry = 0;
+  for (int j = 0; j < nsp; ++j) {
+    const uint64_t e = ufl64(gld(&h->span[j]));
+    bool okr;
+    const int tb = rep_span_lds(tbl, S.pred, region + (uint32_t)e, (int)((e >> 32) & 0xFFFFFF), hcarry, careful, okr,
+                                lane);
+    if (!okr) return false;
+    if (lane == 0) h->span[j] = (e & ~(0xFFFFFFull << 32)) | ((uint64_t)(uint32_t)tb << 32);
+  }
+  gsync();
+  return true;
 }
 
 // The fused span builder emits separators and pads as ' ' without lowering

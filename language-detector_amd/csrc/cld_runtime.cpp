@@ -383,7 +383,16 @@ struct Device {
   uint8_t* d_slots = nullptr; // k_long per-wave slots (0 slots: CLD_LONG=0, long documents go to k_general)
   cld_result* d_spec_out = nullptr;   // k_long's speculative pass-2 results (small batches; CLD_LONG_SPEC=0: off)
   uint32_t* d_spec_take = nullptr;
-  int n_slots = 0;
+  int n_slots = 0;               // the fused k_long's resident waves (its grid)
+  // Staged long-document path (cld_launch_staged; CLD_LONG_STAGED=0: off):
+  // pass 1's spans of every long document in a store (CLD_LONG_STORE_MB, 8 GB
+  // default; a document finding it full takes the fused kernel), the list
+  // entries' regions (meta) and the stage lists
+  bool staged = false;
+  int st_waves = 0;             // slots the staged kernels use (>= n_slots slots are allocated)
+  uint8_t* d_store = nullptr; uint64_t store_bytes = 0;
+  uint64_t* d_meta = nullptr; size_t meta_cap = 0;
+  uint32_t* d_stlists = nullptr; size_t stlists_cap = 0;   // ok / pass-2 / fallback lists, 3 x cap
   uint32_t* d_requeue2 = nullptr;
   size_t requeue2_cap = 0;
   bool long_order = true;       // k_long takes its list longest first (CLD_LONG_ORDER=0: arrival order)
@@ -626,9 +635,24 @@ int init_device(Device* d) {
   int n_slots = (prop.multiProcessorCount * waves / kLongWPB) * kLongWPB;
   const uint64_t slot = cld_long_slot_bytes();
   while (n_slots > 0 && (uint64_t)n_slots * slot > (8ull << 30)) n_slots -= kLongWPB;
+  int alloc_slots = n_slots;
+  if (n_slots > 0 && !(getenv("CLD_LONG_STAGED") && atoi(getenv("CLD_LONG_STAGED")) == 0)) {
+    const int st = prop.multiProcessorCount * 4 * cld_staged_waves_per_simd();
+    uint64_t mb = 8192;
+    if (const char* e = getenv("CLD_LONG_STORE_MB")) mb = strtoull(e, nullptr, 10);
+    if (mb && (uint64_t)st * slot <= (12ull << 30) && hipMalloc(&d->d_store, mb << 20) == hipSuccess) {
+      d->store_bytes = mb << 20;
+      d->st_waves = st;
+      d->staged = true;
+      alloc_slots = std::max(n_slots, st);
+    } else {
+      (void)hipGetLastError();
+      d->d_store = nullptr;
+    }
+  }
   if (n_slots > 0) {
-    HIP_OK(hipMalloc(&d->d_slots, (uint64_t)n_slots * slot));
-    HIP_OK(hipMemset(d->d_slots, 0, (uint64_t)n_slots * slot));   // predictor epochs start at 0
+    HIP_OK(hipMalloc(&d->d_slots, (uint64_t)alloc_slots * slot));
+    HIP_OK(hipMemset(d->d_slots, 0, (uint64_t)alloc_slots * slot));   // predictor epochs start at 0
     d->n_slots = n_slots;
     const char* sp = getenv("CLD_LONG_SPEC");
     if (!sp || atoi(sp) != 0) {
@@ -728,10 +752,29 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       HIP_OK(cld_launch_order_long(offs, d->d_requeue, ctr, d->d_lkey, d->d_lhist, d->d_lsorted, n > 0, s));
       list = d->d_lsorted;
     }
+    // the staged path takes the list unless diagnostics (the fused kernel's
+    // trace / debug dump / stage cycles) are on; what it does not take goes to
+    // the fused kernel as the fallback list
+    const bool staged = d->staged && !d->h_trace && !d->d_dbg && !d->d_prof;
+    int ctr_total = kCtrRequeue, ctr_deq = kCtrDequeue;
+    if (staged) {
+      if (grow(&d->d_meta, &d->meta_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
+      if (grow(&d->d_stlists, &d->stlists_cap, 3 * std::max<size_t>(n, 1))) return CLD_ENOMEM;
+      const size_t c = d->stlists_cap / 3;
+      uint32_t* fall = d->d_stlists + 2 * c;
+      // a list of at most 4 documents per fused wave goes whole to the fused
+      // kernel: small batches keep its two-wave speculation (section 6)
+      HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
+                               d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
+                               priors, hbuf, hflag, d->fault_doc, 4u * (uint32_t)d->n_slots, s));
+      list = fall;
+      ctr_total = kCtrStFall;
+      ctr_deq = kCtrStDqFall;
+    }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            ctr, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, d->fault_doc,
-                           d->d_spec_out, d->d_spec_take, s));
+                           d->d_spec_out, d->d_spec_take, ctr_total, ctr_deq, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
                               ctr, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
@@ -1734,6 +1777,7 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag); (void)hipFree(d->d_hpos);
     (void)hipFree(d->d_spec_out); (void)hipFree(d->d_spec_take);
+    (void)hipFree(d->d_store); (void)hipFree(d->d_meta); (void)hipFree(d->d_stlists);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);

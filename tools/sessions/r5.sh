@@ -30,6 +30,11 @@ for s in ${STEPS:-suite smoke bench}; do
       step 400 pmc_c2.log bash tools/pmc_session.sh ${TAG}_pmc_c2 c2 k_wave
       step 400 pmc_c3.log bash tools/pmc_session.sh ${TAG}_pmc_c3 c3 k_long ;;
     dl) step 400 dl_rate.jsonl python3 tools/dl_rate.py ;;
+    ab)  # staged vs fused long-document path (A/B), C3 and C5 lines
+      for c in ${ABCFG:-c3 c5}; do
+        step 400 ab_${c}_staged.json python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
+        step 400 ab_${c}_fused.json env CLD_LONG_STAGED=0 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
+      done ;;
     dlab) step 600 dl_ab.jsonl env DL_RATE_VARIANTS="${DLVARS:--;CLD_TINY_ZC=1;CLD_TINY=0}" DL_RATE_CFG=c2 python3 tools/dl_rate.py ;;
     req) step 400 req_rate.jsonl env REQ_RATE_CALLERS=1,8,32,128 python3 tools/req_rate.py ;;
     rates)
