@@ -26,7 +26,7 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
        // staged long-document path (k_lspan / k_lscore / k_lrep): list counts and dequeue cursors
        kCtrStFall = 19 /* to the fused k_long */, kCtrStDqSpan = 20, kCtrStOk = 21 /* spans stored */,
        kCtrStDqS1 = 22, kCtrStP2 = 23 /* pass 2 */, kCtrStDqRep = 24, kCtrStDqS2 = 25, kCtrStDqFall = 26,
-       kCtrStPool = 27 /* store 256-byte units taken */, kCtrSlots = 32 };
+       kCtrStPool = 27 /* store 16-byte units taken */, kCtrSlots = 32 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lspan(
     return;
   }
   const bool exact = lng::space_lowers_to_space(T);
-  const uint64_t units = pool_bytes >> 8;
+  const uint64_t units = pool_bytes >> 4;
   for (;;) {
     const uint32_t k = wave::uflu(atomicAdd(&counters[kCtrStDqSpan], lane == 0 ? 1u : 0u));
     if (k >= total) break;                       // every wave reaches this exit
@@ -475,23 +475,13 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lspan(
     const uint64_t a = offs[i], L = offs[i + 1] - a;
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const bool rw = (spi & kSpecialRewritten) != 0;
-    bool ok = exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc;
-    uint64_t at = 0;
-    const uint64_t need = lng::st_region_bytes(L);
-    if (ok) {
-      const uint32_t u = (uint32_t)((need + 255) >> 8);
-      uint32_t got = 0;
-      if (lane == 0) got = atomicAdd(&counters[kCtrStPool], u);
-      got = wave::uflu(__shfl((int)got, 0, 64));
-      ok = (uint64_t)got + u <= units;
-      at = (uint64_t)got << 8;
-    }
-    if (ok) {
+    uint64_t at = lng::kStNone;
+    if (exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc) {
       const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
-      ok = lng::st_spans(T, dv, S, pool + at, need, lane);
+      at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane);
     }
     if (lane == 0) {
-      if (ok) {
+      if (at != lng::kStNone) {
         meta[k] = at;
         ok_list[atomicAdd(&counters[kCtrStOk], 1u)] = k;
       } else {

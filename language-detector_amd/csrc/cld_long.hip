@@ -2721,48 +2721,64 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
 // each with its own register and LDS budget.  The stages are the very
 // functions detect() calls, in the same order, on the same span text (pass 2
 // from the span cache), so results are the same.  A document the staged path
-// does not take -- the Squeeze restart, a re-queued span, more than kStSpans
-// spans, no room in the store -- goes to the fused k_long whole, from scratch.
-constexpr int kStSpans = 32;
-struct StHdr {                                   // at the start of a document's region
-  uint32_t nsp, careful, rsv0, rsv1;
-  uint64_t span[kStSpans];                       // offset in the region | tb << 32 | ulscript << 56
+// does not take -- the Squeeze restart, a re-queued span, spans that outgrow
+// the slot's span cache, no room left in the store -- goes to the fused k_long
+// whole, from scratch.
+//
+// A document's region: StHdr, the spans back to back (each followed by its
+// pads and NULs, 16-byte aligned), then the span table (one u64 per span:
+// offset in the region | text_bytes << 32 | ulscript << 56).
+struct StHdr {
+  uint32_t nsp, careful, tab, rsv;
 };
-constexpr int kStHdr = (int)sizeof(StHdr);       // (272: the span text after it stays 16-byte aligned)
 constexpr uint64_t kStNone = ~0ull;
-// A document's region: its header, then the worst case of its spans -- at
-// most 4 lowered bytes per raw byte (olen <= 4 per character), a ' ' per run
-// and per span 128 bytes of pads, NULs and hash read slack.
-__device__ __forceinline__ uint64_t st_region_bytes(uint64_t L) { return (4 * L + 4096 + 15) & ~15ull; }
+__device__ __forceinline__ int st_advance(int tb) { return (tb + 48 + 15) & ~15; }   // text + "   \0" + NULs
 
-// Pass 1's spans of one document into its region (detect()'s pass-1 span
-// loop up to the scoring).  False: the fused kernel takes the document.
-__device__ bool st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* region, uint64_t cap, int lane) {
+// Pass 1's spans of one document (detect()'s pass-1 span loop up to the
+// scoring) into the slot's span cache, then, at their exact size, into a
+// region of the store taken from *pool_units (16-byte units).  Returns the
+// region's byte offset, or kStNone: the fused kernel takes the document.
+__device__ uint64_t st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* pool, uint64_t pool_units,
+                             uint32_t* pool_ctr, int lane) {
   bool careful;
-  if (!classify(T, dv, S, careful, lane)) return false;
-  const int L = dv.len;
-  int next = 0, nsp = 0;
-  uint64_t cur = kStHdr;
-  StHdr* h = reinterpret_cast<StHdr*>(region);
+  if (!classify(T, dv, S, careful, lane)) return kStNone;
+  int next = 0, nsp = 0, cur = 0;
   for (;;) {
-    // room for the worst case of the span to come (st_region_bytes): never
-    // written past the region
-    if (cur + 4ull * (uint64_t)(L - next) + 128 > cap) return false;
+    if (cur + kLB > kLbdCap || nsp >= kMaxSpans) return kStNone;
     int ul = 0, st = 0;
-    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane);
+    const int tb = next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane);
     if (st == 0) break;
-    if (st < 0 || nsp == kStSpans) return false;
-    if (tb > 2048 && squeeze_trigger(S, region + cur, careful, lane)) return false;   // the Squeeze restart
-    if (lane == 0) h->span[nsp] = cur | ((uint64_t)(uint32_t)tb << 32) | ((uint64_t)(uint32_t)ul << 56);
+    if (st < 0) return kStNone;
+    if (tb > 2048 && squeeze_trigger(S, S.lbd + cur, careful, lane)) return kStNone;   // the Squeeze restart
+    if (lane == 0) {
+      S.sp_off[nsp] = cur;
+      S.sp_tb[nsp] = tb;
+      S.sp_ul[nsp] = ul;
+    }
     ++nsp;
-    cur += (uint64_t)((tb + 64 + 15) & ~15);     // text, pads, hash read slack (as detect()'s cache)
-  }
-  if (lane == 0) {
-    h->nsp = (uint32_t)nsp;
-    h->careful = careful ? 1u : 0u;
+    cur += st_advance(tb);
   }
   gsync();
-  return true;
+  const uint32_t units = (uint32_t)((sizeof(StHdr) + cur + 8 * nsp + 15) >> 4);
+  uint32_t got = 0;
+  if (lane == 0) got = atomicAdd(pool_ctr, units);
+  got = uflu(__shfl((int)got, 0, 64));
+  if ((uint64_t)got + units > pool_units) return kStNone;
+  uint8_t* region = pool + ((uint64_t)got << 4);
+  const int n16 = cur >> 4;
+  uint4* dst = reinterpret_cast<uint4*>(region + sizeof(StHdr));
+  const uint4* src = reinterpret_cast<const uint4*>(S.lbd);
+  for (int i = lane; i < n16; i += 64) dst[i] = src[i];
+  uint64_t* tab = reinterpret_cast<uint64_t*>(region + sizeof(StHdr) + cur);
+  for (int j = lane; j < nsp; j += 64)
+    tab[j] = (uint64_t)(uint32_t)(S.sp_off[j] + (int)sizeof(StHdr)) | ((uint64_t)(uint32_t)S.sp_tb[j] << 32) |
+             ((uint64_t)(uint32_t)S.sp_ul[j] << 56);
+  if (lane == 0) {
+    StHdr h{(uint32_t)nsp, careful ? 1u : 0u, (uint32_t)(sizeof(StHdr) + cur), 0u};
+    *reinterpret_cast<StHdr*>(region) = h;
+  }
+  gsync();
+  return (uint64_t)got << 4;
 }
 
 // One pass over a document's stored spans: detect()'s span loop (scoring
@@ -2783,9 +2799,10 @@ __device__ int st_score(const DevTables& T, Slot& S, SM& s, const uint8_t* regio
   wsync();
   const StHdr* h = reinterpret_cast<const StHdr*>(region);
   const int nsp = (int)uflu(gld(&h->nsp));
+  const uint64_t* tab = reinterpret_cast<const uint64_t*>(region + uflu(gld(&h->tab)));
   int total = 0;
   for (int j = 0; j < nsp; ++j) {
-    const uint64_t e = ufl64(gld(&h->span[j]));
+    const uint64_t e = ufl64(gld(tab + j));
     const uint8_t* lb = region + (uint32_t)e;
     const int tb = (int)((e >> 32) & 0xFFFFFF), ul = (int)(e >> 56);
     bool ok;
@@ -2813,16 +2830,17 @@ __device__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, int lane) {
   StHdr* h = reinterpret_cast<StHdr*>(region);
   const int nsp = (int)uflu(gld(&h->nsp));
   const bool careful = uflu(gld(&h->careful)) != 0;
+  uint64_t* tab = reinterpret_cast<uint64_t*>(region + uflu(gld(&h->tab)));
   for (int i = lane; i < kPredictionTableSize / 8; i += 64) reinterpret_cast<uint4*>(tbl)[i] = make_uint4(0, 0, 0, 0);
   wsync();
   uint32_t hcarry = 0;
   for (int j = 0; j < nsp; ++j) {
-    const uint64_t e = ufl64(gld(&h->span[j]));
+    const uint64_t e = ufl64(gld(tab + j));
     bool okr;
     const int tb = rep_span_lds(tbl, S.pred, region + (uint32_t)e, (int)((e >> 32) & 0xFFFFFF), hcarry, careful, okr,
                                 lane);
     if (!okr) return false;
-    if (lane == 0) h->span[j] = (e & ~(0xFFFFFFull << 32)) | ((uint64_t)(uint32_t)tb << 32);
+    if (lane == 0) tab[j] = (e & ~(0xFFFFFFull << 32)) | ((uint64_t)(uint32_t)tb << 32);
   }
   gsync();
   return true;

@@ -640,7 +640,8 @@ int init_device(Device* d) {
     const int st = prop.multiProcessorCount * 4 * cld_staged_waves_per_simd();
     uint64_t mb = 8192;
     if (const char* e = getenv("CLD_LONG_STORE_MB")) mb = strtoull(e, nullptr, 10);
-    if (mb && (uint64_t)st * slot <= (12ull << 30) && hipMalloc(&d->d_store, mb << 20) == hipSuccess) {
+    // (64 KB past the last region: the span readers' slack reads stay inside the allocation)
+    if (mb && (uint64_t)st * slot <= (12ull << 30) && hipMalloc(&d->d_store, (mb << 20) + (64u << 10)) == hipSuccess) {
       d->store_bytes = mb << 20;
       d->st_waves = st;
       d->staged = true;
