@@ -2725,6 +2725,10 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
 // the slot's span cache, no room left in the store -- goes to the fused k_long
 // whole, from scratch.
 //
+// The stage functions are inlined into their kernels: an out-of-line call
+// passes the LDS state as a generic pointer, and its FLAT accesses count
+// against LGKM like the gathers.
+//
 // A document's region: StHdr, the spans back to back (each followed by its
 // pads and NULs, 16-byte aligned), then the span table (one u64 per span:
 // offset in the region | text_bytes << 32 | ulscript << 56).
@@ -2738,7 +2742,7 @@ __device__ __forceinline__ int st_advance(int tb) { return (tb + 48 + 15) & ~15;
 // scoring) into the slot's span cache, then, at their exact size, into a
 // region of the store taken from *pool_units (16-byte units).  Returns the
 // region's byte offset, or kStNone: the fused kernel takes the document.
-__device__ uint64_t st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* pool, uint64_t pool_units,
+__device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* pool, uint64_t pool_units,
                              uint32_t* pool_ctr, int lane) {
   bool careful;
   if (!classify(T, dv, S, careful, lane)) return kStNone;
@@ -2786,7 +2790,7 @@ __device__ uint64_t st_spans(const DevTables& T, const DocView& dv, Slot& S, uin
 // already through st_rep.  Returns 1 (result written), 0 (pass 1 not good
 // enough: pass 2 follows) or -kWhyCapacity.
 template <class SM>
-__device__ int st_score(const DevTables& T, Slot& S, SM& s, const uint8_t* region, bool rep, cld_result* out,
+__device__ __forceinline__ int st_score(const DevTables& T, Slot& S, SM& s, const uint8_t* region, bool rep, cld_result* out,
                         uint32_t cflags, const uint32_t* __restrict__ pri, int lane) {
   if (lane == 0) s.has_pri = pri != nullptr;
   if (lane < 16) {
@@ -2826,7 +2830,7 @@ __device__ int st_score(const DevTables& T, Slot& S, SM& s, const uint8_t* regio
 // CheapRepWordsInplace over a document's stored spans, in order, one
 // predictor for the document (detect()'s from_cache pass 2).  False: a span
 // the in-place formulation cannot take (k_general redoes the document).
-__device__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, int lane) {
+__device__ __forceinline__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, int lane) {
   StHdr* h = reinterpret_cast<StHdr*>(region);
   const int nsp = (int)uflu(gld(&h->nsp));
   const bool careful = uflu(gld(&h->careful)) != 0;
