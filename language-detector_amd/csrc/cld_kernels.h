@@ -139,7 +139,9 @@ size_t cld_long_spec_docs(int n_slots);
 // k_long: cld_launch_long with kCtrStFall / kCtrStDqFall); k_lscore scores
 // pass 1 (to p2_list when not good enough), k_lrep runs Repeats over those,
 // k_lscore<pass 2> finishes them.  small_total: a list this short goes whole
-// to the fused kernel, in order (its speculation is for small batches).
+// to the fused kernel, in order (its speculation is for small batches), and
+// so does a list holding a document of 20 KB or more (hist: k_len_hist's
+// length buckets; nullable).
 // n_waves: resident waves the staged kernels may use (slots).
 int cld_staged_waves_per_simd();
 hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
@@ -147,6 +149,6 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, hipStream_t s);
+                             uint32_t small_total, const uint32_t* hist, hipStream_t s);
 }
 #endif

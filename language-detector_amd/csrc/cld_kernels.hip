@@ -444,6 +444,7 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
 #define LNG_ST_TEXT 5120
 #endif
 constexpr int kStWPB = 4;
+constexpr int kStHeavyKB = 20;
 using StSmem = lng::SmemT<LNG_ST_TEXT, false>;
 static_assert(kStWPB * sizeof(StSmem) * (4 * LNG_ST_WPS / kStWPB) <= 160 * 1024, "k_lscore LDS per CU");
 
@@ -452,14 +453,23 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lspan(
     const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
     uint64_t* __restrict__ meta, uint32_t* __restrict__ ok_list, uint32_t* __restrict__ fall_list,
     uint32_t* __restrict__ counters, const uint8_t* __restrict__ special, const uint8_t* __restrict__ hbuf,
-    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total) {
+    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist) {
   const DevTables& T = *Tp;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (total == 0) return;
-  if (total <= small_total) {                    // a small batch: the fused kernel takes it all, in list order
+  // Documents of kStHeavyKB and more (k_len_hist's length buckets, longest
+  // first) take one wave tens of milliseconds (a 64 KB page ~40 ms): every
+  // stage kernel would wait for them in turn, where the fused kernel waits
+  // once while its other waves run the rest (C5: fused 51.6 ms, staged 91 ms;
+  // C3's 16 KB pages: staged 77 ms, fused 86 ms).  A batch holding one goes
+  // to the fused kernel whole.
+  uint32_t heavy = 0;
+  if (hist && lane < kLenBuckets - kStHeavyKB) heavy = hist[lane];   // buckets of (L >> 10) >= kStHeavyKB
+  heavy = wave::wsum(heavy);
+  if (total <= small_total || heavy) {           // the fused kernel takes it all, in list order
     if (blockIdx.x == 0) {
       for (uint32_t k = threadIdx.x; k < total; k += blockDim.x) fall_list[k] = list[k];
       if (threadIdx.x == 0) counters[kCtrStFall] = total;
@@ -728,14 +738,14 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, hipStream_t s) {
+                             uint32_t small_total, const uint32_t* hist, hipStream_t s) {
   // n_waves: the slots (resident waves) of the widest launch below
   const int per_simd = cld_staged_waves_per_simd();
   const int cus = n_waves / (4 * per_simd);
   if (cus < 1) return hipErrorInvalidValue;
   const dim3 gst(cus * 4 * LNG_ST_WPS / cld::kStWPB), bst(64 * cld::kStWPB);
   hipLaunchKernelGGL(cld::k_lspan, gst, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
-                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total);
+                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total, hist);
   hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
                      requeue2, counters, cflags, special, priors);
   hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,

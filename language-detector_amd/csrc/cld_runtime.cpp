@@ -767,7 +767,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       // kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
-                               priors, hbuf, hflag, d->fault_doc, 4u * (uint32_t)d->n_slots, s));
+                               priors, hbuf, hflag, d->fault_doc, 4u * (uint32_t)d->n_slots,
+                               d->long_order ? d->d_lhist : nullptr, s));
       list = fall;
       ctr_total = kCtrStFall;
       ctr_deq = kCtrStDqFall;
