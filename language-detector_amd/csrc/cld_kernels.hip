@@ -430,25 +430,33 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
 
 // ------------------------------------------------ staged long-document path
 // (cld_long.hip, st_spans / st_score / st_rep).  Persistent grids, one wave
-// per document at a time, each with its own occupancy: LNG_ST_WPS waves per
-// SIMD for k_lspan / k_lscore (their registers fit 96 VGPRs; k_lscore's LDS is
-// the LNG_ST_TEXT text window without the Repeats predictor), LNG_REP_WPS for
-// k_lrep (one wave per workgroup, 8 KB of LDS predictor each).
+// per document at a time, each with its own occupancy: LNG_SPAN_WPS waves per
+// SIMD for k_lspan (96 VGPRs, no LDS), LNG_ST_WPS for k_lscore (its LDS is the
+// LNG_ST_TEXT text window without the Repeats predictor; a longer span is
+// scored through windows of it), LNG_REP_WPS for k_lrep (one wave per
+// workgroup, 8 KB of LDS predictor each).  C3, 100K 16 KB pages: fused k_long
+// 86.1 ms; staged at 5/5/5 waves and a 5 KB window 77.0 ms, at 5/6/5 and 3 KB
+// 73.6 ms (gpurun_out/r5j), at 6/7/5 and 2 KB ~72 ms (r5k).  A block of a span
+// wider than the window (win_text) sends the document to the fused kernel,
+// whose window is 6 KB (a 1 KB window sent 81% of C3 to k_general).
 #ifndef LNG_ST_WPS
-#define LNG_ST_WPS 5
+#define LNG_ST_WPS 7
+#endif
+#ifndef LNG_SPAN_WPS
+#define LNG_SPAN_WPS 6
 #endif
 #ifndef LNG_REP_WPS
 #define LNG_REP_WPS 5
 #endif
 #ifndef LNG_ST_TEXT
-#define LNG_ST_TEXT 5120
+#define LNG_ST_TEXT 2048
 #endif
 constexpr int kStWPB = 4;
 constexpr int kStHeavyKB = 20;
 using StSmem = lng::SmemT<LNG_ST_TEXT, false>;
 static_assert(kStWPB * sizeof(StSmem) * (4 * LNG_ST_WPS / kStWPB) <= 160 * 1024, "k_lscore LDS per CU");
 
-__global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lspan(
+__global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
     uint64_t* __restrict__ meta, uint32_t* __restrict__ ok_list, uint32_t* __restrict__ fall_list,
@@ -505,7 +513,7 @@ template <bool P2>
 __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
     const DevTables* __restrict__ Tp, const uint32_t* __restrict__ list, cld_result* __restrict__ out,
     uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, const uint64_t* __restrict__ meta,
-    const uint32_t* __restrict__ in_list, uint32_t* __restrict__ p2_list, uint32_t* __restrict__ requeue2,
+    const uint32_t* __restrict__ in_list, uint32_t* __restrict__ p2_list, uint32_t* __restrict__ fall_list,
     uint32_t* __restrict__ counters, uint32_t cflags, const uint8_t* __restrict__ special,
     const uint32_t* __restrict__ priors) {
   __shared__ StSmem smem[kStWPB];
@@ -535,9 +543,8 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
         atomicAdd(&counters[P2 ? kCtrPass2 : kCtrPass1], 1u);
       } else if (r == 0 && !P2) {
         p2_list[atomicAdd(&counters[kCtrStP2], 1u)] = k;
-      } else {                                   // capacity (or a pass 2 that did not finish): k_general
-        requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = i;
-        atomicAdd(&counters[kCtrWhy + lng::kWhyCapacity], 1u);
+      } else {                                   // capacity (the LDS window): the fused kernel redoes it
+        fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
       }
     }
   }
@@ -731,7 +738,10 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
 }
 size_t cld_long_spec_docs(int n_slots) { return (size_t)n_slots / cld::kSpecShare; }
 
-int cld_staged_waves_per_simd() { return LNG_ST_WPS > LNG_REP_WPS ? LNG_ST_WPS : LNG_REP_WPS; }
+int cld_staged_waves_per_simd() {
+  const int a = LNG_ST_WPS > LNG_REP_WPS ? LNG_ST_WPS : LNG_REP_WPS;
+  return a > LNG_SPAN_WPS ? a : LNG_SPAN_WPS;
+}
 
 hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
@@ -743,15 +753,15 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
   const int per_simd = cld_staged_waves_per_simd();
   const int cus = n_waves / (4 * per_simd);
   if (cus < 1) return hipErrorInvalidValue;
-  const dim3 gst(cus * 4 * LNG_ST_WPS / cld::kStWPB), bst(64 * cld::kStWPB);
-  hipLaunchKernelGGL(cld::k_lspan, gst, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
+  const dim3 gst(cus * 4 * LNG_ST_WPS / cld::kStWPB), gsp(cus * 4 * LNG_SPAN_WPS / cld::kStWPB), bst(64 * cld::kStWPB);
+  hipLaunchKernelGGL(cld::k_lspan, gsp, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
                      fall_list, counters, special, hbuf, hflag, fault_doc, small_total, hist);
   hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
-                     requeue2, counters, cflags, special, priors);
+                     fall_list, counters, cflags, special, priors);
   hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,
                      requeue2, counters);
   hipLaunchKernelGGL(cld::k_lscore<true>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, p2_list, p2_list,
-                     requeue2, counters, cflags, special, priors);
+                     fall_list, counters, cflags, special, priors);
   return hipGetLastError();
 }
 
