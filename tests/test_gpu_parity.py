@@ -208,3 +208,49 @@ def test_mixed_language_short_documents(gpu, oracle):
     # the mixture must reach the document-level passes the wave kernel gates
     assert (got["percent3"][:, 1] > 0).sum() > 5000
     assert (~got["is_reliable"].astype(bool)).sum() > 1000
+
+
+STAGED = r'''
+import numpy as np, cld_amd, corpus
+from oracle import Oracle
+from test_gpu_parity import assert_same
+cld_amd.init()
+o = Oracle()
+b3, o3 = corpus.c3(20000, seed=171)
+want = o.detect_batch(b3, o3, threads=16)
+got = cld_amd.detect_batch(buf=b3, offsets=o3)
+assert_same(got, want, "c3 staged")
+st = cld_amd.last_stats(0)
+assert st.general_docs == 0 and st.long_docs == 20000, (st.general_docs, st.long_docs)
+print("staged ok", st.passes[0], st.passes[1])
+'''
+
+
+def test_staged_long_path_and_its_hand_ons(gpu, oracle):
+    """The staged long-document path (cld_long.hip st_spans / st_score /
+    st_rep in k_lspan / k_lscore / k_lrep) and the documents it hands to the
+    fused k_long: a span block wider than its 2 KB LDS window (a 3 KB word),
+    hundreds of spans, the Squeeze restart, pass 2 with Repeats -- in one
+    batch large enough to take the staged path (more than 4 documents per
+    fused wave), all equal to the oracle and none on the sequential kernel.
+    Then the store exhausted (CLD_LONG_STORE_MB=1, child process): every
+    document the store cannot hold goes to the fused kernel, same results."""
+    import subprocess
+    import sys
+    b3, o3 = corpus.c3(17000, seed=172, page=2048)
+    docs = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(17000)]
+    b2, o2 = corpus.c2(3000, seed=173)
+    docs[5] = b"x" * 3000 + b" " + bytes(b2[o2[0]:o2[40]])                  # one 3 KB word
+    docs[9] = " ".join(["ab", "где", "xy", "कि"] * 300).encode()             # ~1200 spans
+    docs[11] = ("abc дом " * 500).encode()                                      # many two-script spans
+    docs[13] = corpus.BOILERPLATE * 20 + bytes(b2[o2[0]:o2[30]])             # the Squeeze restart
+    buf, offs = gpu.pack(docs)
+    got = check(gpu, oracle, buf, offs, "staged")
+    st = gpu.last_stats(0)
+    assert st.general_docs == 0, list(st.long_requeue)
+    assert st.passes[1] > 1000                                                # pass 2 (Repeats) taken
+    env = dict(os.environ, CLD_LONG_STORE_MB="1",
+               PYTHONPATH=os.pathsep.join(os.path.join(ROOT, p) for p in ("language-detector_amd", "oracle", "tests")))
+    r = subprocess.run([sys.executable, "-c", STAGED], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "staged ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    assert len(got) == len(docs)
