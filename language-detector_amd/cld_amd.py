@@ -182,7 +182,7 @@ def init_device(device, tables=None):
 
 
 def plan_shards(offsets, nshards):
-    """Byte-balanced contiguous document shards (host-only, no GPU)."""
+    """Contiguous document shards of equal estimated kernel cost (cld_plan_shards; host-only, no GPU)."""
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     cuts = np.zeros(nshards + 1, dtype=np.uint64)
     rc = lib().cld_plan_shards(offsets.ctypes.data, len(offsets) - 1, nshards, cuts.ctypes.data)
