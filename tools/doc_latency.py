@@ -18,6 +18,12 @@ import corpus  # noqa: E402
 from oracle import Oracle  # noqa: E402
 from test_html_hints import oracle_spans  # noqa: E402
 
+# LAT_PROFILE=1: the fused kernel's per-stage cycles per document too
+# (CLD_PROFILE_STAGES: k_long's diagnostic instantiation)
+PROF = os.environ.get("LAT_PROFILE") == "1"
+if PROF:
+    os.environ["CLD_PROFILE_STAGES"] = "1"
+LSTAGES = ["classify", "span+lower", "squeeze", "repeats", "words+chain", "quad", "octa/uni/bi", "score"]
 cld_amd.init()
 o = Oracle()
 docs = []
@@ -34,13 +40,19 @@ for name, d in docs:
     for _ in range(2):
         cld_amd.detect_batch(buf=buf, offsets=offs)
     cld_amd.kernel_times(0)
+    if PROF:
+        cld_amd.stage_cycles(0)
     reps = 3
     for _ in range(reps):
         r = cld_amd.detect_batch(buf=buf, offsets=offs)
     ms, launches = cld_amd.kernel_times(0)
     st = cld_amd.last_stats(0)
     spans = oracle_spans(o, d, True)
-    print(json.dumps({"doc": name, "bytes": len(d), "spans": len(spans),
+    extra = {}
+    if PROF:
+        c = cld_amd.stage_cycles(0).astype(np.float64)[8:16] / reps
+        extra = {"stage_kcycles": {LSTAGES[k]: round(c[k] / 1e3, 1) for k in range(8)}}
+    print(json.dumps({"doc": name, "bytes": len(d), "spans": len(spans), **extra,
                       "span_bytes_max": max((len(t) for _, t in spans), default=0),
                       "passes": [int(x) for x in st.passes[:3]], "long_ms": round(ms[1] / max(1, launches), 3),
                       "general_ms": round(ms[2] / max(1, launches), 3)}), flush=True)
