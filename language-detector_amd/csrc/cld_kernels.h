@@ -16,7 +16,7 @@ constexpr int kWaveWPB = WAVE_WPB;   // waves (documents) per workgroup
 constexpr int kMaxLgProbScore = 16;
 
 
-// Device counter slots (two 64-byte lines, zeroed per batch)
+// Device counter slots (three 64-byte lines, zeroed per batch)
 // kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general;
 // kCtrSpecial: HTML / hinted documents the wave kernel sent straight to k_general.
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
@@ -26,7 +26,10 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
        // staged long-document path (k_lspan / k_lscore / k_lrep): list counts and dequeue cursors
        kCtrStFall = 19 /* to the fused k_long */, kCtrStDqSpan = 20, kCtrStOk = 21 /* spans stored */,
        kCtrStDqS1 = 22, kCtrStP2 = 23 /* pass 2 */, kCtrStDqRep = 24, kCtrStDqS2 = 25, kCtrStDqFall = 26,
-       kCtrStPool = 27 /* store 16-byte units taken */, kCtrSlots = 32 };
+       kCtrStPool = 27 /* store 16-byte units taken */,
+       // span-parallel documents: group lists and document lists of passes 1 and 2
+       kCtrStG1 = 28, kCtrStDqG1 = 29, kCtrStPar1 = 30, kCtrStDqF1 = 31,
+       kCtrStG2 = 32, kCtrStDqG2 = 33, kCtrStPar2 = 34, kCtrStDqF2 = 35, kCtrSlots = 48 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.
@@ -140,15 +143,18 @@ size_t cld_long_spec_docs(int n_slots);
 // pass 1 (to p2_list when not good enough), k_lrep runs Repeats over those,
 // k_lscore<pass 2> finishes them.  small_total: a list this short goes whole
 // to the fused kernel, in order (its speculation is for small batches), and
-// so does a list holding a document of 20 KB or more (hist: k_len_hist's
-// length buckets; nullable).
+// so does a list holding a document of heavy_kb KB or more (hist: k_len_hist's
+// length buckets; nullable; heavy_kb 0: no such rule).
 // n_waves: resident waves the staged kernels may use (slots).
 int cld_staged_waves_per_simd();
+// par_lists (span-parallel documents): two u32 document lists of n entries
+// each (passes 1, 2), then two u64 group lists of gcap entries each.
 hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, const uint32_t* hist, hipStream_t s);
+                             uint32_t small_total, const uint32_t* hist, uint32_t heavy_kb, uint32_t* par_lists,
+                             size_t n, size_t gcap, hipStream_t s);
 }
 #endif

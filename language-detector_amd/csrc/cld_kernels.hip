@@ -452,7 +452,6 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
 #define LNG_ST_TEXT 2048
 #endif
 constexpr int kStWPB = 4;
-constexpr int kStHeavyKB = 20;
 using StSmem = lng::SmemT<LNG_ST_TEXT, false>;
 static_assert(kStWPB * sizeof(StSmem) * (4 * LNG_ST_WPS / kStWPB) <= 160 * 1024, "k_lscore LDS per CU");
 
@@ -461,21 +460,22 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
     uint64_t* __restrict__ meta, uint32_t* __restrict__ ok_list, uint32_t* __restrict__ fall_list,
     uint32_t* __restrict__ counters, const uint8_t* __restrict__ special, const uint8_t* __restrict__ hbuf,
-    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist) {
+    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist,
+    uint32_t* __restrict__ par_list, uint64_t* __restrict__ group_list, uint32_t gcap, uint32_t heavy_kb) {
   const DevTables& T = *Tp;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrRequeue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (total == 0) return;
-  // Documents of kStHeavyKB and more (k_len_hist's length buckets, longest
+  // Documents of heavy_kb and more (k_len_hist's length buckets, longest
   // first) take one wave tens of milliseconds (a 64 KB page ~40 ms): every
   // stage kernel would wait for them in turn, where the fused kernel waits
   // once while its other waves run the rest (C5: fused 51.6 ms, staged 91 ms;
   // C3's 16 KB pages: staged 77 ms, fused 86 ms).  A batch holding one goes
   // to the fused kernel whole.
   uint32_t heavy = 0;
-  if (hist && lane < kLenBuckets - kStHeavyKB) heavy = hist[lane];   // buckets of (L >> 10) >= kStHeavyKB
+  if (hist && heavy_kb && lane < kLenBuckets - (int)heavy_kb) heavy = hist[lane];   // buckets of (L >> 10) >= heavy_kb
   heavy = wave::wsum(heavy);
   if (total <= small_total || heavy) {           // the fused kernel takes it all, in list order
     if (blockIdx.x == 0) {
@@ -498,12 +498,27 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
       const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
       at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane);
     }
+    // a span-parallel document (more than kParMin spans): its groups to the group list
+    uint32_t ng = 0, gb = 0;
+    if (at != lng::kStNone) {
+      const lng::StHdr* h = reinterpret_cast<const lng::StHdr*>(pool + at);
+      if (wave::uflu(gld(&h->par))) {
+        ng = (wave::uflu(gld(&h->nsp)) + lng::kParG - 1) / lng::kParG;
+        if (lane == 0) gb = atomicAdd(&counters[kCtrStG1], ng);
+        gb = wave::uflu(__shfl((int)gb, 0, 64));
+        const bool fits = (uint64_t)gb + ng <= gcap;
+        for (uint32_t g = lane; g < ng && gb + g < gcap; g += 64)
+          group_list[gb + g] = fits ? ((uint64_t)k | ((uint64_t)g << 32)) : ~0ull;   // (~0: a skipped entry)
+        if (!fits) at = lng::kStNone;
+      }
+    }
     if (lane == 0) {
-      if (at != lng::kStNone) {
-        meta[k] = at;
-        ok_list[atomicAdd(&counters[kCtrStOk], 1u)] = k;
-      } else {
+      if (at == lng::kStNone) {
         fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
+      } else {
+        meta[k] = at;
+        if (ng) par_list[atomicAdd(&counters[kCtrStPar1], 1u)] = k;
+        else ok_list[atomicAdd(&counters[kCtrStOk], 1u)] = k;
       }
     }
   }
@@ -532,6 +547,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
     const uint32_t e = wave::uflu(atomicAdd(&counters[P2 ? kCtrStDqS2 : kCtrStDqS1], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
     const uint32_t k = in_list[e];
+    if (P2 && (k & 0x80000000u)) continue;       // a span-parallel document: k_lgroup / k_lfinish
     const uint64_t at = meta[k];
     if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
     const uint32_t i = list[k];
@@ -550,6 +566,93 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
   }
 }
 
+// Span-parallel documents (cld_long.hip "span-parallel scoring"): kParG
+// spans per wave (k_lgroup), then the document level per document
+// (k_lfinish), for pass 1 and -- after k_lrep -- pass 2.
+using ParSmem = lng::SmemT<LNG_ST_TEXT, false, true>;
+using FinSmem = lng::SmemT<16, false>;
+
+template <bool P2>
+__global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lgroup(
+    const DevTables* __restrict__ Tp, const uint32_t* __restrict__ list, uint8_t* __restrict__ slots,
+    uint8_t* __restrict__ pool, const uint64_t* __restrict__ meta, const uint64_t* __restrict__ group_list,
+    uint32_t gcap, uint32_t* __restrict__ counters, uint32_t cflags, const uint8_t* __restrict__ special,
+    const uint32_t* __restrict__ priors) {
+  __shared__ ParSmem smem[kStWPB];
+  const DevTables& T = *Tp;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
+  uint32_t total = wave::uflu(
+      __hip_atomic_load(&counters[P2 ? kCtrStG2 : kCtrStG1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  total = total < gcap ? total : gcap;
+  if (total == 0) return;
+  if (lane == 0) {
+    smem[wv].dbg = nullptr;
+    smem[wv].dbg_pos = 0;
+    smem[wv].prof = nullptr;
+  }
+  for (;;) {
+    const uint32_t e = wave::uflu(atomicAdd(&counters[P2 ? kCtrStDqG2 : kCtrStDqG1], lane == 0 ? 1u : 0u));
+    if (e >= total) break;                       // every wave reaches this exit
+    const uint64_t it = group_list[e];
+    if (it == ~0ull) continue;
+    const uint32_t k = (uint32_t)it, g = (uint32_t)(it >> 32);
+    const uint64_t at = meta[k];
+    if (at == lng::kStNone) continue;            // (pass 2: k_lrep handed it to k_general)
+    const uint32_t i = list[k];
+    const uint8_t spi = special ? special[i] : (uint8_t)0;
+    const int nsp = (int)wave::uflu(gld(&reinterpret_cast<const lng::StHdr*>(pool + at)->nsp));
+    const int j0 = (int)g * lng::kParG, j1 = min(nsp, j0 + lng::kParG);
+    (void)lng::st_group(T, S, smem[wv], pool + at, j0, j1, cflags,
+                        (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, lane);
+  }
+}
+
+template <bool P2>
+__global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lfinish(
+    const DevTables* __restrict__ Tp, const uint32_t* __restrict__ list, cld_result* __restrict__ out,
+    uint8_t* __restrict__ pool, const uint64_t* __restrict__ meta, uint32_t* __restrict__ par_lists, uint32_t n,
+    uint64_t* __restrict__ group_list2, uint32_t gcap, uint32_t* __restrict__ p2_list,
+    uint32_t* __restrict__ fall_list, uint32_t* __restrict__ counters, uint32_t cflags) {
+  __shared__ FinSmem smem[kStWPB];
+  const DevTables& T = *Tp;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t* in_list = par_lists + (P2 ? n : 0);
+  const uint32_t total = wave::uflu(
+      __hip_atomic_load(&counters[P2 ? kCtrStPar2 : kCtrStPar1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (total == 0) return;
+  for (;;) {
+    const uint32_t e = wave::uflu(atomicAdd(&counters[P2 ? kCtrStDqF2 : kCtrStDqF1], lane == 0 ? 1u : 0u));
+    if (e >= total) break;                       // every wave reaches this exit
+    const uint32_t k = in_list[e];
+    const uint64_t at = meta[k];
+    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
+    const uint32_t i = list[k];
+    const int r = lng::st_par_finish(T, smem[wv], pool + at, P2, &out[i], cflags, lane);
+    if (r == 0 && !P2) {                         // pass 2: Repeats (k_lrep), then its groups again
+      const int nsp = (int)wave::uflu(gld(&reinterpret_cast<const lng::StHdr*>(pool + at)->nsp));
+      const uint32_t ng = (uint32_t)(nsp + lng::kParG - 1) / lng::kParG;
+      uint32_t gb = 0;
+      if (lane == 0) gb = atomicAdd(&counters[kCtrStG2], ng);
+      gb = wave::uflu(__shfl((int)gb, 0, 64));
+      const bool fits = (uint64_t)gb + ng <= gcap;
+      for (uint32_t g = lane; g < ng && gb + g < gcap; g += 64)
+        group_list2[gb + g] = fits ? ((uint64_t)k | ((uint64_t)g << 32)) : ~0ull;
+      if (lane == 0) {
+        if (fits) {
+          p2_list[atomicAdd(&counters[kCtrStP2], 1u)] = k | 0x80000000u;
+          par_lists[n + atomicAdd(&counters[kCtrStPar2], 1u)] = k;
+        } else {
+          fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
+        }
+      }
+    } else if (lane == 0) {
+      if (r == 1) atomicAdd(&counters[P2 ? kCtrPass2 : kCtrPass1], 1u);
+      else fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;   // (records outgrew their room, a group failed)
+    }
+  }
+}
+
 __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __restrict__ list,
                                                          uint8_t* __restrict__ slots, uint8_t* __restrict__ pool,
                                                          uint64_t* __restrict__ meta,
@@ -564,7 +667,7 @@ __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __rest
   for (;;) {
     const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrStDqRep], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
-    const uint32_t k = p2_list[e];
+    const uint32_t k = p2_list[e] & 0x7FFFFFFFu;   // (bit 31: a span-parallel document)
     if (!lng::st_rep(pred, S, pool + meta[k], lane) && lane == 0) {
       meta[k] = lng::kStNone;
       requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = list[k];
@@ -748,20 +851,33 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, const uint32_t* hist, hipStream_t s) {
+                             uint32_t small_total, const uint32_t* hist, uint32_t heavy_kb, uint32_t* par_lists,
+                             size_t n, size_t gcap, hipStream_t s) {
   // n_waves: the slots (resident waves) of the widest launch below
   const int per_simd = cld_staged_waves_per_simd();
   const int cus = n_waves / (4 * per_simd);
   if (cus < 1) return hipErrorInvalidValue;
   const dim3 gst(cus * 4 * LNG_ST_WPS / cld::kStWPB), gsp(cus * 4 * LNG_SPAN_WPS / cld::kStWPB), bst(64 * cld::kStWPB);
+  uint64_t* gl1 = reinterpret_cast<uint64_t*>(par_lists + 2 * n);
+  uint64_t* gl2 = gl1 + gcap;
+  const uint32_t gc = (uint32_t)gcap, nn = (uint32_t)n;
   hipLaunchKernelGGL(cld::k_lspan, gsp, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
-                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total, hist);
+                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total, hist, par_lists, gl1, gc,
+                     heavy_kb);
   hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
                      fall_list, counters, cflags, special, priors);
+  hipLaunchKernelGGL(cld::k_lgroup<false>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl1, gc, counters, cflags,
+                     special, priors);
+  hipLaunchKernelGGL(cld::k_lfinish<false>, gst, bst, 0, s, d_T, list, out, pool, meta, par_lists, nn, gl2, gc,
+                     p2_list, fall_list, counters, cflags);
   hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,
                      requeue2, counters);
   hipLaunchKernelGGL(cld::k_lscore<true>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, p2_list, p2_list,
                      fall_list, counters, cflags, special, priors);
+  hipLaunchKernelGGL(cld::k_lgroup<true>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl2, gc, counters, cflags,
+                     special, priors);
+  hipLaunchKernelGGL(cld::k_lfinish<true>, gst, bst, 0, s, d_T, list, out, pool, meta, par_lists, nn, gl2, gc,
+                     p2_list, fall_list, counters, cflags);
   return hipGetLastError();
 }
 

@@ -133,8 +133,11 @@ struct Slot {
 // rep_all), so they share the first 8 KB.  The staged kernels (k_lspan /
 // k_lscore / k_lrep) score without the predictor and with a smaller text
 // window: SmemT<TEXT, false> (the stage functions take either layout).
-template <int TEXT, bool PRED>
+template <int TEXT, bool PRED, bool REC = false>
 struct alignas(16) SmemT {
+  // REC (the span-parallel scoring of k_lgroup): DocTote adds are recorded
+  // in order at rec[rec_n++] instead of added, and replayed by k_lfinish
+  static constexpr bool kRec = REC;
   union {
     struct {
       uint8_t text[TEXT];                // a window of the current span's lowered text (Win)
@@ -159,8 +162,26 @@ struct alignas(16) SmemT {
   uint32_t* dbg;                         // debug dump of one document (CLD_DEBUG_DOC), else null
   uint32_t dbg_pos;
   unsigned long long* prof;              // per-stage cycle sums (CLD_PROFILE_STAGES=1), else null
+  uint64_t* rec;                         // (REC) where this span's DocTote adds go
+  uint32_t rec_n, rec_cap;
+  int rec_over;                          // (REC) more adds than rec_cap
 };
 using Smem = SmemT<kLdsText, true>;
+// A DocTote add as recorded (REC): key | bytes << 16 | score << 32 | reliability << 48.
+__device__ __forceinline__ uint64_t dt_rec(int key, int bytes, int score, int rel) {
+  return (uint64_t)(uint16_t)key | ((uint64_t)(uint16_t)bytes << 16) | ((uint64_t)(uint16_t)score << 32) |
+         ((uint64_t)(uint8_t)rel << 48);
+}
+template <class SM>
+__device__ __forceinline__ void dt_add(SM& s, int key, int bytes, int score, int rel) {   // lane 0
+  if constexpr (SM::kRec) {
+    if (s.rec_n < s.rec_cap) s.rec[s.rec_n] = dt_rec(key, bytes, score, rel);
+    else s.rec_over = 1;
+    ++s.rec_n;
+  } else {
+    s.dt.add((uint16_t)key, bytes, score, rel);
+  }
+}
 static_assert(sizeof(Smem) <= 10240, "k_long LDS per wave: 4 blocks of 4 waves per CU must fit 160 KB");
 
 // ------------------------------------------------ ResultChunkVector (vec mode)
@@ -2328,7 +2349,7 @@ LNG_SR_INL void score_round(const DevTables& T, Slot& S, SM& s, int ulscript, bo
     const int r1 = rdl(rd, k), r2 = rdl(rsc, k);
     if (lane == 0) {
       const uint16_t bytes = (uint16_t)(h0 - l0);
-      if (k < kMaxSummaries) s.dt.add((uint16_t)l1, bytes, sc, r1 < r2 ? r1 : r2);
+      if (k < kMaxSummaries) dt_add(s, (uint16_t)l1, bytes, sc, r1 < r2 ? r1 : r2);
       if (D && s.dbg) {
         const int bs = s.bst[k], be = k == K - 1 ? eb : s.bst[k + 1];
         const int ds = s.st[0][k], de = s.st[0][k + 1], xs = s.st[1][k], xe = s.st[1][k + 1];
@@ -2427,7 +2448,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, SM& s, W
   int rt = rtype_of(T, ulscript);
   if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // scoreonescriptspan.cc:1318-1320
   if (rt == RTypeNone || rt == RTypeOne) {
-    if (lane == 0) s.dt.add((uint16_t)default_language(T, ulscript), tb, tb, 100);
+    if (lane == 0) dt_add(s, (uint16_t)default_language(T, ulscript), tb, tb, 100);
     wsync();
     if constexpr (VEC) {
       // JustOneItemToVector (:513-548): the span after its leading space
@@ -2732,8 +2753,10 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
 // A document's region: StHdr, the spans back to back (each followed by its
 // pads and NULs, 16-byte aligned), then the span table (one u64 per span:
 // offset in the region | text_bytes << 32 | ulscript << 56).
+constexpr int kParMin = 48, kParG = 16;      // span-parallel documents: > kParMin spans, kParG spans per group
 struct StHdr {
-  uint32_t nsp, careful, tab, rsv;
+  uint32_t nsp, careful, tab;
+  uint32_t par;                                  // span-parallel documents: offset of the record arrays, else 0
 };
 constexpr uint64_t kStNone = ~0ull;
 __device__ __forceinline__ int st_advance(int tb) { return (tb + 48 + 15) & ~15; }   // text + "   \0" + NULs
@@ -2763,7 +2786,20 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
     cur += st_advance(tb);
   }
   gsync();
-  const uint32_t units = (uint32_t)((sizeof(StHdr) + cur + 8 * nsp + 15) >> 4);
+  // span-parallel documents (more than kParMin spans): after the span table,
+  // roff[nsp + 1] (first record of span j), rcnt[nsp], then the records --
+  // at most tb / 16 + 8 DocTote adds per span (a chunk holds >= 20 base hits
+  // or 50 unigrams, a round <= 1000 hits: chunks <= tb / 40 + rounds)
+  uint32_t par = 0, recs = 0;
+  uint64_t bytes = sizeof(StHdr) + cur + 8ull * nsp;
+  if (nsp > kParMin) {
+    par = (uint32_t)bytes;
+    for (int j = 0; j < nsp; ++j) recs += (uint32_t)(ufl(S.sp_tb[j]) / 16 + 8);
+    bytes += 4ull * (2 * nsp + 1);
+    bytes = (bytes + 7) & ~7ull;
+    bytes += 8ull * recs;
+  }
+  const uint32_t units = (uint32_t)((bytes + 15) >> 4);
   uint32_t got = 0;
   if (lane == 0) got = atomicAdd(pool_ctr, units);
   got = uflu(__shfl((int)got, 0, 64));
@@ -2777,8 +2813,19 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   for (int j = lane; j < nsp; j += 64)
     tab[j] = (uint64_t)(uint32_t)(S.sp_off[j] + (int)sizeof(StHdr)) | ((uint64_t)(uint32_t)S.sp_tb[j] << 32) |
              ((uint64_t)(uint32_t)S.sp_ul[j] << 56);
+  if (par) {                                     // record offsets (lane 0: once per document)
+    uint32_t* roff = reinterpret_cast<uint32_t*>(region + par);
+    if (lane == 0) {
+      uint32_t acc = 0;
+      for (int j = 0; j < nsp; ++j) {
+        roff[j] = acc;
+        acc += (uint32_t)(S.sp_tb[j] / 16 + 8);
+      }
+      roff[nsp] = acc;
+    }
+  }
   if (lane == 0) {
-    StHdr h{(uint32_t)nsp, careful ? 1u : 0u, (uint32_t)(sizeof(StHdr) + cur), 0u};
+    StHdr h{(uint32_t)nsp, careful ? 1u : 0u, (uint32_t)(sizeof(StHdr) + cur), par};
     *reinterpret_cast<StHdr*>(region) = h;
   }
   gsync();
@@ -2848,6 +2895,212 @@ __device__ __forceinline__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, 
   }
   gsync();
   return true;
+}
+
+// ------------------------------------------------ span-parallel scoring
+// A span costs a wave ~15 us per pass whatever its length (every stage is a
+// chain of dependent steps), so a document of thousands of short spans --
+// scripts alternating word by word -- takes one wave tens of milliseconds
+// (a 64 KB page of 3,082 spans: 48 ms; profiles/round5_doc_latency.jsonl), and
+// every launch holding one waits for it.  Within a pass the spans depend on
+// each other only through the DocTote (adds in span order) and the boost ring
+// of each script class (the last four distinct-hit langprobs,
+// scoreonescriptspan.cc:112-152, 305-315).  So a document of more than
+// kParMin spans is scored kParG spans per wave (k_lgroup, st_group):
+//   * a group's entering ring, per class its spans use, is the last four
+//     distinct emissions of the earlier spans of that class: they come from
+//     re-running the hit rounds (no scoring) of those spans, newest first,
+//     until four are found or the document start is reached (span_distinct);
+//   * the group's spans are then scored as one wave would, the ring carried
+//     from span to span, and their DocTote adds recorded in order (REC);
+//   * k_lfinish replays every span's adds into the DocTote in span order and
+//     runs the document level (st_par_finish).
+// Scoring is a function of the span text, the entering ring and the priors,
+// so the result is what one wave scoring the spans in order computes.
+
+// The rtype a stored span is scored with (score_span).
+__device__ __forceinline__ int span_rt(const DevTables& T, int ul, uint32_t cflags) {
+  int rt = rtype_of(T, ul);
+  if ((cflags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;
+  return rt;
+}
+
+// A round's last (up to) four distinct emissions into last[] (newest at [3]).
+__device__ __forceinline__ void take_distinct(const Slot& S, int exm, uint32_t (&last)[4], int& cnt) {
+  for (int i = exm - 4 < 0 ? 0 : exm - 4; i < exm; ++i) {
+    last[0] = last[1];
+    last[1] = last[2];
+    last[2] = last[3];
+    last[3] = uflu(gld(&S.x_ai[i]));
+    ++cnt;
+  }
+}
+
+// The distinct emissions of one stored span (its hit rounds, no scoring):
+// the last four as tote adds into ring[idx-4 .. idx) going backwards -- the
+// newest is written at ring[idx - 1] -- until idx reaches 0.
+template <class SM>
+__device__ __forceinline__ bool span_distinct(const DevTables& T, Slot& S, SM& s, const uint8_t* lb, int tb, int rt,
+                                              uint64_t* ring, int& idx, int lane) {
+  if (rt == RTypeNone || rt == RTypeOne || tb <= 1) return true;
+  bool ok = true;
+  Win win{lb, 0, 0, (tb + 48 + 15) & ~15};
+  if (tb + 48 <= (int)sizeof(s.text)) {
+    const int n16 = (tb + 48 + 15) >> 4;
+    for (int i = lane; i < n16; i += 64)
+      reinterpret_cast<uint4*>(s.text)[i] = gld4(reinterpret_cast<const uint32_t*>(lb) + 4 * i);
+    wsync();
+    win = Win{nullptr, 0, 16 * n16, 16 * n16};
+  }
+  // the rounds' distinct emissions, newest last; kept: the last four overall
+  uint32_t last[4] = {0, 0, 0, 0};               // adds indices, newest at [3]
+  int cnt = 0;
+  int off = 1;
+  if (rt == RTypeCJK) {
+    while (off < tb) {
+      int nb, nd, nx, eb, edm, exm;
+      const int next = cjk_round<false>(T, win, s, tb, S, off, nb, nd, nx, eb, edm, exm, ok, lane);
+      if (!ok) return false;
+      take_distinct(S, exm, last, cnt);
+      off = next;
+    }
+  } else {
+    const int start = 1 + (ufl(win_text(win, s, 0, 2, ok, lane)[1]) == ' ' ? 1 : 0);
+    int nws, nsp;
+    if (!ok || !word_lists(win, s, tb, start, S, nws, nsp, lane)) return false;
+    const int nch = build_chain(win, s, tb, S, nws, lane);
+    if (nch < 0) return false;
+    int c0 = 0, j0 = 0;
+    while (off < tb) {
+      int nb, nd, nx, eb, edm, exm;
+      const int next = quad_round<false>(T, win, s, tb, S, nch, c0, nb, eb, ok, lane);
+      if (!ok) return false;
+      octa_round<false>(T, win, s, S, nsp, j0, off, next, nd, nx, edm, exm, ok, lane);
+      if (!ok) return false;
+      take_distinct(S, exm, last, cnt);
+      off = next;
+    }
+  }
+  const int n = cnt < 4 ? cnt : 4;
+  for (int i = 0; i < n && idx > 0; ++i) {
+    --idx;
+    if (lane == 0) ring[idx] = adds_by_index(T, last[3 - i]);
+  }
+  return true;
+}
+
+// Group [j0, j1) of a span-parallel document: priors, the entering rings
+// (lookback), then the spans scored in order with their DocTote adds
+// recorded.  Returns 1, or -kWhyCapacity (the fused kernel redoes it).
+template <class SM>
+__device__ __forceinline__ int st_group(const DevTables& T, Slot& S, SM& s, uint8_t* region, int j0, int j1,
+                                        uint32_t cflags, const uint32_t* __restrict__ pri, int lane) {
+  if (lane == 0) s.has_pri = pri != nullptr;
+  if (lane < 16) {
+    const uint32_t lp = pri ? gld(pri + lane) : 0u;
+    if (lane < 8) s.pri_add[lane >> 2][lane & 3] = lp ? tote_adds(T, lp) : 0ull;
+    else s.pri_wk[(lane - 8) >> 2][lane & 3] = (uint8_t)((lp >> 8) & 0xFF);
+  }
+  if (lane < 8) s.ring[lane >> 2][lane & 3] = 0;
+  wsync();
+  const StHdr* h = reinterpret_cast<const StHdr*>(region);
+  const uint64_t* tab = reinterpret_cast<const uint64_t*>(region + uflu(gld(&h->tab)));
+  const uint32_t par = uflu(gld(&h->par));
+  const uint32_t* roff = reinterpret_cast<const uint32_t*>(region + par);
+  const int nsp = (int)uflu(gld(&h->nsp));
+  uint32_t* rcnt = const_cast<uint32_t*>(roff) + nsp + 1;
+  uint64_t* recs = reinterpret_cast<uint64_t*>(region + ((par + 4ull * (2 * nsp + 1) + 7) & ~7ull));
+  // the classes the group's scored spans use
+  bool need[2] = {false, false};
+  for (int j = j0; j < j1; ++j) {
+    const uint64_t e = ufl64(gld(tab + j));
+    const int ul = (int)(e >> 56), rt = span_rt(T, ul, cflags);
+    if (rt == RTypeMany || rt == RTypeCJK) need[((uint32_t)ul == T.latin) ? 0 : 1] = true;
+  }
+  int idx[2] = {need[0] ? 4 : 0, need[1] ? 4 : 0};
+  for (int j = j0 - 1; j >= 0 && (idx[0] > 0 || idx[1] > 0); --j) {
+    const uint64_t e = ufl64(gld(tab + j));
+    const int ul = (int)(e >> 56), tb = (int)((e >> 32) & 0xFFFFFF), rt = span_rt(T, ul, cflags);
+    const int rs = ((uint32_t)ul == T.latin) ? 0 : 1;
+    if (idx[rs] == 0 || !(rt == RTypeMany || rt == RTypeCJK)) continue;
+    if (!span_distinct(T, S, s, region + (uint32_t)e, tb, rt, s.ring[rs], idx[rs], lane)) {
+      if (lane == 0) rcnt[j0] = 0xFFFFFFFFu;
+      gsync();
+      return -kWhyCapacity;
+    }
+  }
+  wsync();
+  for (int j = j0; j < j1; ++j) {
+    const uint64_t e = ufl64(gld(tab + j));
+    const uint8_t* lb = region + (uint32_t)e;
+    const int tb = (int)((e >> 32) & 0xFFFFFF), ul = (int)(e >> 56);
+    if (lane == 0) {
+      const uint32_t r0 = gld(roff + j);
+      s.rec = recs + r0;
+      s.rec_cap = gld(roff + j + 1) - r0;
+      s.rec_n = 0;
+      s.rec_over = 0;
+    }
+    wsync();
+    bool ok;
+    if (tb + 48 <= (int)sizeof(s.text)) {
+      const int n16 = (tb + 48 + 15) >> 4;
+      for (int i = lane; i < n16; i += 64)
+        reinterpret_cast<uint4*>(s.text)[i] = gld4(reinterpret_cast<const uint32_t*>(lb) + 4 * i);
+      wsync();
+      Win win{nullptr, 0, 16 * n16, 16 * n16};
+      ok = score_span<false, false>(T, S, s, win, tb, ul, lane, nullptr, 0, cflags, nullptr);
+    } else {
+      Win win{lb, 0, 0, (tb + 48 + 15) & ~15};
+      ok = score_span<false, false>(T, S, s, win, tb, ul, lane, nullptr, 0, cflags, nullptr);
+    }
+    if (!ok) {
+      if (lane == 0) rcnt[j0] = 0xFFFFFFFFu;     // the document's finish hands it to the fused kernel
+      gsync();
+      return -kWhyCapacity;
+    }
+    if (lane == 0) rcnt[j] = s.rec_over ? 0xFFFFFFFFu : s.rec_n;
+  }
+  gsync();
+  return 1;
+}
+
+// The document level of a span-parallel document: every span's recorded
+// adds into the DocTote in span order, then finish_document.  Returns as
+// st_score; -kWhyCapacity when a span's adds outgrew their room.
+template <class SM>
+__device__ __forceinline__ int st_par_finish(const DevTables& T, SM& s, const uint8_t* region, bool rep,
+                                             cld_result* out, uint32_t cflags, int lane) {
+  const StHdr* h = reinterpret_cast<const StHdr*>(region);
+  const uint64_t* tab = reinterpret_cast<const uint64_t*>(region + uflu(gld(&h->tab)));
+  const uint32_t par = uflu(gld(&h->par));
+  const uint32_t* roff = reinterpret_cast<const uint32_t*>(region + par);
+  const int nsp = (int)uflu(gld(&h->nsp));
+  const uint32_t* rcnt = roff + nsp + 1;
+  const uint64_t* recs = reinterpret_cast<const uint64_t*>(region + ((par + 4ull * (2 * nsp + 1) + 7) & ~7ull));
+  int total = 0, bad = 0;
+  for (int j0 = 0; j0 < nsp; j0 += 64) {
+    const int j = j0 + lane;
+    int tb = 0;
+    if (j < nsp) {
+      tb = (int)((gld(tab + j) >> 32) & 0xFFFFFF);
+      bad |= gld(rcnt + j) == 0xFFFFFFFFu;
+    }
+    total += (int)wave::wsum((uint32_t)tb);
+  }
+  if (__ballot(bad != 0)) return -kWhyCapacity;
+  if (lane == 0) {
+    s.dt.init();
+    for (int j = 0; j < nsp; ++j) {
+      const uint32_t r0 = roff[j], n = rcnt[j];
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint64_t r = recs[r0 + k];
+        s.dt.add((uint16_t)(r & 0xFFFF), (int)((r >> 16) & 0xFFFF), (int)((r >> 32) & 0xFFFF), (int)((r >> 48) & 0xFF));
+      }
+    }
+  }
+  wsync();
+  return wave::finish_document(T, s.dt, total, rep, out, lane, (cflags & kCLDFlagBestEffort) != 0);
 }
 
 // The fused span builder emits separators and pads as ' ' without lowering

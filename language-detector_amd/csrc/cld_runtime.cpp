@@ -393,6 +393,7 @@ struct Device {
   uint8_t* d_store = nullptr; uint64_t store_bytes = 0;
   uint64_t* d_meta = nullptr; size_t meta_cap = 0;
   uint32_t* d_stlists = nullptr; size_t stlists_cap = 0;   // ok / pass-2 / fallback lists, 3 x cap
+  uint32_t* d_parlists = nullptr; size_t parlists_cap = 0; // span-parallel: 2 document lists + 2 group lists
   uint32_t* d_requeue2 = nullptr;
   size_t requeue2_cap = 0;
   bool long_order = true;       // k_long takes its list longest first (CLD_LONG_ORDER=0: arrival order)
@@ -683,6 +684,14 @@ constexpr uint32_t kPrepFlags = CLD_FLAG_STRIP_EXTRAS | CLD_FLAG_CSTRING;
 constexpr uint32_t kCldFlags = CLD_FLAG_SCORE_AS_QUADS | CLD_FLAG_BEST_EFFORT;
 constexpr uint32_t kPublicFlags = kCldFlags | CLD_FLAG_DEBUG_MASK;
 
+// Batches holding a document of this many KB go to the fused k_long whole
+// (CLD_LONG_HEAVY_KB; 0: never): its single-wave latency would repeat in
+// every stage kernel (cld_kernels.hip k_lspan).
+uint32_t heavy_kb() {
+  static const uint32_t v = getenv("CLD_LONG_HEAVY_KB") ? (uint32_t)atoi(getenv("CLD_LONG_HEAVY_KB")) : 20u;
+  return v;
+}
+
 // Text preparation (handlers.go:150-151) on device d: documents [buf, offs) ->
 // prepared documents in d->d_sbuf / d->d_soffs.  cap_bytes bounds offs[n].
 int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, uint64_t cap_bytes,
@@ -763,12 +772,16 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       if (grow(&d->d_stlists, &d->stlists_cap, 3 * std::max<size_t>(n, 1))) return CLD_ENOMEM;
       const size_t c = d->stlists_cap / 3;
       uint32_t* fall = d->d_stlists + 2 * c;
+      // span-parallel lists: documents (n each, passes 1 and 2) and groups
+      // (gcap each; a document whose groups find no room takes the fused kernel)
+      const size_t np = std::max<size_t>(n, 1), gcap = std::max<size_t>(4 * np, 1u << 16);
+      if (grow(&d->d_parlists, &d->parlists_cap, 2 * np + 4 * gcap)) return CLD_ENOMEM;
       // a list of at most 4 documents per fused wave goes whole to the fused
       // kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
                                priors, hbuf, hflag, d->fault_doc, 4u * (uint32_t)d->n_slots,
-                               d->long_order ? d->d_lhist : nullptr, s));
+                               d->long_order ? d->d_lhist : nullptr, heavy_kb(), d->d_parlists, np, gcap, s));
       list = fall;
       ctr_total = kCtrStFall;
       ctr_deq = kCtrStDqFall;
@@ -1779,7 +1792,7 @@ void cld_shutdown(void) {
     (void)hipFree(d->d_sbuf); (void)hipFree(d->d_soffs); (void)hipFree(d->d_sscr);
     (void)hipFree(d->d_hbuf); (void)hipFree(d->d_hflag); (void)hipFree(d->d_hpos);
     (void)hipFree(d->d_spec_out); (void)hipFree(d->d_spec_take);
-    (void)hipFree(d->d_store); (void)hipFree(d->d_meta); (void)hipFree(d->d_stlists);
+    (void)hipFree(d->d_store); (void)hipFree(d->d_meta); (void)hipFree(d->d_stlists); (void)hipFree(d->d_parlists);
     for (auto& t : d->ev_pool) for (auto& e : t) (void)hipEventDestroy(e);
     for (auto& h : d->hs) {
       (void)hipHostFree(h.h_in); (void)hipHostFree(h.h_offs); (void)hipHostFree(h.h_out);

@@ -228,11 +228,13 @@ print("staged ok", st.passes[0], st.passes[1])
 
 def test_staged_long_path_and_its_hand_ons(gpu, oracle):
     """The staged long-document path (cld_long.hip st_spans / st_score /
-    st_rep in k_lspan / k_lscore / k_lrep) and the documents it hands to the
-    fused k_long: a span block wider than its 2 KB LDS window (a 3 KB word),
-    hundreds of spans, the Squeeze restart, pass 2 with Repeats -- in one
-    batch large enough to take the staged path (more than 4 documents per
-    fused wave), all equal to the oracle and none on the sequential kernel.
+    st_rep in k_lspan / k_lscore / k_lrep, span-parallel documents in
+    k_lgroup / k_lfinish) and the documents it hands to the fused k_long: a
+    span block wider than its 2 KB LDS window (a 3 KB word), hundreds of
+    spans (span-parallel, passes 1 and 2), more than 1,024 spans, the Squeeze
+    restart, pass 2 with Repeats -- in one batch large enough to take the
+    staged path (more than 4 documents per fused wave), all equal to the
+    oracle and none on the sequential kernel.
     Then the store exhausted (CLD_LONG_STORE_MB=1, child process): every
     document the store cannot hold goes to the fused kernel, same results."""
     import subprocess
@@ -242,8 +244,18 @@ def test_staged_long_path_and_its_hand_ons(gpu, oracle):
     b2, o2 = corpus.c2(3000, seed=173)
     docs[5] = b"x" * 3000 + b" " + bytes(b2[o2[0]:o2[40]])                  # one 3 KB word
     docs[9] = " ".join(["ab", "где", "xy", "कि"] * 300).encode()             # ~1200 spans
-    docs[11] = ("abc дом " * 500).encode()                                      # many two-script spans
+    docs[11] = ("abc дом " * 500).encode()                                      # many two-script spans (span-parallel)
     docs[13] = corpus.BOILERPLATE * 20 + bytes(b2[o2[0]:o2[30]])             # the Squeeze restart
+    # span-parallel documents (more than 48 spans, cld_long.hip "span-parallel
+    # scoring"): the words of 16 KB four-script pages shuffled, so scripts
+    # alternate every word or few -- hundreds of spans, pass 1 and pass 2
+    rng = np.random.default_rng(174)
+    bw, ow = corpus.c3(400, seed=175, page=8192)
+    for k in range(400):
+        w = bytes(bw[ow[k]:ow[k + 1]]).split()
+        rng.shuffle(w)
+        cut = int(rng.integers(len(w) // 4, len(w)))
+        docs[20 + 7 * k] = b" ".join(w[:cut])
     buf, offs = gpu.pack(docs)
     got = check(gpu, oracle, buf, offs, "staged")
     st = gpu.last_stats(0)
