@@ -69,8 +69,8 @@ constexpr int kMaxCh = 64;                           // chunks per round (<= 50 
 // Span cache: pass 1 builds every lowered span into lbd (16-byte aligned, each
 // followed by its pads), so pass 2 (Repeats) reads them back instead of
 // re-running the span builder over the per-byte classes.
-constexpr int kLbdCap = 160 * 1024;
-constexpr int kMaxSpans = 1024;
+constexpr int kLbdCap = 512 * 1024;
+constexpr int kMaxSpans = 4096;
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 // A lowered span of up to kLdsText - 48 bytes (pads included) is scored from
 // LDS: the chain walk, the gram hashes and the word scans then read the text
