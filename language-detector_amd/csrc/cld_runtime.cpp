@@ -685,10 +685,12 @@ constexpr uint32_t kCldFlags = CLD_FLAG_SCORE_AS_QUADS | CLD_FLAG_BEST_EFFORT;
 constexpr uint32_t kPublicFlags = kCldFlags | CLD_FLAG_DEBUG_MASK;
 
 // Batches holding a document of this many KB go to the fused k_long whole
-// (CLD_LONG_HEAVY_KB; 0: never): its single-wave latency would repeat in
-// every stage kernel (cld_kernels.hip k_lspan).
+// (CLD_LONG_HEAVY_KB; default 0: never).  Before span-parallel scoring a C5
+// batch's many-span 64 KB pages (~48 ms on one wave) repeated their latency
+// in every stage kernel, and 20 KB kept C5 on the fused kernel (18.1M
+// docs/s); with it the staged path runs C5 at 22.0M (gpurun_out/r5r).
 uint32_t heavy_kb() {
-  static const uint32_t v = getenv("CLD_LONG_HEAVY_KB") ? (uint32_t)atoi(getenv("CLD_LONG_HEAVY_KB")) : 20u;
+  static const uint32_t v = getenv("CLD_LONG_HEAVY_KB") ? (uint32_t)atoi(getenv("CLD_LONG_HEAVY_KB")) : 0u;
   return v;
 }
 
