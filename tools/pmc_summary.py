@@ -9,20 +9,28 @@ from collections import defaultdict
 
 
 def summarise(d):
-    vals = defaultdict(list)
-    info = {}
+    """Per-launch counters: per kernel name the average over its dispatches
+    (the first, cold one excluded when there are more), summed over the
+    kernels the regex matched -- a pipeline of kernels (the staged long path)
+    is reported per launch of the whole pipeline."""
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))   # counter -> kernel -> dispatch -> value
+    kinfo = {}
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
-        per = defaultdict(lambda: defaultdict(float))
         for r in csv.DictReader(open(f)):
-            per[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
-            info = {"kernel": r["Kernel_Name"].split("(")[0], "grid": int(r["Grid_Size"]),
-                    "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]), "scratch": int(r["Scratch_Size"]),
-                    "lds": int(r["LDS_Block_Size"])}
-        for c, byd in per.items():
-            v = [byd[k] for k in sorted(byd)]
+            k = r["Kernel_Name"].split("(")[0]
+            per[r["Counter_Name"]][k][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            kinfo[k] = {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                        "scratch": int(r["Scratch_Size"]), "lds": int(r["LDS_Block_Size"])}
+    vals = defaultdict(float)
+    for c, byk in per.items():
+        for k, byd in byk.items():
+            v = [byd[x] for x in sorted(byd)]
             if len(v) > 1:
                 v = v[1:]
-            vals[c] = sum(v) / len(v)
+            vals[c] += sum(v) / len(v)
+    info = {"kernel": " + ".join(sorted(kinfo)), "kernels": kinfo}
+    if len(kinfo) == 1:
+        info.update(next(iter(kinfo.values())))
     out = dict(info)
     out["counters_per_launch"] = dict(vals)
     v = vals

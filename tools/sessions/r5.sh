@@ -28,7 +28,7 @@ for s in ${STEPS:-suite smoke bench}; do
       (cd /tmp && step 300 prof_c3.log rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o c3 --output-format csv -- python3 $R/bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1 ;;
     pmc)
       step 400 pmc_c2.log bash tools/pmc_session.sh ${TAG}_pmc_c2 c2 k_wave
-      step 400 pmc_c3.log bash tools/pmc_session.sh ${TAG}_pmc_c3 c3 k_long ;;
+      step 400 pmc_c3.log bash tools/pmc_session.sh ${TAG}_pmc_c3 c3 "k_l(span|score|group|finish|rep|ong)" ;;
     dl) step 400 dl_rate.jsonl python3 tools/dl_rate.py ;;
     ab)  # staged vs fused long-document path (A/B), C3 and C5 lines
       for c in ${ABCFG:-c3 c5}; do
