@@ -20,9 +20,8 @@
 //     on an entity saw the raw '&' (script 0): the rewrite marks those
 //     positions in hflag, and the span builders read script 0 there;
 //   * the lowercaser's HTML half: a page holding a character whose HTML-mode
-//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, more
-//     than kHtmlCands '<' / '&' bytes, or more than kHtmlRewriteMax bytes is not
-//     rewritten and stays on k_general.  (The span soft limit reads the raw
+//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, or
+//     more than kHtmlRewriteMax bytes is not rewritten and stays on k_general.  (The span soft limit reads the raw
 //     bytes left, :815-819; it splits nothing below kMaxScriptBytes, ~40 KB,
 //     so up to 32 KB raw and rewritten pages cut their spans alike.)
 // A rewritten page that k_wave / k_long re-queue goes to k_general, which
@@ -32,7 +31,8 @@
 // sequential, but only its '<' / '&' stops carry state):
 //   1. the page goes to LDS; every '<' and '&' of it is a candidate; each
 //      lane evaluates one '&' as if the scan reached it (ReadEntity: bytes
-//      consumed, bytes decoded) into an LDS list;
+//      consumed, bytes decoded) into an LDS list (a segment of the page at a
+//      time: whole 64-byte windows holding at most kHtmlCands candidates);
 //   2. the scan's order decides which candidates it reaches: a candidate
 //      inside an earlier reached tag or entity is skipped (a scalar walk over
 //      the list, 64 candidates per register); a reached '<' is scanned there,
@@ -55,7 +55,7 @@ using wave::wsync;
 
 constexpr int kHtmlRewriteMax = 32768;  // larger pages stay on k_general (the span soft limit, above)
 constexpr int kHtmlStage = 8192;        // pages up to this size are staged in LDS, larger ones read in place
-constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per page (more: the page stays on k_general)
+constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per segment of a page (round 5: any number per page)
 constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
 
 // The character b0 b1 b2 (n bytes) lowers the same way in HTML mode as in plain text.
@@ -139,161 +139,171 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
                                              unsigned long long* __restrict__ prof, const uint64_t am0,
                                              const uint64_t am1, const int lane) {
   const DocView dv{txt, L};
-  // 1a. candidates, in page order
-  int K = 0;
-  for (int w0 = 0; w0 < L; w0 += 64) {
-    const int p = w0 + lane;
-    const uint32_t c = p < L ? txt[p] : 0u;
-    const bool cand = c == '<' || c == '&';
-    const uint64_t m = __ballot(cand);
-    const int k = K + __popcll(m & lanemask_lt(lane));
-    if (cand && k < kHtmlCands) S.pos[k] = (uint16_t)p;
-    K += __popcll(m);
-  }
-  if (K > kHtmlCands) return;                                // stays HTML: k_general
-  wsync();
-  // 1b. each candidate as if the scan reached it
-  for (int j = lane; j < K; j += 64) {
-    const int p = S.pos[j];
-    int ln = 1, kind = 0, plen = 0;
-    bool bad = false;
-    uint32_t dec = 0;
-    if (txt[p] == '<') {
-      ln = 0;                                                  // (a reached tag is scanned in step 2)
-    } else {
-      uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      int tlen = 0;
-      entity_to_buffer(T, dv, p, L - p, tmp, &tlen, &plen);
-      if (plen > 0) {
-        kind = 1;
-        ln = tlen;
-        dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
-        bad = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
-              (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
-      } else {
-        kind = 2;                                              // undecodable: the '&' is dropped
-        plen = 0;
-      }
-    }
-    S.len[j] = (uint16_t)ln;
-    S.dec[j] = dec;
-    S.meta[j] = (uint8_t)(kind | (plen << 2) | (bad ? 0x20 : 0));
-  }
-  wsync();
-  // 2. which candidates the scan reaches: past the end of the last reached one
-  const long long t2 = prof ? (long long)clock64() : 0;
-  int cur = 0;
-  for (int j0 = 0; j0 < K; j0 += 64) {
-    const int j = j0 + lane;
-    const int p = j < K ? (int)S.pos[j] : 0x7FFFFFFF, ln = j < K ? (int)S.len[j] : 0;
-    const int m = K - j0 < 64 ? K - j0 : 64;
-    const uint64_t tag_m = __ballot(j < K && (S.meta[j] & 3) == 0);
-    uint64_t reach = 0;
-    for (int t = 0; t < m; ++t) {
-      const int pt = rdl(p, t);
-      if (pt >= cur) {
-        reach |= 1ull << t;
-        int lt = rdl(ln, t);
-        if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
-          lt = scan_tag_wave(tt, txt, pt, L - pt, lane);
-          if (lane == t) S.len[j] = (uint16_t)lt;
-        }
-        cur = pt + lt;
-      }
-    }
-    if (j < K) S.meta[j] = (uint8_t)(S.meta[j] | (((reach >> lane) & 1) ? 0x40 : 0));
-  }
-  wsync();
-  if (prof && lane == 0) atomicAdd(prof, (unsigned long long)((long long)clock64() - t2));
-  // 3. the output, window by window
+  // The page in segments of whole 64-byte windows holding at most kHtmlCands
+  // candidates each: steps 1-2 per segment (the scan's reach carried in
+  // `cur`), then step 3 over the segment's windows (its carries below).  A
+  // tag or entity reached in one segment may run into the next: `cur` skips
+  // the candidates it covers there, `cover` the text bytes.
   uint8_t* o = hbuf + a;
   uint8_t* f = hflag + a;
   uint32_t* hp = hpos ? hpos + a : nullptr;
   uint32_t* hg = hpos ? hgap + a : nullptr;
-  int q = 0, cb = 0, bad = 0, conts = 0, need = 0, novec = 0;
+  int q = 0, bad = 0, conts = 0, need = 0, novec = 0;
   int drop_run = 0;                                            // dropped '&'s ending the previous window
   uint32_t cover = 0;                                          // end of the last reached candidate so far
   uint32_t drop_prev = 0;                                      // the byte before this window was a dropped '&'
-  for (int w0 = 0; w0 < L; w0 += 64) {
-    const int p = w0 + lane;
-    const bool in = p < L;
-    const uint32_t c = in ? txt[p] : 0u;
-    const bool cand = in && (c == '<' || c == '&');
-    const uint64_t cm = __ballot(cand);
-    const int j = cand ? cb + __popcll(cm & lanemask_lt(lane)) : 0;
-    cb += __popcll(cm);
-    const uint32_t meta = cand ? S.meta[j] : 0u;
-    const bool reached = (meta & 0x40) != 0;
-    const uint32_t end = reached ? (uint32_t)(p + S.len[j]) : 0u;
-    // covered: inside a reached candidate that starts before p (the running
-    // maximum of reached ends, carried across windows)
-    const uint32_t mx = dpp_scan_incl(end, 0u, OpMax());
-    const uint32_t before = wshr1(mx, 0u);
-    const uint32_t cov_end = before > cover ? before : cover;
-    const bool covered = in && !reached && (uint32_t)p < cov_end;
-    const int kind = meta & 3, plen = (meta >> 2) & 7;
-    const bool text = in && !covered && !reached;
-    int emit = 0;
-    if (reached) emit = kind == 0 ? 1 : kind == 1 ? plen : 0;
-    else if (text) emit = 1;
-    // the first byte after a dropped '&' carries the lookahead mark
-    const bool dropped = reached && kind == 2;
-    const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
-    const int at = q + excl_scan(emit, lane);
-    // vec mode (hpos): every output byte's page offset, as map2original_ maps
-    // it -- a text byte its own, a tag's space the tag start, an entity's k-th
-    // byte start + k (Copy(plen), then Delete(tlen - plen)).  An entity whose
-    // Delete is a single byte, or that grows (Insert), could merge with the
-    // run's closing Insert(1) into a Copy (offsetmap.cc:122-156): such pages
-    // keep the sequential kernel in vec mode (kSpecialNoVec).
-    // the first byte after dropped '&'s also records where they began (hpos
-    // second half, read where hflag bit 1 is set): a run ending there has its
-    // gap start at the first of them (they merge into the gap's Delete)
-    const uint64_t dm = __ballot(dropped);
-    if (hp && dprev) {
-      const uint64_t nd = ~dm & lanemask_lt(lane);             // bytes before this one that were not dropped
-      const int first = nd ? w0 + (63 - __builtin_clzll(nd)) + 1 : w0 - drop_run;
-      hg[at] = (uint32_t)first;
+  int cur = 0;                                                 // the scan's position after the last reached one
+  for (int P0 = 0; P0 < L;) {
+    // 1a. the segment's candidates, in page order: whole windows while they fit
+    int K = 0, P1 = P0;
+    for (int w0 = P0; w0 < L; w0 += 64) {
+      const int p = w0 + lane;
+      const uint32_t c = p < L ? txt[p] : 0u;
+      const bool cand = c == '<' || c == '&';
+      const uint64_t m = __ballot(cand);
+      if (K + __popcll(m) > kHtmlCands) break;                 // (a window holds at most 64)
+      if (cand) S.pos[K + __popcll(m & lanemask_lt(lane))] = (uint16_t)p;
+      K += __popcll(m);
+      P1 = w0 + 64 < L ? w0 + 64 : L;
     }
-    drop_run = dm == ~0ull ? drop_run + 64 : (int)__builtin_clzll(~dm);   // dropped bytes ending the window
-    if (hp) {
-      if (text || (reached && kind == 0)) hp[at] = (uint32_t)p;
-      if (reached && kind == 1) {
-        for (int k = 0; k < plen; ++k) hp[at + k] = (uint32_t)(p + k);
-        const int tl = S.len[j];
-        if (tl - plen == 1 || plen > tl) novec = 1;
-      }
-    }
-    if (text) {
-      o[at] = (uint8_t)c;
-      f[at] = (uint8_t)(dprev ? 3 : 0);          // bit 1: the byte after a dropped '&'
-
-      // plain characters: well formed, and the same lowering in HTML mode
-      if (c < 0x80) {
-        bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
-      } else if ((c & 0xC0) == 0x80) {
-        ++conts;
+    wsync();
+    // 1b. each candidate as if the scan reached it
+    for (int j = lane; j < K; j += 64) {
+      const int p = S.pos[j];
+      int ln = 1, kind = 0, plen = 0;
+      bool bd = false;
+      uint32_t dec = 0;
+      if (txt[p] == '<') {
+        ln = 0;                                                // (a reached tag is scanned in step 2)
       } else {
-        const int m = utf8_len((uint8_t)c);
-        const uint32_t b1 = txt_at<kStaged>(txt, p + 1, L), b2 = txt_at<kStaged>(txt, p + 2, L);
-        bad |= (p + m > L || !html_lower_same(T, c, b1, b2, m)) ? 1 : 0;
-        need += m - 1;
+        uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int tlen = 0;
+        entity_to_buffer(T, dv, p, L - p, tmp, &tlen, &plen);
+        if (plen > 0) {
+          kind = 1;
+          ln = tlen;
+          dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
+          bd = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
+               (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
+        } else {
+          kind = 2;                                            // undecodable: the '&' is dropped
+          plen = 0;
+        }
       }
-    } else if (reached && kind == 0) {
-      o[at] = ' ';
-      f[at] = (uint8_t)(dprev ? 3 : 0);
-    } else if (reached && kind == 1) {
-      const uint32_t d = S.dec[j];
-      for (int k = 0; k < plen; ++k) {
-        o[at + k] = (uint8_t)(d >> (8 * k));
-        f[at + k] = k == 0 ? 1 : 0;
-      }
-      bad |= (meta & 0x20) ? 1 : 0;
+      S.len[j] = (uint16_t)ln;
+      S.dec[j] = dec;
+      S.meta[j] = (uint8_t)(kind | (plen << 2) | (bd ? 0x20 : 0));
     }
-    q = rdl(at + emit, 63);
-    const uint32_t wmx = rdlu(mx, 63);
-    cover = wmx > cover ? wmx : cover;
-    drop_prev = rdlu(dropped ? 1u : 0u, 63);
+    wsync();
+    // 2. which candidates the scan reaches: past the end of the last reached one
+    const long long t2 = prof ? (long long)clock64() : 0;
+    for (int j0 = 0; j0 < K; j0 += 64) {
+      const int j = j0 + lane;
+      const int p = j < K ? (int)S.pos[j] : 0x7FFFFFFF, ln = j < K ? (int)S.len[j] : 0;
+      const int m = K - j0 < 64 ? K - j0 : 64;
+      const uint64_t tag_m = __ballot(j < K && (S.meta[j] & 3) == 0);
+      uint64_t reach = 0;
+      for (int t = 0; t < m; ++t) {
+        const int pt = rdl(p, t);
+        if (pt >= cur) {
+          reach |= 1ull << t;
+          int lt = rdl(ln, t);
+          if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
+            lt = scan_tag_wave(tt, txt, pt, L - pt, lane);
+            if (lane == t) S.len[j] = (uint16_t)lt;
+          }
+          cur = pt + lt;
+        }
+      }
+      if (j < K) S.meta[j] = (uint8_t)(S.meta[j] | (((reach >> lane) & 1) ? 0x40 : 0));
+    }
+    wsync();
+    if (prof && lane == 0) atomicAdd(prof, (unsigned long long)((long long)clock64() - t2));
+    // 3. the output, window by window
+    int cb = 0;
+    for (int w0 = P0; w0 < P1; w0 += 64) {
+      const int p = w0 + lane;
+      const bool in = p < L;
+      const uint32_t c = in ? txt[p] : 0u;
+      const bool cand = in && (c == '<' || c == '&');
+      const uint64_t cm = __ballot(cand);
+      const int j = cand ? cb + __popcll(cm & lanemask_lt(lane)) : 0;
+      cb += __popcll(cm);
+      const uint32_t meta = cand ? S.meta[j] : 0u;
+      const bool reached = (meta & 0x40) != 0;
+      const uint32_t end = reached ? (uint32_t)(p + S.len[j]) : 0u;
+      // covered: inside a reached candidate that starts before p (the running
+      // maximum of reached ends, carried across windows and segments)
+      const uint32_t mx = dpp_scan_incl(end, 0u, OpMax());
+      const uint32_t before = wshr1(mx, 0u);
+      const uint32_t cov_end = before > cover ? before : cover;
+      const bool covered = in && !reached && (uint32_t)p < cov_end;
+      const int kind = meta & 3, plen = (meta >> 2) & 7;
+      const bool text = in && !covered && !reached;
+      int emit = 0;
+      if (reached) emit = kind == 0 ? 1 : kind == 1 ? plen : 0;
+      else if (text) emit = 1;
+      // the first byte after a dropped '&' carries the lookahead mark
+      const bool dropped = reached && kind == 2;
+      const uint32_t dprev = wshr1(dropped ? 1u : 0u, drop_prev);
+      const int at = q + excl_scan(emit, lane);
+      // vec mode (hpos): every output byte's page offset, as map2original_ maps
+      // it -- a text byte its own, a tag's space the tag start, an entity's k-th
+      // byte start + k (Copy(plen), then Delete(tlen - plen)).  An entity whose
+      // Delete is a single byte, or that grows (Insert), could merge with the
+      // run's closing Insert(1) into a Copy (offsetmap.cc:122-156): such pages
+      // keep the sequential kernel in vec mode (kSpecialNoVec).
+      // the first byte after dropped '&'s also records where they began (hpos
+      // second half, read where hflag bit 1 is set): a run ending there has its
+      // gap start at the first of them (they merge into the gap's Delete)
+      const uint64_t dm = __ballot(dropped);
+      if (hp && dprev) {
+        const uint64_t nd = ~dm & lanemask_lt(lane);             // bytes before this one that were not dropped
+        const int first = nd ? w0 + (63 - __builtin_clzll(nd)) + 1 : w0 - drop_run;
+        hg[at] = (uint32_t)first;
+      }
+      drop_run = dm == ~0ull ? drop_run + 64 : (int)__builtin_clzll(~dm);   // dropped bytes ending the window
+      if (hp) {
+        if (text || (reached && kind == 0)) hp[at] = (uint32_t)p;
+        if (reached && kind == 1) {
+          for (int k = 0; k < plen; ++k) hp[at + k] = (uint32_t)(p + k);
+          const int tl = S.len[j];
+          if (tl - plen == 1 || plen > tl) novec = 1;
+        }
+      }
+      if (text) {
+        o[at] = (uint8_t)c;
+        f[at] = (uint8_t)(dprev ? 3 : 0);          // bit 1: the byte after a dropped '&'
+
+        // plain characters: well formed, and the same lowering in HTML mode
+        if (c < 0x80) {
+          bad |= (((c < 64 ? am0 : am1) >> (c & 63)) & 1) ? 1 : 0;
+        } else if ((c & 0xC0) == 0x80) {
+          ++conts;
+        } else {
+          const int mm = utf8_len((uint8_t)c);
+          const uint32_t b1 = txt_at<kStaged>(txt, p + 1, L), b2 = txt_at<kStaged>(txt, p + 2, L);
+          bad |= (p + mm > L || !html_lower_same(T, c, b1, b2, mm)) ? 1 : 0;
+          need += mm - 1;
+        }
+      } else if (reached && kind == 0) {
+        o[at] = ' ';
+        f[at] = (uint8_t)(dprev ? 3 : 0);
+      } else if (reached && kind == 1) {
+        const uint32_t d = S.dec[j];
+        for (int k = 0; k < plen; ++k) {
+          o[at + k] = (uint8_t)(d >> (8 * k));
+          f[at + k] = k == 0 ? 1 : 0;
+        }
+        bad |= (meta & 0x20) ? 1 : 0;
+      }
+      q = rdl(at + emit, 63);
+      const uint32_t wmx = rdlu(mx, 63);
+      cover = wmx > cover ? wmx : cover;
+      drop_prev = rdlu(dropped ? 1u : 0u, 63);
+    }
+    wsync();                                                   // S.* reused by the next segment
+    P0 = P1;
   }
   // the page keeps its length: spaces after the text
   for (int p = q + lane; p < L; p += 64) {
