@@ -684,6 +684,14 @@ constexpr uint32_t kPrepFlags = CLD_FLAG_STRIP_EXTRAS | CLD_FLAG_CSTRING;
 constexpr uint32_t kCldFlags = CLD_FLAG_SCORE_AS_QUADS | CLD_FLAG_BEST_EFFORT;
 constexpr uint32_t kPublicFlags = kCldFlags | CLD_FLAG_DEBUG_MASK;
 
+// A long list this short goes whole to the fused k_long, whose two-wave
+// speculation is for small batches: 4 documents per fused wave, or
+// CLD_LONG_SMALL documents (0: the staged path for every batch).
+uint32_t small_long_list(const Device* d) {
+  static const long v = getenv("CLD_LONG_SMALL") ? atol(getenv("CLD_LONG_SMALL")) : -1;
+  return v >= 0 ? (uint32_t)v : 4u * (uint32_t)d->n_slots;
+}
+
 // Batches holding a document of this many KB go to the fused k_long whole
 // (CLD_LONG_HEAVY_KB; default 0: never).  Before span-parallel scoring a C5
 // batch's many-span 64 KB pages (~48 ms on one wave) repeated their latency
@@ -782,7 +790,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       // kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
-                               priors, hbuf, hflag, d->fault_doc, 4u * (uint32_t)d->n_slots,
+                               priors, hbuf, hflag, d->fault_doc, small_long_list(d),
                                d->long_order ? d->d_lhist : nullptr, heavy_kb(), d->d_parlists, np, gcap, s));
       list = fall;
       ctr_total = kCtrStFall;

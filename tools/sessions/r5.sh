@@ -36,7 +36,9 @@ for s in ${STEPS:-suite smoke bench}; do
         step 400 ab_${c}_fused.json env CLD_LONG_STAGED=0 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
       done ;;
     dlab) step 600 dl_ab.jsonl env DL_RATE_VARIANTS="${DLVARS:--;CLD_TINY_ZC=1;CLD_TINY=0}" DL_RATE_CFG=c2 python3 tools/dl_rate.py ;;
-    req) step 400 req_rate.jsonl env REQ_RATE_CALLERS=1,8,32,128 python3 tools/req_rate.py ;;
+    req) step 400 req_rate.jsonl env REQ_RATE_CALLERS=${REQCALLERS:-1,8,32,128} python3 tools/req_rate.py ;;
+    reqab) step 400 req_staged.jsonl env CLD_LONG_SMALL=0 REQ_RATE_CALLERS=${REQCALLERS:-1,8,32} python3 tools/req_rate.py
+           step 400 req_fused.jsonl env REQ_RATE_CALLERS=${REQCALLERS:-1,8,32} python3 tools/req_rate.py ;;
     rates)
       step 300 html_rate.json python3 tools/html_rate.py
       step 400 vec_rate.jsonl python3 tools/vec_rate.py ;;
