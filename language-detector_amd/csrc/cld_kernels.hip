@@ -477,13 +477,9 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
   uint32_t heavy = 0;
   if (hist && heavy_kb && lane < kLenBuckets - (int)heavy_kb) heavy = hist[lane];   // buckets of (L >> 10) >= heavy_kb
   heavy = wave::wsum(heavy);
-  if (total <= small_total || heavy) {           // the fused kernel takes it all, in list order
-    if (blockIdx.x == 0) {
-      for (uint32_t k = threadIdx.x; k < total; k += blockDim.x) fall_list[k] = list[k];
-      if (threadIdx.x == 0) counters[kCtrStFall] = total;
-    }
-    return;
-  }
+  // the fused kernel takes the batch, in list order (documents over kDocCap,
+  // which it does not take, still come here)
+  const bool fused = total <= small_total || heavy;
   const bool exact = lng::space_lowers_to_space(T);
   const uint64_t units = pool_bytes >> 4;
   for (;;) {
@@ -491,12 +487,25 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     if (k >= total) break;                       // every wave reaches this exit
     const uint32_t i = list[k];
     const uint64_t a = offs[i], L = offs[i + 1] - a;
+    if (fused && L <= (uint64_t)(lng::kDocCap - 64)) {
+      if (lane == 0) fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
+      continue;
+    }
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const bool rw = (spi & kSpecialRewritten) != 0;
     uint64_t at = lng::kStNone;
     if (exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc) {
       const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
       at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane);
+    } else if (exact && L <= lng::kStBigMax && i != fault_doc) {   // over kDocCap: a worst-case region
+      const uint64_t u = (lng::st_big_bytes(L) + 15) >> 4;
+      uint32_t got = 0;
+      if (lane == 0) got = atomicAdd(&counters[kCtrStPool], (uint32_t)u);
+      got = wave::uflu(__shfl((int)got, 0, 64));
+      if ((uint64_t)got + u <= units) {
+        const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
+        if (lng::st_spans_big(T, dv, S, pool + ((uint64_t)got << 4), lane)) at = (uint64_t)got << 4;
+      }
     }
     // a span-parallel document (more than kParMin spans): its groups to the group list
     uint32_t ng = 0, gb = 0;

@@ -567,7 +567,9 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // letter-stop bitmap (one bit per byte) the span builder searches for span
 // starts.  False if the document does not tile into characters with local
 // scanner behaviour (then k_general redoes it).
-__device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane) {
+__device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane,
+                                         uint64_t* lsm_ext = nullptr) {
+  uint64_t* const lsm = lsm_ext ? lsm_ext : S.lsm;   // (documents over kDocCap: a bitmap in the staged store)
   lane = wave::lane_here();
   const int L = dv.len;
   int bad = 0, conts = 0, need = 0;
@@ -598,7 +600,7 @@ __device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, 
     e = en;
     i2 = j2;
     const uint64_t m = __ballot((cw >> 20) & 1);
-    if (lane == 0) S.lsm[w] = m;
+    if (lane == 0) lsm[w] = m;
     cut |= __ballot(cls_cut(cw)) != 0;
   }
   bad |= (wsum(conts) != wsum(need)) ? 1 : 0;
@@ -650,14 +652,15 @@ __device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
 template <bool VEC = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane, uint32_t* omap = nullptr, const uint32_t* hpos = nullptr,
-                         const uint32_t* hgap = nullptr) {
+                         const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr) {
+  const uint64_t* const lsm = lsm_ext ? lsm_ext : S.lsm;
   lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
   const int remaining = L - next;
   int soft = kMaxScriptBytes - kWithinScriptTail;
   if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) soft = remaining / 2;
-  const int q = find_first_g(S.lsm, next, L);
+  const int q = find_first_g(lsm, next, L);
   status = 1;
   if (q >= L) {
     next = L;
@@ -785,7 +788,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         // the gap; a gap of one byte makes that a Copy(1) of the gap byte, no
         // gap an Insert at the run end (:955-993)
         const int fr = sep ? x : x + n;
-        const int nl = orig(next_stop(S.lsm, fr, L));
+        const int nl = orig(next_stop(lsm, fr, L));
         int from = orig(fr);
         // dropped '&'s just before the break (hflag bit 1 on the byte after
         // them) are deleted in the letter loop, and that Delete merges with
@@ -811,8 +814,8 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
     if (stop < 64) {
       const int xs = (w << 6) + stop;
-      if ((Hm >> stop) & 1) nxt = find_first_g(S.lsm, xs + rdl(n, stop), L);
-      else if ((Sm >> stop) & 1) nxt = find_first_g(S.lsm, xs, L);   // the gap scan starts at the break char
+      if ((Hm >> stop) & 1) nxt = find_first_g(lsm, xs + rdl(n, stop), L);
+      else if ((Sm >> stop) & 1) nxt = find_first_g(lsm, xs, L);   // the gap scan starts at the break char
       else {
         nxt = xs;                                                     // another script's letter stop
         // vec mode: dropped '&'s right before it may stop the reference's scan
@@ -2830,6 +2833,62 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   }
   gsync();
   return (uint64_t)got << 4;
+}
+
+// Documents over kDocCap (round 5; they used to take the sequential kernel):
+// the span cache and the slot's letter-stop bitmap hold at most 512 KB of
+// spans and 1 MB of text, so the region is reserved at its worst case and
+// written directly -- the spans (at most 4 lowered bytes per raw byte plus
+// 128 bytes per span), the span table and the span-parallel arrays at fixed
+// places, then the bitmap -- the same layout the other kernels read.
+constexpr uint64_t kStBigMax = 64ull << 20;      // longest document taken here
+__device__ __forceinline__ uint64_t st_big_text(uint64_t L) { return 4 * L + 128ull * kMaxSpans; }
+__device__ __forceinline__ uint64_t st_big_bytes(uint64_t L) {
+  const uint64_t tc = st_big_text(L);
+  return sizeof(StHdr) + tc + 8ull * kMaxSpans + 4ull * (2 * kMaxSpans + 1) + 8 + 8 * (tc / 16 + 8ull * kMaxSpans) +
+         8 * (L / 64 + 2) + 64;
+}
+__device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& dv, Slot& S, uint8_t* region,
+                                             int lane) {
+  const uint64_t L = (uint64_t)dv.len, tc = st_big_text(L), tab_off = sizeof(StHdr) + tc;
+  const uint64_t par_off = tab_off + 8ull * kMaxSpans;
+  uint64_t* lsm = reinterpret_cast<uint64_t*>(region + ((st_big_bytes(L) - 8 * (L / 64 + 2) - 64) & ~7ull));
+  bool careful;
+  if (!classify(T, dv, S, careful, lane, lsm)) return false;
+  uint64_t* tab = reinterpret_cast<uint64_t*>(region + tab_off);
+  int next = 0, nsp = 0;
+  uint64_t cur = sizeof(StHdr);
+  for (;;) {
+    if (cur + 4ull * (L - (uint64_t)next) + 128 > sizeof(StHdr) + tc || nsp >= kMaxSpans) return false;
+    int ul = 0, st = 0;
+    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm);
+    if (st == 0) break;
+    if (st < 0) return false;
+    if (tb > 2048 && squeeze_trigger(S, region + cur, careful, lane)) return false;   // the Squeeze restart
+    if (lane == 0) tab[nsp] = cur | ((uint64_t)(uint32_t)tb << 32) | ((uint64_t)(uint32_t)ul << 56);
+    ++nsp;
+    cur += (uint64_t)st_advance(tb);
+  }
+  gsync();
+  uint32_t par = 0;
+  if (nsp > kParMin) {
+    par = (uint32_t)par_off;
+    if (lane == 0) {
+      uint32_t* roff = reinterpret_cast<uint32_t*>(region + par);
+      uint32_t acc = 0;
+      for (int j = 0; j < nsp; ++j) {
+        roff[j] = acc;
+        acc += (uint32_t)(((tab[j] >> 32) & 0xFFFFFF) / 16 + 8);
+      }
+      roff[nsp] = acc;
+    }
+  }
+  if (lane == 0) {
+    StHdr h{(uint32_t)nsp, careful ? 1u : 0u, (uint32_t)tab_off, par};
+    *reinterpret_cast<StHdr*>(region) = h;
+  }
+  gsync();
+  return true;
 }
 
 // One pass over a document's stored spans: detect()'s span loop (scoring

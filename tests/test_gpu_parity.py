@@ -266,3 +266,30 @@ def test_staged_long_path_and_its_hand_ons(gpu, oracle):
     r = subprocess.run([sys.executable, "-c", STAGED], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "staged ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
     assert len(got) == len(docs)
+
+
+def test_documents_over_one_megabyte(gpu, oracle):
+    """Documents between 1 and 4 MB (over k_long's kDocCap): the staged path
+    writes their spans straight into a worst-case region of its store with the
+    letter-stop bitmap there too (cld_long.hip st_spans_big), in a small batch
+    and in a large one -- equal to the oracle, none on the sequential kernel."""
+    rng = np.random.default_rng(181)
+    b3, o3 = corpus.c3(260, seed=182)
+    b2, o2 = corpus.c2(40000, seed=183)
+    big = []
+    for k in range(20):
+        size = int(rng.integers(1_100_000, 4_000_000))
+        if k % 2:
+            d = bytes(b3[:size])                                  # four-script pages back to back
+        else:
+            d = bytes(b2[o2[0]:o2[-1]])[:size]                    # tweets run together
+        big.append(d)
+    buf, offs = gpu.pack(big)
+    check(gpu, oracle, buf, offs, "over 1 MB", threads=16)
+    st = gpu.last_stats(0)
+    assert st.general_docs == 0, list(st.long_requeue)
+    # in a batch large enough for the staged path proper
+    docs = [bytes(b2[o2[i]:o2[i + 40]]) for i in range(0, 20000 * 40 // 40, 1)][:20000] + big[:4]
+    buf, offs = gpu.pack(docs)
+    check(gpu, oracle, buf, offs, "over 1 MB, large batch", threads=16)
+    assert gpu.last_stats(0).general_docs == 0
