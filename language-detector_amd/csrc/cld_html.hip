@@ -21,9 +21,12 @@
 //     positions in hflag, and the span builders read script 0 there;
 //   * the lowercaser's HTML half: a page holding a character whose HTML-mode
 //     lowering differs (kCptHtmlLower), a 4-byte or malformed character, or
-//     more than kHtmlRewriteMax bytes is not rewritten and stays on k_general.  (The span soft limit reads the raw
-//     bytes left, :815-819; it splits nothing below kMaxScriptBytes, ~40 KB,
-//     so up to 32 KB raw and rewritten pages cut their spans alike.)
+//     more than kHtmlRewriteMax bytes is not rewritten and stays on k_general;
+//   * the span soft limit reads the raw bytes left (:814-819); it splits
+//     nothing below kMaxScriptBytes (40,928), and for longer pages the rewrite
+//     also records each output byte's page offset (hpos, with hgap after
+//     dropped '&'s), from which the span builders read it (cld_long.hip
+//     next_span).
 // A rewritten page that k_wave / k_long re-queue goes to k_general, which
 // scores the original page in HTML mode.
 //
@@ -53,7 +56,7 @@ using wave::wshr1;
 using wave::wsum;
 using wave::wsync;
 
-constexpr int kHtmlRewriteMax = 32768;  // larger pages stay on k_general (the span soft limit, above)
+constexpr int kHtmlRewriteMax = 64 << 20;  // (lng::kStBigMax) larger pages stay on k_general
 constexpr int kHtmlStage = 8192;        // pages up to this size are staged in LDS, larger ones read in place
 constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per segment of a page (round 5: any number per page)
 constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
@@ -115,8 +118,8 @@ __device__ __forceinline__ int scan_tag_wave(const TagTables& tt, const uint8_t*
 
 struct HtmlSmem {
   uint8_t text[kHtmlStage + 16];       // the page (up to kHtmlStage bytes)
-  uint16_t pos[kHtmlCands];            // candidate positions, in page order
-  uint16_t len[kHtmlCands];            // bytes the scan consumes there
+  uint32_t pos[kHtmlCands];            // candidate positions, in page order
+  uint32_t len[kHtmlCands];            // bytes the scan consumes there
   uint32_t dec[kHtmlCands];            // an entity's decoded bytes
   uint8_t meta[kHtmlCands];            // kind (0 tag, 1 entity, 2 dropped '&') | plen << 2 | bad << 5 | reached << 6
 };
@@ -136,7 +139,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
                                              const uint8_t sp, uint8_t* __restrict__ special,
                                              uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
                                              uint32_t* __restrict__ hpos, uint32_t* __restrict__ hgap,
-                                             unsigned long long* __restrict__ prof, const uint64_t am0,
+                                             const int hpos_min, unsigned long long* __restrict__ prof, const uint64_t am0,
                                              const uint64_t am1, const int lane) {
   const DocView dv{txt, L};
   // The page in segments of whole 64-byte windows holding at most kHtmlCands
@@ -146,8 +149,8 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
   // the candidates it covers there, `cover` the text bytes.
   uint8_t* o = hbuf + a;
   uint8_t* f = hflag + a;
-  uint32_t* hp = hpos ? hpos + a : nullptr;
-  uint32_t* hg = hpos ? hgap + a : nullptr;
+  uint32_t* hp = hpos && L >= hpos_min ? hpos + a : nullptr;
+  uint32_t* hg = hp ? hgap + a : nullptr;
   int q = 0, bad = 0, conts = 0, need = 0, novec = 0;
   int drop_run = 0;                                            // dropped '&'s ending the previous window
   uint32_t cover = 0;                                          // end of the last reached candidate so far
@@ -162,7 +165,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
       const bool cand = c == '<' || c == '&';
       const uint64_t m = __ballot(cand);
       if (K + __popcll(m) > kHtmlCands) break;                 // (a window holds at most 64)
-      if (cand) S.pos[K + __popcll(m & lanemask_lt(lane))] = (uint16_t)p;
+      if (cand) S.pos[K + __popcll(m & lanemask_lt(lane))] = (uint32_t)p;
       K += __popcll(m);
       P1 = w0 + 64 < L ? w0 + 64 : L;
     }
@@ -190,7 +193,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
           plen = 0;
         }
       }
-      S.len[j] = (uint16_t)ln;
+      S.len[j] = (uint32_t)ln;
       S.dec[j] = dec;
       S.meta[j] = (uint8_t)(kind | (plen << 2) | (bd ? 0x20 : 0));
     }
@@ -210,7 +213,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
           int lt = rdl(ln, t);
           if ((tag_m >> t) & 1) {                    // a reached tag: ScanToPossibleLetter, by the wave
             lt = scan_tag_wave(tt, txt, pt, L - pt, lane);
-            if (lane == t) S.len[j] = (uint16_t)lt;
+            if (lane == t) S.len[j] = (uint32_t)lt;
           }
           cur = pt + lt;
         }
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
                                                                uint8_t* __restrict__ special,
                                                                uint8_t* __restrict__ hbuf, uint8_t* __restrict__ hflag,
                                                                uint32_t* __restrict__ hpos, uint32_t* __restrict__ hgap,
-                                                               unsigned long long* __restrict__ prof) {
+                                                               int hpos_min, unsigned long long* __restrict__ prof) {
   __shared__ HtmlSmem smem[kHtmlWPB];
   __shared__ TagTables tt;
   for (int t = threadIdx.x; t < 256 + kTagStates * kTagClasses; t += blockDim.x) {
@@ -346,7 +349,8 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
     if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: k_general
     const int L = (int)len64;
     if (L > kHtmlStage) {
-      rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, hpos, hgap, prof, am0, am1, lane);
+      rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, hpos, hgap, hpos_min, prof, am0, am1,
+                          lane);
     } else {
       // the page into LDS (from aligned dwords), NUL padded
       const uint8_t* g = buf + a;
@@ -357,7 +361,8 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
         *reinterpret_cast<uint32_t*>(&S.text[p]) = v;
       }
       wsync();
-      rewrite_page<true>(T, tt, S, S.text, L, a, i, sp, special, hbuf, hflag, hpos, hgap, prof, am0, am1, lane);
+      rewrite_page<true>(T, tt, S, S.text, L, a, i, sp, special, hbuf, hflag, hpos, hgap, hpos_min, prof, am0, am1,
+                         lane);
     }
     wsync();
   }

@@ -84,17 +84,22 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
 // requeue_list == nullptr (counters unused), marked in their result:
 // summary_lang = kWaveRequeued.
 constexpr uint16_t kWaveRequeued = 0xFFFE;
+// kMaxScriptBytes (cld_pipeline.hip): rewritten HTML pages this long and
+// longer carry page offsets (hpos / hgap) for the span soft limit
+constexpr int kHtmlSoftMin = 40928;
 hipError_t cld_launch_wave_only(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n, cld_result* out,
                                 uint32_t* requeue_list, uint32_t* counters, uint32_t cflags, hipStream_t s);
 // HTML documents of the batch (special & kSpecialHtml) rewritten into plain
 // text (cld_html.hip): hbuf / hflag are indexed like buf (offs); special is
 // updated in place (kSpecialHtml -> kSpecialRewritten for each rewritten page);
 // prof (nullable, CLD_PROFILE_STAGES=1): cycles of step 2 summed into prof[0].
-// hpos (nullable, vec mode): per rewritten byte, its page offset for MapBack;
-// hgap (with hpos): at a byte that follows dropped '&'s, where they began.
+// hpos (nullable): per rewritten byte, its page offset (vec mode's MapBack;
+// the span soft limit of pages of kMaxScriptBytes and more); hgap (with hpos):
+// at a byte that follows dropped '&'s, where they began.  Written for pages of
+// hpos_min bytes and more (vec mode 0, plain kMaxScriptBytes).
 hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                    uint8_t* special, uint8_t* hbuf, uint8_t* hflag, uint32_t* hpos, uint32_t* hgap,
-                                   unsigned long long* prof, hipStream_t s);
+                                   int hpos_min, unsigned long long* prof, hipStream_t s);
 size_t cld_wave_smem_bytes();
 hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
                               const uint32_t* list, cld_result* out, uint8_t* arena,
@@ -129,8 +134,9 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           cld_result* spec_out, uint32_t* spec_take, int ctr_total, int ctr_deq, hipStream_t s);
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
+                           const uint32_t* hgap, uint32_t fault_doc, cld_result* spec_out, uint32_t* spec_take,
+                           int ctr_total, int ctr_deq, hipStream_t s);
 // spec_out / spec_take (nullable: no speculation): cld_long_spec_docs(n_slots)
 // results and u32 entries, k_long's speculative pass-2 results for the
 // longest documents of a small batch.
@@ -153,8 +159,8 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
-                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, const uint32_t* hist, uint32_t heavy_kb, uint32_t* par_lists,
-                             size_t n, size_t gcap, hipStream_t s);
+                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
+                             const uint32_t* hgap, uint32_t fault_doc, uint32_t small_total, const uint32_t* hist,
+                             uint32_t heavy_kb, uint32_t* par_lists, size_t n, size_t gcap, hipStream_t s);
 }
 #endif

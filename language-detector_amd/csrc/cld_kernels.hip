@@ -18,6 +18,8 @@
 #include "cld_long.hip"
 #include "cld_html.hip"
 
+static_assert(kHtmlSoftMin == cld::kMaxScriptBytes, "kHtmlSoftMin is kMaxScriptBytes");
+
 #ifndef GEN_LANES_PER_WAVE
 // k_general / k_general_vec: documents per wavefront.  One per wave: the
 // sequential per-document code then never diverges between documents in a
@@ -351,6 +353,11 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     wave::wsync();
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const bool rw = (spi & kSpecialRewritten) != 0;   // a rewritten HTML page (cld_html.hip)
+    // its byte -> page offset maps, for the span soft limit of pages of
+    // kMaxScriptBytes and more (cld_html.hip writes them for those)
+    const bool hbig = rw && hpos && len >= (uint64_t)kMaxScriptBytes;
+    const uint32_t* hp = hbig ? hpos + a : nullptr;
+    const uint32_t* hg = hbig ? hgap + a : nullptr;
     if constexpr (VEC) {
       // ResultChunkVector mode (cld_detect_batch_vec): the vector goes to the
       // document's pool region; a vector that outgrows it reports -1 (the host
@@ -370,14 +377,14 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
       if (exact && len <= (uint64_t)lng::kDocCap)
         passes = lng::detect<DIAG, true>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i,
                                          cflags, (spi & kSpecialPriors) ? priors + 16ull * i : nullptr,
-                                         rw ? hflag + a : nullptr, &V);
+                                         rw ? hflag + a : nullptr, &V, lng::kPassesAll, hp, hg);
       if (lane == 0 && passes >= 1 && passes <= 3) n_chunks[i] = V.over ? -1 : V.n;
     } else {
       cld_result* o = mode == lng::kPassRepeatsOnly ? spec_out + k : &out[i];
       if (exact && len <= (uint64_t)lng::kDocCap)
         passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, o, tr, i, cflags,
                                    (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr,
-                                   nullptr, mode);
+                                   nullptr, mode, hp, hg);
     }
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
@@ -460,8 +467,9 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
     uint64_t* __restrict__ meta, uint32_t* __restrict__ ok_list, uint32_t* __restrict__ fall_list,
     uint32_t* __restrict__ counters, const uint8_t* __restrict__ special, const uint8_t* __restrict__ hbuf,
-    const uint8_t* __restrict__ hflag, uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist,
-    uint32_t* __restrict__ par_list, uint64_t* __restrict__ group_list, uint32_t gcap, uint32_t heavy_kb) {
+    const uint8_t* __restrict__ hflag, const uint32_t* __restrict__ hpos, const uint32_t* __restrict__ hgap,
+    uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist, uint32_t* __restrict__ par_list,
+    uint64_t* __restrict__ group_list, uint32_t gcap, uint32_t heavy_kb) {
   const DevTables& T = *Tp;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
@@ -493,9 +501,12 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     }
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const bool rw = (spi & kSpecialRewritten) != 0;
+    const bool hbig = rw && hpos && L >= (uint64_t)kMaxScriptBytes;   // (the soft limit's page offsets)
+    const uint32_t* hp = hbig ? hpos + a : nullptr;
+    const uint32_t* hg = hbig ? hgap + a : nullptr;
     uint64_t at = lng::kStNone;
     if (exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc) {
-      const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
+      const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr, hp, hg};
       at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane);
     } else if (exact && L <= lng::kStBigMax && i != fault_doc) {   // over kDocCap: a worst-case region
       const uint64_t u = (lng::st_big_bytes(L) + 15) >> 4;
@@ -503,7 +514,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
       if (lane == 0) got = atomicAdd(&counters[kCtrStPool], (uint32_t)u);
       got = wave::uflu(__shfl((int)got, 0, 64));
       if ((uint64_t)got + u <= units) {
-        const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr};
+        const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr, hp, hg};
         if (lng::st_spans_big(T, dv, S, pool + ((uint64_t)got << 4), lane)) at = (uint64_t)got << 4;
       }
     }
@@ -830,8 +841,9 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
-                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                           cld_result* spec_out, uint32_t* spec_take, int ctr_total, int ctr_deq, hipStream_t s) {
+                           const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
+                           const uint32_t* hgap, uint32_t fault_doc, cld_result* spec_out, uint32_t* spec_take,
+                           int ctr_total, int ctr_deq, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
@@ -839,12 +851,12 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   if (trace || dbg || prof)
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take, ctr_total,
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
   else
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
-                       fault_doc, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, spec_out, spec_take, ctr_total,
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
   return hipGetLastError();
 }
@@ -859,8 +871,9 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
                              uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
-                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, uint32_t fault_doc,
-                             uint32_t small_total, const uint32_t* hist, uint32_t heavy_kb, uint32_t* par_lists,
+                             const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
+                             const uint32_t* hgap, uint32_t fault_doc, uint32_t small_total, const uint32_t* hist,
+                             uint32_t heavy_kb, uint32_t* par_lists,
                              size_t n, size_t gcap, hipStream_t s) {
   // n_waves: the slots (resident waves) of the widest launch below
   const int per_simd = cld_staged_waves_per_simd();
@@ -871,8 +884,8 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
   uint64_t* gl2 = gl1 + gcap;
   const uint32_t gc = (uint32_t)gcap, nn = (uint32_t)n;
   hipLaunchKernelGGL(cld::k_lspan, gsp, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
-                     fall_list, counters, special, hbuf, hflag, fault_doc, small_total, hist, par_lists, gl1, gc,
-                     heavy_kb);
+                     fall_list, counters, special, hbuf, hflag, hpos, hgap, fault_doc, small_total, hist, par_lists,
+                     gl1, gc, heavy_kb);
   hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
                      fall_list, counters, cflags, special, priors);
   hipLaunchKernelGGL(cld::k_lgroup<false>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl1, gc, counters, cflags,
@@ -967,11 +980,11 @@ hipError_t cld_launch_wave_only(const DevTables* T, const uint8_t* buf, const ui
 
 hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
                                    uint8_t* special, uint8_t* hbuf, uint8_t* hflag, uint32_t* hpos, uint32_t* hgap,
-                                   unsigned long long* prof, hipStream_t s) {
+                                   int hpos_min, unsigned long long* prof, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int blocks = std::min((n + cld::kHtmlWPB - 1) / cld::kHtmlWPB, 2048);   // persistent: pages by stride
   hipLaunchKernelGGL(cld::k_html_rewrite, dim3(blocks), dim3(64 * cld::kHtmlWPB), 0, s, d_T, buf, offs, n, special,
-                     hbuf, hflag, hpos, hgap, prof);
+                     hbuf, hflag, hpos, hgap, hpos_min, prof);
   return hipGetLastError();
 }
 

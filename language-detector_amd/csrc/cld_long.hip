@@ -657,9 +657,28 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
-  const int remaining = L - next;
-  int soft = kMaxScriptBytes - kWithinScriptTail;
-  if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) soft = remaining / 2;
+  // the soft limit (getonescriptspan.cc:814-819) from the raw bytes left: on
+  // a rewritten page the page offset of the resume point.  After dropped
+  // '&'s (hflag bit 1) the reference may resume at the first of them (a
+  // stale script, see the letter stop below): a document whose soft limit
+  // differs between the two, or whose two sit in different regimes, is
+  // re-queued (k_general scores the page itself).
+  auto soft_of = [](int r) {
+    return (kMaxScriptBytes <= r && r < 2 * kMaxScriptBytes) ? r / 2 : kMaxScriptBytes - kWithinScriptTail;
+  };
+  auto regime = [](int r) { return r < kMaxScriptBytes ? 0 : r < 2 * kMaxScriptBytes ? 1 : 2; };
+  int remaining = L - next;
+  if (dv.hp && next > 0 && next < L) {
+    remaining = L - (int)gld(dv.hp + next);
+    if (gld(dv.hf + next) & 2) {
+      const int r0 = L - (int)gld(dv.hg + next);
+      if (soft_of(r0) != soft_of(remaining) || regime(r0) != regime(remaining)) {
+        status = -1;
+        return 0;
+      }
+    }
+  }
+  const int soft = soft_of(remaining);
   const int q = find_first_g(lsm, next, L);
   status = 1;
   if (q >= L) {
@@ -2548,7 +2567,7 @@ template <bool D, bool VEC = false>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
                       const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf, VecState* V = nullptr,
-                      int mode = kPassesAll) {
+                      int mode = kPassesAll, const uint32_t* hp = nullptr, const uint32_t* hg = nullptr) {
   const int unk = (int)T.unknown_lang;
   // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
   if (lane == 0) s.has_pri = pri != nullptr;
@@ -2568,7 +2587,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
     return 1;
   }
   if (L > kDocCap - 64) return -kWhyLength;
-  const DocView dv{g, L, hf};
+  const DocView dv{g, L, hf, hp, hg};
   if constexpr (D) trace(tr, lane, doc, 1, L);
   long long t = (D && s.prof) ? (long long)clock64() : 0;
 
@@ -2840,18 +2859,20 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
 // spans and 1 MB of text, so the region is reserved at its worst case and
 // written directly -- the spans (at most 4 lowered bytes per raw byte plus
 // 128 bytes per span), the span table and the span-parallel arrays at fixed
-// places, then the bitmap -- the same layout the other kernels read.
+// places, then the bitmap -- the same layout the other kernels read.  Spans:
+// up to one per 16 raw bytes (tweets run together make one per ~100 bytes;
+// more, and the fused kernel hands the document on).
 constexpr uint64_t kStBigMax = 64ull << 20;      // longest document taken here
-__device__ __forceinline__ uint64_t st_big_text(uint64_t L) { return 4 * L + 128ull * kMaxSpans; }
+__device__ __forceinline__ uint64_t st_big_spans(uint64_t L) { return L / 16 > kMaxSpans ? L / 16 : kMaxSpans; }
+__device__ __forceinline__ uint64_t st_big_text(uint64_t L) { return 4 * L + 128ull * st_big_spans(L); }
 __device__ __forceinline__ uint64_t st_big_bytes(uint64_t L) {
-  const uint64_t tc = st_big_text(L);
-  return sizeof(StHdr) + tc + 8ull * kMaxSpans + 4ull * (2 * kMaxSpans + 1) + 8 + 8 * (tc / 16 + 8ull * kMaxSpans) +
-         8 * (L / 64 + 2) + 64;
+  const uint64_t tc = st_big_text(L), ns = st_big_spans(L);
+  return sizeof(StHdr) + tc + 8ull * ns + 4ull * (2 * ns + 1) + 8 + 8 * (tc / 16 + 8ull * ns) + 8 * (L / 64 + 2) + 64;
 }
 __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& dv, Slot& S, uint8_t* region,
                                              int lane) {
-  const uint64_t L = (uint64_t)dv.len, tc = st_big_text(L), tab_off = sizeof(StHdr) + tc;
-  const uint64_t par_off = tab_off + 8ull * kMaxSpans;
+  const uint64_t L = (uint64_t)dv.len, tc = st_big_text(L), tab_off = sizeof(StHdr) + tc, ns = st_big_spans(L);
+  const uint64_t par_off = tab_off + 8ull * ns;
   uint64_t* lsm = reinterpret_cast<uint64_t*>(region + ((st_big_bytes(L) - 8 * (L / 64 + 2) - 64) & ~7ull));
   bool careful;
   if (!classify(T, dv, S, careful, lane, lsm)) return false;
@@ -2859,7 +2880,7 @@ __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& 
   int next = 0, nsp = 0;
   uint64_t cur = sizeof(StHdr);
   for (;;) {
-    if (cur + 4ull * (L - (uint64_t)next) + 128 > sizeof(StHdr) + tc || nsp >= kMaxSpans) return false;
+    if (cur + 4ull * (L - (uint64_t)next) + 128 > sizeof(StHdr) + tc || (uint64_t)nsp >= ns) return false;
     int ul = 0, st = 0;
     const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm);
     if (st == 0) break;

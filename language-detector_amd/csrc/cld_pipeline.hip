@@ -72,6 +72,11 @@ struct DocView {
   // where the original had an entity's '&': a script lookahead landing there
   // sees that '&' (script 0), not the decoded character
   const uint8_t* hf = nullptr;
+  // (rewritten pages of kMaxScriptBytes and more) each byte's page offset and,
+  // after dropped '&'s, where they began (cld_html.hip hpos / hgap): the span
+  // soft limit reads the page's raw bytes left (getonescriptspan.cc:814-819)
+  const uint32_t* hp = nullptr;
+  const uint32_t* hg = nullptr;
   __device__ __forceinline__ uint8_t at(int i) const { return (unsigned)i < (unsigned)len ? p[i] : 0; }
 };
 

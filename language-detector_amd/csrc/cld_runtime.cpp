@@ -729,10 +729,18 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
             uint64_t html_base = 0, uint64_t html_bytes = 0, uint32_t* ctr = nullptr) {
   cflags &= kCldFlags;
   const uint8_t *hbuf = nullptr, *hflag = nullptr;
+  uint32_t *hpos = nullptr, *hgap = nullptr;
   if (special && html_bytes) {
     if (grow(&d->d_hbuf, &d->hbuf_cap, html_bytes) || grow(&d->d_hflag, &d->hflag_cap, html_bytes)) return CLD_ENOMEM;
     hbuf = d->d_hbuf - html_base;
     hflag = d->d_hflag - html_base;
+    // pages of kMaxScriptBytes and more also get each rewritten byte's page
+    // offset: their span soft limit reads the raw bytes left
+    if (html_bytes >= (uint64_t)kHtmlSoftMin) {
+      if (grow(&d->d_hpos, &d->hpos_cap, 2 * html_bytes)) return CLD_ENOMEM;
+      hpos = d->d_hpos - html_base;
+      hgap = d->d_hpos + html_bytes - html_base;
+    }
   }
   if (grow(&d->d_requeue, &d->requeue_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
   if (grow(&d->d_requeue2, &d->requeue2_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
@@ -758,7 +766,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
   HIP_OK(hipEventRecord(ev[0], s));
   if (hbuf)
     HIP_OK(cld_launch_html_rewrite(d->d_T, buf, offs, (int)n, const_cast<uint8_t*>(special), const_cast<uint8_t*>(hbuf),
-                                   const_cast<uint8_t*>(hflag), nullptr, nullptr, d->d_prof ? d->d_prof + 7 : nullptr, s));
+                                   const_cast<uint8_t*>(hflag), hpos, hgap, kHtmlSoftMin,
+                                   d->d_prof ? d->d_prof + 7 : nullptr, s));
   // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
   uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
   const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
@@ -790,7 +799,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       // kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
-                               priors, hbuf, hflag, d->fault_doc, small_long_list(d),
+                               priors, hbuf, hflag, hpos, hgap, d->fault_doc, small_long_list(d),
                                d->long_order ? d->d_lhist : nullptr, heavy_kb(), d->d_parlists, np, gcap, s));
       list = fall;
       ctr_total = kCtrStFall;
@@ -798,7 +807,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     }
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
                            ctr, d->h_trace, d->d_dbg, d->dbg_doc,
-                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, d->fault_doc,
+                           d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, hpos, hgap,
+                           d->fault_doc,
                            d->d_spec_out, d->d_spec_take, ctr_total, ctr_deq, s));
     HIP_OK(hipEventRecord(ev[2], s));
     HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
@@ -1494,7 +1504,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
         hgz = d->d_hpos + std::max<size_t>(bytes, 1) - base;
         HIP_OK(cld_launch_html_rewrite(d->d_T, V.in - base, V.offs, (int)m, V.sp, const_cast<uint8_t*>(hb),
                                        const_cast<uint8_t*>(hf), const_cast<uint32_t*>(hpz),
-                                       const_cast<uint32_t*>(hgz), nullptr, s));
+                                       const_cast<uint32_t*>(hgz), 0, nullptr, s));
       }
       HIP_OK(cld_launch_route_vec((int)m, sp ? V.sp : nullptr, d->d_counters, d->d_requeue, d->d_requeue2, s));
       HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, false, s));

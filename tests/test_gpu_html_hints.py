@@ -81,8 +81,8 @@ def test_html_rewrite_lookahead_edges(gpu, oracle):
     """The rewrite's exactness edges: a script lookahead from a letter of
     another script onto an entity (decoded to a letter of either script, or
     undecodable and dropped), entities next to tags, runs broken by decoded
-    non-letters, characters the HTML lowercaser treats differently, and pages
-    longer than the rewrite takes (kHtmlRewriteMax)."""
+    non-letters, characters the HTML lowercaser treats differently, and a
+    page past kMaxScriptBytes (its soft limit from page offsets)."""
     parts = ["abc\u03b1&eacute;def", "abc\u03b1&#945;def", "abc\u03b1&#1044;def", "abc\u03b1&bogus;def",
              "abc\u03b1&amp;def", "abc\u03b1&xyz def", "\u0434\u043e\u043c&#x434;\u043c", "\u03b1&&eacute;b",
              "x&lt;b&gt;y", "caf&eacute;<b>cr&egrave;me</b>", "na&iuml;ve&nbsp;text", "&#12354;&#12356;\u3042",
@@ -99,7 +99,7 @@ def test_html_rewrite_lookahead_edges(gpu, oracle):
         words += [filler[int(rng.integers(0, len(filler)))] for _ in range(int(rng.integers(0, 60)))]
         rng.shuffle(words)
         docs.append(" ".join(words).encode())
-    docs.append(("<p>" + "caf&eacute; " * 4000 + "</p>").encode())        # > kHtmlRewriteMax: stays on k_general
+    docs.append(("<p>" + "caf&eacute; " * 4000 + "</p>").encode())        # 56 KB: the soft limit from page offsets
     buf, offs = gpu.pack(docs)
     n = len(docs)
     got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
@@ -112,9 +112,10 @@ def test_html_rewrite_lookahead_edges(gpu, oracle):
 
 def test_html_rewrite_large_pages(gpu, oracle):
     """Pages past the LDS stage (kHtmlStage, 8 KB) are rewritten in place in
-    HBM up to kHtmlRewriteMax (32 KB), with any number of '<' / '&' bytes
-    (segments of kHtmlCands candidates, round 5); more than 32 KB keeps the
-    sequential kernel."""
+    HBM, with any number of '<' / '&' bytes (segments of kHtmlCands
+    candidates, round 5); pages of kMaxScriptBytes (40,928) and more carry
+    each rewritten byte's page offset, from which the span builders take the
+    soft limit's raw bytes left -- none takes the sequential kernel."""
     parts = ["abcα&eacute;def", "дом&#x434;м", "x&lt;b&gt;y", "caf&eacute;<b>cr&egrave;me</b>",
              "na&iuml;ve&nbsp;text", "&#12354;&#12356;あ", "<a <b>text</b> more", "<!-- c -->d&#101;f",
              "le chat noir mange la souris grise"]
@@ -123,13 +124,13 @@ def test_html_rewrite_large_pages(gpu, oracle):
             (" ".join(parts) + " ").encode() * 45,                                                  # 8.6 KB, 765 candidates
             ("<script>var x = '<p>';</script>" + "der Hund lief die Strasse entlang " * 400).encode(),  # 14 KB, a tag scan in HBM
             ("<div>" + "der Hund l&auml;uft &uuml;ber die Stra&szlig;e <br> " * 300 + "</div>").encode(),  # > kHtmlCands
-            ("<p>" + "caf&eacute; " * 4000 + "</p>").encode()]                                       # > kHtmlRewriteMax
+            ("<p>" + "caf&eacute; " * 4000 + "</p>").encode()]                                       # 56 KB
     assert 8192 < min(len(d) for d in docs) and len(docs[1]) <= 32768
     buf, offs = gpu.pack(docs)
     n = len(docs)
     got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
     st = gpu.last_stats()
-    assert 1 <= st.general_docs <= 2
+    assert st.general_docs == 0
     pr = priors_for(gpu, buf, offs, True, None)
     ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr)
     assert_same(got, ref, "html large pages")
@@ -144,6 +145,60 @@ def test_html_rewrite_large_pages(gpu, oracle):
     assert gpu.last_stats().general_docs == 0
     pr = priors_for(gpu, mb, mo, True, None)
     assert_same(got, oracle.detect_batch_ex(mb, mo, plain=np.zeros(len(many), np.uint8), priors=pr), "html candidates")
+
+
+def soft_limit_pages(n=24, seed=0xC1D20061, big=2):
+    """HTML pages past kMaxScriptBytes (41 to 200 KB, and `big` over 1 MB):
+    long runs of one language's words (spans up to the soft limit) among tags
+    with long attributes and entities, so the raw bytes left differ widely
+    from the rewritten ones; some pages switch script partway."""
+    rng = np.random.default_rng(seed)
+    v = corpus.vocab()
+    langs = ["en", "fr", "de", "es", "it", "pl", "cs", "ru", "bg", "el"]
+    langs = [l for l in langs if l in v]
+    marks = [b"<b>", b"</b>", b"<span class='note' style='color:#336699;font-weight:bold'>", b"</span>",
+             b"<a href='http://www.example.com/articles/2013/index.html?id=12345'>", b"</a>", b"<br/>",
+             b"<!-- navigation block -->", b"&amp;", b"&eacute;", b"&nbsp;", b"&bogus;", b"&", b"&#233;"]
+    docs = []
+    sizes = list(np.linspace(41000, 200000, n).astype(int)) + [int(x) for x in rng.integers(1_100_000, 1_400_000, big)]
+    for target in sizes:
+        out, size = [b"<html><body><p>"], 15
+        lang = langs[int(rng.integers(0, len(langs)))]
+        switch = target * float(rng.uniform(0.3, 0.9)) if rng.random() < 0.4 else None
+        markup = float(rng.uniform(0.1, 0.6))          # share of items that are markup
+        while size < target:
+            if switch is not None and size > switch:
+                lang, switch = langs[int(rng.integers(0, len(langs)))], None
+            if rng.random() < markup:
+                t = marks[int(rng.integers(0, len(marks)))]
+            else:
+                w = v[lang]
+                t = b" ".join(w[int(i)] for i in rng.integers(0, len(w), size=int(rng.integers(1, 6)))) + b" "
+            out.append(t)
+            size += len(t)
+        out.append(b"</p></body></html>")
+        docs.append(b"".join(out))
+    return docs
+
+
+def test_html_soft_limit_pages(gpu, oracle):
+    """Pages of kMaxScriptBytes (40,928) and more: the span soft limit
+    (getonescriptspan.cc:814-819) reads the page's raw bytes left, in both
+    regimes (under 2 x kMaxScriptBytes left: half of them; more: the
+    constant); the rewrite hands the span builders each byte's page offset
+    (cld_html.hip hpos / hgap).  Pages over 1 MB take the staged path's
+    worst-case regions.  Equal to the oracle; most pages stay on the parallel
+    kernels (a page holding a character whose HTML lowering differs, or a
+    4-byte one, is not rewritten)."""
+    docs = soft_limit_pages()
+    buf, offs = gpu.pack(docs)
+    n = len(docs)
+    got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+    st = gpu.last_stats()
+    pr = priors_for(gpu, buf, offs, True, None)
+    ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=8)
+    assert_same(got, ref, "html soft limit")
+    assert st.general_docs < n // 2, st.general_docs
 
 
 @pytest.mark.parametrize("cfg,n,seed", [("c2", 20000, 31), ("c3", 300, 32), ("c4", 11000, 33), ("c5", 20000, 34)])

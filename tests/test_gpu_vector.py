@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import corpus
-from test_gpu_html_hints import random_hints
+from test_gpu_html_hints import random_hints, soft_limit_pages
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -62,6 +62,14 @@ def test_vector_squeeze_html_hints(gpu, oracle):
     from test_gpu_parity import EDGE
     b, o = gpu.pack(EDGE)
     check(gpu, oracle, b, o, "edge")
+
+
+def test_vector_html_soft_limit_pages(gpu, oracle):
+    """Rewritten pages of kMaxScriptBytes and more in vec mode: page offsets
+    serve both MapBack and the span soft limit."""
+    docs = soft_limit_pages(n=12, seed=0xC1D20071, big=0)
+    buf, offs = gpu.pack(docs)
+    check(gpu, oracle, buf, offs, "html soft limit", html=True)
 
 
 def test_vector_matches_reference_directly(gpu):
