@@ -827,7 +827,9 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     // raw bytes of the lanes up to the stop (a prefix-sum read, not another
     // reduction), plus the hard limit's ' '
     put += rdl(pre + raw, stop < 64 ? stop : 63) + ((stop < 64 && ((Hm >> stop) & 1)) ? 1 : 0);
-    if (lpos + 64 > kLB || put + 64 > kMaxScriptBuffer) {
+    // (lb / omap room for the next window; put itself never passes
+    // kMaxScriptBytes + 1: the hard limit stops the span)
+    if (lpos + 64 > kLB) {
       bad = 1;
       break;
     }
