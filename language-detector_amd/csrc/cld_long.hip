@@ -649,29 +649,40 @@ __device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
 // vec mode: omap receives map2original_'s MapBack per span text byte; hpos
 // (a rewritten HTML page, cld_html.hip) maps each byte of dv to its offset in
 // the page as given -- offsets in omap are always page offsets.
+constexpr int kResumeRange = 1 << 30;           // next_span's *rlo: a range's low end, not an exact offset
 template <bool VEC = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane, uint32_t* omap = nullptr, const uint32_t* hpos = nullptr,
-                         const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr) {
+                         const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr, int* rlo = nullptr) {
   const uint64_t* const lsm = lsm_ext ? lsm_ext : S.lsm;
   lane = wave::lane_here();
   const int L = dv.len;
   const int common = (int)T.common, inherited = (int)T.inherited;
   // the soft limit (getonescriptspan.cc:814-819) from the raw bytes left: on
-  // a rewritten page the page offset of the resume point.  After dropped
-  // '&'s (hflag bit 1) the reference may resume at the first of them (a
-  // stale script, see the letter stop below): a document whose soft limit
-  // differs between the two, or whose two sit in different regimes, is
-  // re-queued (k_general scores the page itself).
+  // a rewritten page the page offset of the resume point.  Where the
+  // reference's scan stops at a dropped '&' (a stale script: the scan's
+  // script is not reset by an undecodable entity, :874-883, 974-987) it
+  // resumes up to a run of dropped '&'s earlier than the letter the span
+  // builder resumes at; the previous span left in *rlo either that offset
+  // (a letter stop of another script) or, with kResumeRange, the earliest one
+  // (after the hard limit); -1: none; no rlo: any resume point right after
+  // dropped '&'s counts as a range.
+  // A document whose soft limit differs across that range, or whose range
+  // straddles a regime, is re-queued (k_general scores the page itself).
   auto soft_of = [](int r) {
     return (kMaxScriptBytes <= r && r < 2 * kMaxScriptBytes) ? r / 2 : kMaxScriptBytes - kWithinScriptTail;
   };
   auto regime = [](int r) { return r < kMaxScriptBytes ? 0 : r < 2 * kMaxScriptBytes ? 1 : 2; };
   int remaining = L - next;
+  const int rl = rlo ? *rlo : -2;
+  if (rlo) *rlo = -1;
   if (dv.hp && next > 0 && next < L) {
     remaining = L - (int)gld(dv.hp + next);
-    if (gld(dv.hf + next) & 2) {
-      const int r0 = L - (int)gld(dv.hg + next);
+    if (rl >= 0 && !(rl & kResumeRange)) remaining = L - rl;   // the exact resume offset
+    const int lo = rl >= 0 ? ((rl & kResumeRange) ? rl & ~kResumeRange : -1)
+                           : (rl == -2 && (gld(dv.hf + next) & 2)) ? (int)gld(dv.hg + next) : -1;
+    if (lo >= 0) {
+      const int r0 = L - lo;
       if (soft_of(r0) != soft_of(remaining) || regime(r0) != regime(remaining)) {
         status = -1;
         return 0;
@@ -835,10 +846,36 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
     if (stop < 64) {
       const int xs = (w << 6) + stop;
-      if ((Hm >> stop) & 1) nxt = find_first_g(lsm, xs + rdl(n, stop), L);
-      else if ((Sm >> stop) & 1) nxt = find_first_g(lsm, xs, L);   // the gap scan starts at the break char
-      else {
+      if ((Hm >> stop) & 1) {
+        const int xe = xs + rdl(n, stop);
+        nxt = find_first_g(lsm, xe, L);
+        // after the hard limit the reference's gap scan keeps the last
+        // letter's script: the first dropped '&' in the gap stops it
+        if (rlo && dv.hp) {
+          const int e = nxt < L ? nxt : L - 1;
+          for (int y = xe; y <= e; y += 64) {
+            const uint64_t dm = __ballot(y + lane <= e && (gld(dv.hf + y + lane) & 2));
+            if (dm) {
+              *rlo = (int)gld(dv.hg + y + __builtin_ctzll(dm)) | kResumeRange;
+              break;
+            }
+          }
+        }
+      } else if ((Sm >> stop) & 1) {
+        nxt = find_first_g(lsm, xs, L);                               // the gap scan starts at the break char
+      } else {
         nxt = xs;                                                     // another script's letter stop
+        // dropped '&'s right before it: after a letter of a third script (the
+        // single-letter continuation) the reference's script is stale there,
+        // and its scan stops at the last of them (:916-931: the next byte's
+        // script decides); after a letter of the span's own script it
+        // consumes them
+        if (rlo && dv.hp && (gld(dv.hf + xs) & 2)) {
+          int pc = xs - 1;
+          while (pc > 0 && (dv.p[pc] & 0xC0) == 0x80) --pc;
+          const int scp = pc >= 0 ? script_num(T, dv, pc) : 0;
+          if (scp != 0 && scp != common && scp != ss && scp != inherited) *rlo = (int)gld(dv.hp + xs) - 1;
+        }
         // vec mode: dropped '&'s right before it may stop the reference's scan
         // at the first of them (a stale script after a foreign letter,
         // getonescriptspan.cc:876-931), one offset earlier: the sequential kernel
@@ -1326,14 +1363,20 @@ __device__ __forceinline__ int range_pop(const uint64_t* m, int a, int b) {   //
 
 // Out of line: Squeeze is rare, and inlined its state would count against the
 // registers of every pass.
+// OW (vec mode): CheapSqueezeInplaceOverwrite (:869-940) -- the chunks start
+// after the leading space, and a squeezed stretch becomes '.'s (each skipped
+// chunk closing with a ' ') instead of being cut, so the text keeps its
+// length and the offset map stays valid.
+template <bool OW = false>
 __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool careful, int lane) {
   constexpr int kChunk = 48;
+  constexpr int s0 = OW ? 1 : 0;                 // (OW: the first byte, a space, is always kept)
   const int nw = (len + 63) >> 6;
   // chunk starts
   for (int i = lane; i < nw + 1; i += 64) S.chm[i] = 0;
   gsync();
   {
-    int src = 0, cw = 0;
+    int src = s0, cw = 0;
     uint64_t cur = 0;
     while (src < len) {
       if ((src >> 6) != cw) {
@@ -1355,7 +1398,7 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
   int carry = 0;
   for (int w = 0; w < nw; ++w) {
     const int x = (w << 6) + lane;
-    const bool valid = x < len;
+    const bool valid = x >= s0 && x < len;
     const uint8_t b = valid ? text[x] : (uint8_t)0;
     const uint64_t st = char_starts(text, w << 6, len, S.chm, carry, careful, lane);
     const bool lead = valid && ((st >> lane) & 1);
@@ -1375,6 +1418,50 @@ __device__ __noinline__ int squeeze_span(Slot& S, uint8_t* text, int len, bool c
   }
   gsync();
   constexpr int kSpaceThresh = (kChunk * 25) / 100, kPredictThresh = (kChunk * 40) / 100;
+  if constexpr (OW) {
+    bool skipping = false;
+    for (int src = 1; src < len;) {
+      int clen = min(kChunk, len - src);
+      while ((ufl(text[src + clen]) & 0xC0) == 0x80) ++clen;   // move past continuation bytes
+      const int space_n = range_pop(S.spm, src, src + (clen & ~3));
+      const int predb_n = range_pop(S.delm, src, src + clen) + range_pop(S.aux[0], src, src + clen) +
+                          2 * range_pop(S.aux[1], src, src + clen);
+      if (space_n >= kSpaceThresh || predb_n >= kPredictThresh) {
+        if (!skipping) {                         // keeping -> skipping: the word before becomes '.'s
+          const int lim = min(src, 32);
+          const uint64_t spc = __ballot(lane < lim && text[src - lane - 1] == ' ');
+          int n = 0;
+          if (spc) {
+            n = __builtin_ctzll(spc);
+          } else {
+            const uint64_t cb = __ballot(lane < lim && (text[src - lane] & 0xC0) != 0x80);
+            n = cb ? __builtin_ctzll(cb) : 0;
+          }
+          gsync();
+          if (lane < n) text[src - n + lane] = '.';
+          skipping = true;
+        }
+        gsync();
+        if (lane < clen) text[src + lane] = lane == clen - 1 ? ' ' : '.';   // (clen <= 51)
+      } else if (skipping) {                     // skipping -> keeping: up to the next word start
+        const int lim = min(clen, 32);
+        const uint64_t spc = __ballot(lane < lim && text[src + lane] == ' ');
+        int n = 0;
+        if (spc) {
+          n = __builtin_ctzll(spc) + 1;
+        } else {
+          const uint64_t cb = __ballot(lane < lim && (text[src + lane] & 0xC0) != 0x80);
+          n = cb ? __builtin_ctzll(cb) : 0;
+        }
+        gsync();
+        if (lane < n - 1) text[src + lane] = '.';
+        skipping = false;
+      }
+      gsync();
+      src += clen;
+    }
+    return len;                                  // (no pads: the text keeps its length)
+  }
   int src = 0, dst = 0;
   bool skipping = false;
   while (src < len) {
@@ -2634,7 +2721,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
     }
     const bool rep_inline = rep && !from_cache;
     wsync();
-    int next = 0, total = 0, ci = 0;
+    int next = 0, total = 0, ci = 0, rlo = -1;
     bool restart = false;
     for (;;) {
       int ul = 0, st = 0, tb;
@@ -2651,7 +2738,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
         tb = next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr, VEC ? V->hpos : nullptr,
-                            VEC ? V->hgap : nullptr);
+                            VEC ? V->hgap : nullptr, nullptr, &rlo);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {
@@ -2664,7 +2751,6 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
       if constexpr (D) mark(s, lane, 1, t);
       if (pass == 1) {
         if (tb > 2048 && squeeze_trigger(S, lb, careful, lane)) {   // recursion with Squeeze (:1867-1900)
-          if constexpr (VEC) return -kWhySqueeze;  // (CheapSqueezeInplaceOverwrite: the sequential kernel)
           restart = true;
           cache_ok = false;
           break;
@@ -2678,7 +2764,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         for (int i = lane; i < n16; i += 64)
           reinterpret_cast<uint4*>(s.text)[i] = reinterpret_cast<const uint4*>(lb)[i];
         wsync();
-        if (sq) tb = squeeze_span(S, s.text, tb, careful, lane);             // in place, as the reference does
+        if (sq) tb = squeeze_span<VEC>(S, s.text, tb, careful, lane);        // in place, as the reference does
         if (rep_inline) {
           bool okr;
           tb = rep_words<VEC>(S, s.text, s.text, tb, hcarry, ep, careful, okr, lane);   // in place, as the reference does
@@ -2694,7 +2780,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
       } else {
         const uint8_t* text = lb;
-        if (sq) tb = squeeze_span(S, lb, tb, careful, lane);
+        if (sq) tb = squeeze_span<VEC>(S, lb, tb, careful, lane);
         if (rep_inline) {
           bool okr;
           tb = rep_words<VEC>(S, lb, S.lb[1], tb, hcarry, ep, careful, okr, lane);
@@ -2793,11 +2879,11 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
                              uint32_t* pool_ctr, int lane) {
   bool careful;
   if (!classify(T, dv, S, careful, lane)) return kStNone;
-  int next = 0, nsp = 0, cur = 0;
+  int next = 0, nsp = 0, cur = 0, rlo = -1;
   for (;;) {
     if (cur + kLB > kLbdCap || nsp >= kMaxSpans) return kStNone;
     int ul = 0, st = 0;
-    const int tb = next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane);
+    const int tb = next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane, nullptr, nullptr, nullptr, nullptr, &rlo);
     if (st == 0) break;
     if (st < 0) return kStNone;
     if (tb > 2048 && squeeze_trigger(S, S.lbd + cur, careful, lane)) return kStNone;   // the Squeeze restart
@@ -2879,12 +2965,12 @@ __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& 
   bool careful;
   if (!classify(T, dv, S, careful, lane, lsm)) return false;
   uint64_t* tab = reinterpret_cast<uint64_t*>(region + tab_off);
-  int next = 0, nsp = 0;
+  int next = 0, nsp = 0, rlo = -1;
   uint64_t cur = sizeof(StHdr);
   for (;;) {
     if (cur + 4ull * (L - (uint64_t)next) + 128 > sizeof(StHdr) + tc || (uint64_t)nsp >= ns) return false;
     int ul = 0, st = 0;
-    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm);
+    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm, &rlo);
     if (st == 0) break;
     if (st < 0) return false;
     if (tb > 2048 && squeeze_trigger(S, region + cur, careful, lane)) return false;   // the Squeeze restart

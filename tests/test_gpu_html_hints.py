@@ -158,7 +158,8 @@ def soft_limit_pages(n=24, seed=0xC1D20061, big=2):
     langs = [l for l in langs if l in v]
     marks = [b"<b>", b"</b>", b"<span class='note' style='color:#336699;font-weight:bold'>", b"</span>",
              b"<a href='http://www.example.com/articles/2013/index.html?id=12345'>", b"</a>", b"<br/>",
-             b"<!-- navigation block -->", b"&amp;", b"&eacute;", b"&nbsp;", b"&bogus;", b"&", b"&#233;"]
+             b"<!-- navigation block -->", b"&amp;", b"&eacute;", b"&nbsp;", b"&bogus;", b"&", b"&#233;",
+             "дом&&chat ".encode(), "word, &&дом ".encode(), b"x&&y "]
     docs = []
     sizes = list(np.linspace(41000, 200000, n).astype(int)) + [int(x) for x in rng.integers(1_100_000, 1_400_000, big)]
     for target in sizes:

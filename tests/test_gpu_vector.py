@@ -55,6 +55,8 @@ def test_vector_squeeze_html_hints(gpu, oracle):
     buf, offs = corpus.c3(30, boiler_frac=0.5)
     gv = check(gpu, oracle, buf, offs, "squeeze")
     assert max(len(v) for v in gv) > 5
+    # the Squeeze restart's CheapSqueezeInplaceOverwrite runs in k_long<VEC>
+    assert gpu.last_stats().general_docs == 0
     buf, offs = corpus.html(300, seed=12)
     check(gpu, oracle, buf, offs, "html", html=True)
     buf, offs = corpus.c2(1500, seed=13)
