@@ -650,7 +650,10 @@ __device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
 // (a rewritten HTML page, cld_html.hip) maps each byte of dv to its offset in
 // the page as given -- offsets in omap are always page offsets.
 constexpr int kResumeRange = 1 << 30;           // next_span's *rlo: a range's low end, not an exact offset
-template <bool VEC = false>
+// HB: a rewritten HTML page of kMaxScriptBytes and more (dv.hp set): the
+// soft limit from page offsets and the resume bookkeeping below.  Its own
+// instantiation, so plain documents' span loop carries none of its state.
+template <bool VEC = false, bool HB = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane, uint32_t* omap = nullptr, const uint32_t* hpos = nullptr,
                          const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr, int* rlo = nullptr) {
@@ -674,9 +677,9 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   };
   auto regime = [](int r) { return r < kMaxScriptBytes ? 0 : r < 2 * kMaxScriptBytes ? 1 : 2; };
   int remaining = L - next;
-  const int rl = rlo ? *rlo : -2;
-  if (rlo) *rlo = -1;
-  if (dv.hp && next > 0 && next < L) {
+  const int rl = (HB && rlo) ? *rlo : -2;
+  if (HB && rlo) *rlo = -1;
+  if (HB && dv.hp && next > 0 && next < L) {
     remaining = L - (int)gld(dv.hp + next);
     if (rl >= 0 && !(rl & kResumeRange)) remaining = L - rl;   // the exact resume offset
     const int lo = rl >= 0 ? ((rl & kResumeRange) ? rl & ~kResumeRange : -1)
@@ -851,7 +854,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         nxt = find_first_g(lsm, xe, L);
         // after the hard limit the reference's gap scan keeps the last
         // letter's script: the first dropped '&' in the gap stops it
-        if (rlo && dv.hp) {
+        if (HB && rlo && dv.hp) {
           const int e = nxt < L ? nxt : L - 1;
           for (int y = xe; y <= e; y += 64) {
             const uint64_t dm = __ballot(y + lane <= e && (gld(dv.hf + y + lane) & 2));
@@ -870,7 +873,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         // and its scan stops at the last of them (:916-931: the next byte's
         // script decides); after a letter of the span's own script it
         // consumes them
-        if (rlo && dv.hp && (gld(dv.hf + xs) & 2)) {
+        if (HB && rlo && dv.hp && (gld(dv.hf + xs) & 2)) {
           int pc = xs - 1;
           while (pc > 0 && (dv.p[pc] & 0xC0) == 0x80) --pc;
           const int scp = pc >= 0 ? script_num(T, dv, pc) : 0;
@@ -2737,8 +2740,10 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
-        tb = next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr, VEC ? V->hpos : nullptr,
-                            VEC ? V->hgap : nullptr, nullptr, &rlo);
+        tb = dv.hp ? next_span<VEC, true>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
+                                          VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr, nullptr, &rlo)
+                   : next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
+                                    VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {
@@ -2883,7 +2888,9 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   for (;;) {
     if (cur + kLB > kLbdCap || nsp >= kMaxSpans) return kStNone;
     int ul = 0, st = 0;
-    const int tb = next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane, nullptr, nullptr, nullptr, nullptr, &rlo);
+    const int tb = dv.hp ? next_span<false, true>(T, dv, S, S.lbd + cur, next, ul, st, lane, nullptr, nullptr, nullptr,
+                                                  nullptr, &rlo)
+                         : next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane);
     if (st == 0) break;
     if (st < 0) return kStNone;
     if (tb > 2048 && squeeze_trigger(S, S.lbd + cur, careful, lane)) return kStNone;   // the Squeeze restart
@@ -2970,7 +2977,9 @@ __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& 
   for (;;) {
     if (cur + 4ull * (L - (uint64_t)next) + 128 > sizeof(StHdr) + tc || (uint64_t)nsp >= ns) return false;
     int ul = 0, st = 0;
-    const int tb = next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm, &rlo);
+    const int tb = dv.hp ? next_span<false, true>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr,
+                                                  lsm, &rlo)
+                         : next_span<false>(T, dv, S, region + cur, next, ul, st, lane, nullptr, nullptr, nullptr, lsm);
     if (st == 0) break;
     if (st < 0) return false;
     if (tb > 2048 && squeeze_trigger(S, region + cur, careful, lane)) return false;   // the Squeeze restart
