@@ -32,7 +32,8 @@
 //
 // One wavefront per page, in three steps (the reference's own pass is
 // sequential, but only its '<' / '&' stops carry state):
-//   1. the page goes to LDS; every '<' and '&' of it is a candidate; each
+//   1. the page goes to LDS (up to kHtmlStage bytes; longer pages are read in
+//      place); every '<' and '&' of it is a candidate; each
 //      lane evaluates one '&' as if the scan reached it (ReadEntity: bytes
 //      consumed, bytes decoded) into an LDS list (a segment of the page at a
 //      time: whole 64-byte windows holding at most kHtmlCands candidates);
@@ -57,9 +58,23 @@ using wave::wsum;
 using wave::wsync;
 
 constexpr int kHtmlRewriteMax = 64 << 20;  // (lng::kStBigMax) larger pages stay on k_general
-constexpr int kHtmlStage = 8192;        // pages up to this size are staged in LDS, larger ones read in place
-constexpr int kHtmlCands = 1024;        // '<' / '&' candidates per segment of a page (round 5: any number per page)
-constexpr int kHtmlWPB = 2;            // waves (pages) per workgroup
+// LDS per wave (the page stage + the candidate lists) sets the resident waves
+// of this latency-bound kernel: an 8 KB stage and 1,024 candidates per
+// segment left 1.5 waves/SIMD; 2 KB and 256 (5.4 KB per wave) give 8, and
+// the rewrite of 100 K 16 KB pages takes 21.4 ms instead of 48.2
+// (profiles/round5_html_lds_ab.txt; 1 KB / 128 measured the same).
+#ifndef HTML_STAGE
+#define HTML_STAGE 2048
+#endif
+#ifndef HTML_CANDS
+#define HTML_CANDS 256
+#endif
+#ifndef HTML_WPB
+#define HTML_WPB 4
+#endif
+constexpr int kHtmlStage = HTML_STAGE;  // pages up to this size are staged in LDS, larger ones read in place
+constexpr int kHtmlCands = HTML_CANDS;  // '<' / '&' candidates per segment of a page (round 5: any number per page)
+constexpr int kHtmlWPB = HTML_WPB;      // waves (pages) per workgroup
 
 // The character b0 b1 b2 (n bytes) lowers the same way in HTML mode as in plain text.
 __device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0, uint32_t b1, uint32_t b2, int n) {
