@@ -684,6 +684,7 @@ __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __rest
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)blockIdx.x * sizeof(lng::Slot));
   const uint32_t total =
       wave::uflu(__hip_atomic_load(&counters[kCtrStP2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (total == 0) return;                        // (no dequeue atomics: 5,120 of them on one word took 80 us)
   for (;;) {
     const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrStDqRep], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
