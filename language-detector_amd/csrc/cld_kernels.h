@@ -87,6 +87,9 @@ constexpr uint16_t kWaveRequeued = 0xFFFE;
 // kMaxScriptBytes (cld_pipeline.hip): rewritten HTML pages this long and
 // longer carry page offsets (hpos / hgap) for the span soft limit
 constexpr int kHtmlSoftMin = 40928;
+// lng::kDocCap (cld_long.hip): the fused k_long takes documents up to this
+// many bytes less 64; longer ones need the staged path's big-document regions
+constexpr uint64_t kLongDocCap = 1u << 20;
 hipError_t cld_launch_wave_only(const DevTables* T, const uint8_t* buf, const uint64_t* offs, int n, cld_result* out,
                                 uint32_t* requeue_list, uint32_t* counters, uint32_t cflags, hipStream_t s);
 // HTML documents of the batch (special & kSpecialHtml) rewritten into plain

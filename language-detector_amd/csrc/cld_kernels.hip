@@ -19,6 +19,7 @@
 #include "cld_html.hip"
 
 static_assert(kHtmlSoftMin == cld::kMaxScriptBytes, "kHtmlSoftMin is kMaxScriptBytes");
+static_assert(kLongDocCap == (uint64_t)cld::lng::kDocCap, "kLongDocCap is lng::kDocCap");
 
 #ifndef GEN_LANES_PER_WAVE
 // k_general / k_general_vec: documents per wavefront.  One per wave: the

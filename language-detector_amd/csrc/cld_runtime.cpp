@@ -726,7 +726,7 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 // document bytes span [html_base, html_base + html_bytes) of the offsets.
 int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, hipStream_t s,
             const uint8_t* special = nullptr, const uint32_t* priors = nullptr, uint32_t cflags = 0,
-            uint64_t html_base = 0, uint64_t html_bytes = 0, uint32_t* ctr = nullptr) {
+            uint64_t html_base = 0, uint64_t html_bytes = 0, uint32_t* ctr = nullptr, int64_t long_hint = -1) {
   cflags &= kCldFlags;
   const uint8_t *hbuf = nullptr, *hflag = nullptr;
   uint32_t *hpos = nullptr, *hgap = nullptr;
@@ -784,7 +784,12 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     // the staged path takes the list unless diagnostics (the fused kernel's
     // trace / debug dump / stage cycles) are on; what it does not take goes to
     // the fused kernel as the fallback list
-    const bool staged = d->staged && !d->h_trace && !d->d_dbg && !d->d_prof;
+    // long_hint (the host path, which holds the offsets): documents longer
+    // than k_wave takes.  A list that short goes whole to the fused kernel
+    // anyway, so the eight staged launches are skipped (each costs its
+    // dispatch even when its list is empty: ~60 us per chunk of tweets)
+    const bool staged = d->staged && !d->h_trace && !d->d_dbg && !d->d_prof &&
+                        !(long_hint >= 0 && small_long_list(d) > 0 && long_hint <= (int64_t)small_long_list(d));
     int ctr_total = kCtrRequeue, ctr_deq = kCtrDequeue;
     if (staged) {
       if (grow(&d->d_meta, &d->meta_cap, std::max<size_t>(n, 1))) return CLD_ENOMEM;
@@ -1166,14 +1171,27 @@ int run_host_stream(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
     HIP_BRK(hipStreamWaitEvent(d->stream, h.up, 0))
     if (h.busy) HIP_BRK(hipStreamWaitEvent(d->stream, h.down, 0))
     const uint8_t* kbuf = h.d_in - base;
+    // documents of this chunk longer than k_wave takes (counted up to the
+    // small-list bound; StripExtras only shortens documents); one over the
+    // fused kernel's cap needs the staged path whatever the count
+    int64_t long_hint = 0;
+    {
+      const int64_t lim = (int64_t)small_long_list(d);
+      const uint64_t* o = offs + a;
+      for (size_t i = 0; i < m && long_hint <= lim; ++i) {
+        const uint64_t len = o[i + 1] - o[i];
+        long_hint += len > (uint64_t)kWaveCap;
+        if (len > kLongDocCap - 64) long_hint = lim + 1;
+      }
+    }
     if (flags & kPrepFlags) {
       if ((rc = enqueue_prepare(d, kbuf, h.d_offs, m, bytes, flags, d->stream))) break;
       rc = enqueue(d, d->d_sbuf, d->d_soffs, m, h.d_out, d->stream, nullptr, nullptr, flags, 0, 0,
-                   d->d_ctrs + c * kCtrSlots);
+                   d->d_ctrs + c * kCtrSlots, long_hint);
     } else {
       rc = enqueue(d, kbuf, h.d_offs, m, h.d_out, d->stream, special ? h.d_sp : nullptr,
                    (special && priors) ? h.d_pri : nullptr, flags, base, (special && html) ? bytes : 0,
-                   d->d_ctrs + c * kCtrSlots);
+                   d->d_ctrs + c * kCtrSlots, long_hint);
     }
     if (rc) break;
     HIP_BRK(hipEventRecord(h.comp, d->stream))
