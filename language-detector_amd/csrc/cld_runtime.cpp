@@ -685,11 +685,17 @@ constexpr uint32_t kCldFlags = CLD_FLAG_SCORE_AS_QUADS | CLD_FLAG_BEST_EFFORT;
 constexpr uint32_t kPublicFlags = kCldFlags | CLD_FLAG_DEBUG_MASK;
 
 // A long list this short goes whole to the fused k_long, whose two-wave
-// speculation is for small batches: 4 documents per fused wave, or
-// CLD_LONG_SMALL documents (0: the staged path for every batch).
+// speculation halves a lone long document's latency: 64 documents, or
+// CLD_LONG_SMALL documents (0: the staged path for every batch).  Up to
+// round 5 the bound was 4 per fused wave (16K documents); request-sized
+// batches (~1,000 C5 documents, ~200 of them long) run better staged, where
+// span-parallel scoring splits their many-span pages: 1 caller 96.6K ->
+// 106K docs/s (p99 34 -> 17 ms), 32 callers 699K -> 875K
+// (profiles/round5_req_staged_ab.jsonl).
 uint32_t small_long_list(const Device* d) {
+  (void)d;
   static const long v = getenv("CLD_LONG_SMALL") ? atol(getenv("CLD_LONG_SMALL")) : -1;
-  return v >= 0 ? (uint32_t)v : 4u * (uint32_t)d->n_slots;
+  return v >= 0 ? (uint32_t)v : 64u;
 }
 
 // Batches holding a document of this many KB go to the fused k_long whole

@@ -80,18 +80,19 @@ def test_gpu_equals_reference_with_flags(gpu, ref, ref_tables, golden, flags):
 
 
 def test_small_batches_speculate_and_equal_reference(gpu, ref):
-    """Small batches of long documents: k_long gives the longest of them a
-    pass-1 wave and a pass-2 wave (speculation; the launch turns it on when the
-    long list has at most 4 documents per resident wave, which every batch here
-    has), and takes pass 2's result only where pass 1 was not good enough.
-    Pages that need pass 2 (Repeats), ones that stop after pass 1, hinted and
-    HTML pages, each equal to the reference; request-sized C5 batches too."""
-    b3, o3 = corpus.c3(600, seed=811)
-    got = gpu.detect_batch(buf=b3, offsets=o3)
-    st = gpu.last_stats(0)
-    assert st.long_docs == 600 and st.general_docs == 0
-    assert st.passes[1] > 100 and st.passes[0] > 20      # both outcomes of the pass-1 wave occur (Q0: 44 / 556)
-    same(got, ref.detect_batch(b3, o3, threads=16), "c3 600")
+    """Small batches of long documents: a long list of at most 64 documents
+    goes to the fused k_long, which gives the longest of them a pass-1 wave and
+    a pass-2 wave (speculation) and takes pass 2's result only where pass 1 was
+    not good enough; larger ones (request-sized C5 batches: ~200 long
+    documents) take the staged path.  Pages that need pass 2 (Repeats), ones
+    that stop after pass 1, hinted and HTML pages, each equal to the reference."""
+    for n, seed in ((64, 810), (600, 811)):
+        b3, o3 = corpus.c3(n, seed=seed)
+        got = gpu.detect_batch(buf=b3, offsets=o3)
+        st = gpu.last_stats(0)
+        assert st.long_docs == n and st.general_docs == 0
+        assert st.passes[1] > n // 6 and st.passes[0] > 0    # both outcomes of the pass-1 wave occur (Q0: 44 / 556)
+        same(got, ref.detect_batch(b3, o3, threads=16), "c3 %d" % n)
     for seed in (812, 813, 814):                         # ~1 MiB requests, each with ~180 long documents
         b5, o5 = corpus.c5(1000, seed=seed)
         same(gpu.detect_batch(buf=b5, offsets=o5), ref.detect_batch(b5, o5, threads=16), "c5 request %d" % seed)
