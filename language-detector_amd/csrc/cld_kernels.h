@@ -29,7 +29,9 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
        kCtrStPool = 27 /* store 16-byte units taken */,
        // span-parallel documents: group lists and document lists of passes 1 and 2
        kCtrStG1 = 28, kCtrStDqG1 = 29, kCtrStPar1 = 30, kCtrStDqF1 = 31,
-       kCtrStG2 = 32, kCtrStDqG2 = 33, kCtrStPar2 = 34, kCtrStDqF2 = 35, kCtrSlots = 48 };
+       kCtrStG2 = 32, kCtrStDqG2 = 33, kCtrStPar2 = 34, kCtrStDqF2 = 35,
+       // heavy (many-span) entries of the stored and pass-2 lists, filled from the top
+       kCtrStOkH = 36, kCtrStP2H = 37, kCtrSlots = 48 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
 // (hbuf / hflag); k_general, should it get it back, scores the original page.

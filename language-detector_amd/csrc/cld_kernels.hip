@@ -463,6 +463,28 @@ constexpr int kStWPB = 4;
 using StSmem = lng::SmemT<LNG_ST_TEXT, false>;
 static_assert(kStWPB * sizeof(StSmem) * (4 * LNG_ST_WPS / kStWPB) <= 160 * 1024, "k_lscore LDS per CU");
 
+// The stored and pass-2 lists are two-ended: documents of more than
+// kHeavySpans spans (a span costs a wave ~15 us per pass whatever its length)
+// fill from the top, the others from the bottom, and the consumers take the
+// heavy ones first -- longest work first, as the LPT list orders by bytes.
+// Without it a 200-span page of a C3 batch (16 KB like the rest) or a C5
+// batch's pass-2 list could come last and set the kernel's tail.
+#ifndef LNG_HEAVY_SPANS
+#define LNG_HEAVY_SPANS 32
+#endif
+constexpr uint32_t kHeavySpans = LNG_HEAVY_SPANS;
+__device__ __forceinline__ void st_put(uint32_t* list, uint32_t* counters, int ctr_lo, int ctr_hi, uint32_t n,
+                                       bool heavy, uint32_t v) {   // (one lane)
+  if (heavy) list[n - 1 - atomicAdd(&counters[ctr_hi], 1u)] = v;
+  else list[atomicAdd(&counters[ctr_lo], 1u)] = v;
+}
+__device__ __forceinline__ uint32_t st_get(const uint32_t* list, uint32_t nh, uint32_t n, uint32_t e) {
+  return e < nh ? list[n - 1 - e] : list[e - nh];
+}
+__device__ __forceinline__ uint32_t st_count(uint32_t* counters, int ctr) {
+  return wave::uflu(__hip_atomic_load(&counters[ctr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ list, uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, uint64_t pool_bytes,
@@ -470,7 +492,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     uint32_t* __restrict__ counters, const uint8_t* __restrict__ special, const uint8_t* __restrict__ hbuf,
     const uint8_t* __restrict__ hflag, const uint32_t* __restrict__ hpos, const uint32_t* __restrict__ hgap,
     uint32_t fault_doc, uint32_t small_total, const uint32_t* __restrict__ hist, uint32_t* __restrict__ par_list,
-    uint64_t* __restrict__ group_list, uint32_t gcap, uint32_t heavy_kb) {
+    uint64_t* __restrict__ group_list, uint32_t gcap, uint32_t heavy_kb, uint32_t n) {
   const DevTables& T = *Tp;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
@@ -489,6 +511,18 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
   // the fused kernel takes the batch, in list order (documents over kDocCap,
   // which it does not take, still come here)
   const bool fused = total <= small_total || heavy;
+  // page batches (mean long document >= 8 KB; hist bucket b holds 63 - b KB)
+  // split only their heaviest documents (lng::kParMinPages)
+  int par_min = lng::kParMin;
+  if (hist) {
+    uint64_t cnt = 0, kb = 0;
+    for (int b = 0; b < kLenBuckets; ++b) {
+      const uint64_t c = wave::uflu(hist[b]);
+      cnt += c;
+      kb += c * (uint64_t)(kLenBuckets - 1 - b);
+    }
+    if (cnt && kb >= 8 * cnt) par_min = lng::kParMinPages;
+  }
   const bool exact = lng::space_lowers_to_space(T);
   const uint64_t units = pool_bytes >> 4;
   for (;;) {
@@ -508,7 +542,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     uint64_t at = lng::kStNone;
     if (exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc) {
       const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr, hp, hg};
-      at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane);
+      at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane, par_min);
     } else if (exact && L <= lng::kStBigMax && i != fault_doc) {   // over kDocCap: a worst-case region
       const uint64_t u = (lng::st_big_bytes(L) + 15) >> 4;
       uint32_t got = 0;
@@ -516,15 +550,16 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
       got = wave::uflu(__shfl((int)got, 0, 64));
       if ((uint64_t)got + u <= units) {
         const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr, hp, hg};
-        if (lng::st_spans_big(T, dv, S, pool + ((uint64_t)got << 4), lane)) at = (uint64_t)got << 4;
+        if (lng::st_spans_big(T, dv, S, pool + ((uint64_t)got << 4), lane, par_min)) at = (uint64_t)got << 4;
       }
     }
     // a span-parallel document (more than kParMin spans): its groups to the group list
-    uint32_t ng = 0, gb = 0;
+    uint32_t ng = 0, gb = 0, nsp = 0;
     if (at != lng::kStNone) {
       const lng::StHdr* h = reinterpret_cast<const lng::StHdr*>(pool + at);
+      nsp = wave::uflu(gld(&h->nsp));
       if (wave::uflu(gld(&h->par))) {
-        ng = (wave::uflu(gld(&h->nsp)) + lng::kParG - 1) / lng::kParG;
+        ng = (nsp + lng::kParG - 1) / lng::kParG;
         if (lane == 0) gb = atomicAdd(&counters[kCtrStG1], ng);
         gb = wave::uflu(__shfl((int)gb, 0, 64));
         const bool fits = (uint64_t)gb + ng <= gcap;
@@ -539,7 +574,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
       } else {
         meta[k] = at;
         if (ng) par_list[atomicAdd(&counters[kCtrStPar1], 1u)] = k;
-        else ok_list[atomicAdd(&counters[kCtrStOk], 1u)] = k;
+        else st_put(ok_list, counters, kCtrStOk, kCtrStOkH, n, nsp > kHeavySpans, k);
       }
     }
   }
@@ -551,13 +586,13 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
     uint8_t* __restrict__ slots, uint8_t* __restrict__ pool, const uint64_t* __restrict__ meta,
     const uint32_t* __restrict__ in_list, uint32_t* __restrict__ p2_list, uint32_t* __restrict__ fall_list,
     uint32_t* __restrict__ counters, uint32_t cflags, const uint8_t* __restrict__ special,
-    const uint32_t* __restrict__ priors) {
+    const uint32_t* __restrict__ priors, uint32_t n) {
   __shared__ StSmem smem[kStWPB];
   const DevTables& T = *Tp;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)(blockIdx.x * kStWPB + wv) * sizeof(lng::Slot));
-  const uint32_t total = wave::uflu(
-      __hip_atomic_load(&counters[P2 ? kCtrStP2 : kCtrStOk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t nh = st_count(counters, P2 ? kCtrStP2H : kCtrStOkH);
+  const uint32_t total = nh + st_count(counters, P2 ? kCtrStP2 : kCtrStOk);
   if (total == 0) return;
   if (lane == 0) {
     smem[wv].dbg = nullptr;
@@ -567,7 +602,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
   for (;;) {
     const uint32_t e = wave::uflu(atomicAdd(&counters[P2 ? kCtrStDqS2 : kCtrStDqS1], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
-    const uint32_t k = in_list[e];
+    const uint32_t k = st_get(in_list, nh, n, e);
     if (P2 && (k & 0x80000000u)) continue;       // a span-parallel document: k_lgroup / k_lfinish
     const uint64_t at = meta[k];
     if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
@@ -575,11 +610,12 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const int r = lng::st_score(T, S, smem[wv], pool + at, P2, &out[i], cflags,
                                 (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, lane);
+    const uint32_t nsp = (!P2 && r == 0) ? wave::uflu(gld(&reinterpret_cast<const lng::StHdr*>(pool + at)->nsp)) : 0u;
     if (lane == 0) {
       if (r == 1) {
         atomicAdd(&counters[P2 ? kCtrPass2 : kCtrPass1], 1u);
       } else if (r == 0 && !P2) {
-        p2_list[atomicAdd(&counters[kCtrStP2], 1u)] = k;
+        st_put(p2_list, counters, kCtrStP2, kCtrStP2H, n, nsp > kHeavySpans, k);
       } else {                                   // capacity (the LDS window): the fused kernel redoes it
         fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
       }
@@ -661,7 +697,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lfinish(
         group_list2[gb + g] = fits ? ((uint64_t)k | ((uint64_t)g << 32)) : ~0ull;
       if (lane == 0) {
         if (fits) {
-          p2_list[atomicAdd(&counters[kCtrStP2], 1u)] = k | 0x80000000u;
+          st_put(p2_list, counters, kCtrStP2, kCtrStP2H, n, true, k | 0x80000000u);
           par_lists[n + atomicAdd(&counters[kCtrStPar2], 1u)] = k;
         } else {
           fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = i;
@@ -679,17 +715,17 @@ __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __rest
                                                          uint64_t* __restrict__ meta,
                                                          const uint32_t* __restrict__ p2_list,
                                                          uint32_t* __restrict__ requeue2,
-                                                         uint32_t* __restrict__ counters) {
+                                                         uint32_t* __restrict__ counters, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint16_t pred[kPredictionTableSize];
   const int lane = threadIdx.x & 63;
   lng::Slot& S = *reinterpret_cast<lng::Slot*>(slots + (uint64_t)blockIdx.x * sizeof(lng::Slot));
-  const uint32_t total =
-      wave::uflu(__hip_atomic_load(&counters[kCtrStP2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t nh = st_count(counters, kCtrStP2H);
+  const uint32_t total = nh + st_count(counters, kCtrStP2);
   if (total == 0) return;                        // (no dequeue atomics: 5,120 of them on one word took 80 us)
   for (;;) {
     const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrStDqRep], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
-    const uint32_t k = p2_list[e] & 0x7FFFFFFFu;   // (bit 31: a span-parallel document)
+    const uint32_t k = st_get(p2_list, nh, n, e) & 0x7FFFFFFFu;   // (bit 31: a span-parallel document)
     if (!lng::st_rep(pred, S, pool + meta[k], lane) && lane == 0) {
       meta[k] = lng::kStNone;
       requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = list[k];
@@ -887,17 +923,17 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
   const uint32_t gc = (uint32_t)gcap, nn = (uint32_t)n;
   hipLaunchKernelGGL(cld::k_lspan, gsp, bst, 0, s, d_T, buf, offs, list, slots, pool, pool_bytes, meta, ok_list,
                      fall_list, counters, special, hbuf, hflag, hpos, hgap, fault_doc, small_total, hist, par_lists,
-                     gl1, gc, heavy_kb);
+                     gl1, gc, heavy_kb, nn);
   hipLaunchKernelGGL(cld::k_lscore<false>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, ok_list, p2_list,
-                     fall_list, counters, cflags, special, priors);
+                     fall_list, counters, cflags, special, priors, nn);
   hipLaunchKernelGGL(cld::k_lgroup<false>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl1, gc, counters, cflags,
                      special, priors);
   hipLaunchKernelGGL(cld::k_lfinish<false>, gst, bst, 0, s, d_T, list, out, pool, meta, par_lists, nn, gl2, gc,
                      p2_list, fall_list, counters, cflags);
   hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,
-                     requeue2, counters);
+                     requeue2, counters, nn);
   hipLaunchKernelGGL(cld::k_lscore<true>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, p2_list, p2_list,
-                     fall_list, counters, cflags, special, priors);
+                     fall_list, counters, cflags, special, priors, nn);
   hipLaunchKernelGGL(cld::k_lgroup<true>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl2, gc, counters, cflags,
                      special, priors);
   hipLaunchKernelGGL(cld::k_lfinish<true>, gst, bst, 0, s, d_T, list, out, pool, meta, par_lists, nn, gl2, gc,

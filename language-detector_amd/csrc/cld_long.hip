@@ -2868,7 +2868,17 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
 // A document's region: StHdr, the spans back to back (each followed by its
 // pads and NULs, 16-byte aligned), then the span table (one u64 per span:
 // offset in the region | text_bytes << 32 | ulscript << 56).
-constexpr int kParMin = 48, kParG = 16;      // span-parallel documents: > kParMin spans, kParG spans per group
+#ifndef LNG_PAR_MIN
+#define LNG_PAR_MIN 48
+#endif
+constexpr int kParMin = LNG_PAR_MIN, kParG = 16;   // span-parallel documents: > kParMin spans, kParG spans per group
+// Batches of pages (long documents of 8 KB and more on average, k_lspan)
+// split only documents of more than kParMinPages spans: scored whole, a
+// typical 200-span 16 KB page costs less than its groups plus their boost-ring
+// reconstruction, and the heavy-first lists keep it out of the tail (C3:
+// 73.0 -> 64.7 ms; C5, whose many-span documents stand out from the rest,
+// keeps kParMin: 400 there took 44.1 -> 45.8 ms; profiles/round5_par_ab.txt).
+constexpr int kParMinPages = 400;
 struct StHdr {
   uint32_t nsp, careful, tab;
   uint32_t par;                                  // span-parallel documents: offset of the record arrays, else 0
@@ -2881,7 +2891,7 @@ __device__ __forceinline__ int st_advance(int tb) { return (tb + 48 + 15) & ~15;
 // region of the store taken from *pool_units (16-byte units).  Returns the
 // region's byte offset, or kStNone: the fused kernel takes the document.
 __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& dv, Slot& S, uint8_t* pool, uint64_t pool_units,
-                             uint32_t* pool_ctr, int lane) {
+                             uint32_t* pool_ctr, int lane, int par_min = kParMin) {
   bool careful;
   if (!classify(T, dv, S, careful, lane)) return kStNone;
   int next = 0, nsp = 0, cur = 0, rlo = -1;
@@ -2909,7 +2919,7 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   // or 50 unigrams, a round <= 1000 hits: chunks <= tb / 40 + rounds)
   uint32_t par = 0, recs = 0;
   uint64_t bytes = sizeof(StHdr) + cur + 8ull * nsp;
-  if (nsp > kParMin) {
+  if (nsp > par_min) {
     par = (uint32_t)bytes;
     for (int j = 0; j < nsp; ++j) recs += (uint32_t)(ufl(S.sp_tb[j]) / 16 + 8);
     bytes += 4ull * (2 * nsp + 1);
@@ -2965,7 +2975,7 @@ __device__ __forceinline__ uint64_t st_big_bytes(uint64_t L) {
   return sizeof(StHdr) + tc + 8ull * ns + 4ull * (2 * ns + 1) + 8 + 8 * (tc / 16 + 8ull * ns) + 8 * (L / 64 + 2) + 64;
 }
 __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& dv, Slot& S, uint8_t* region,
-                                             int lane) {
+                                             int lane, int par_min = kParMin) {
   const uint64_t L = (uint64_t)dv.len, tc = st_big_text(L), tab_off = sizeof(StHdr) + tc, ns = st_big_spans(L);
   const uint64_t par_off = tab_off + 8ull * ns;
   uint64_t* lsm = reinterpret_cast<uint64_t*>(region + ((st_big_bytes(L) - 8 * (L / 64 + 2) - 64) & ~7ull));
@@ -2989,7 +2999,7 @@ __device__ __forceinline__ bool st_spans_big(const DevTables& T, const DocView& 
   }
   gsync();
   uint32_t par = 0;
-  if (nsp > kParMin) {
+  if (nsp > par_min) {
     par = (uint32_t)par_off;
     if (lane == 0) {
       uint32_t* roff = reinterpret_cast<uint32_t*>(region + par);
