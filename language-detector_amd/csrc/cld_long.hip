@@ -2894,6 +2894,9 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
                              uint32_t* pool_ctr, int lane, int par_min = kParMin) {
   bool careful;
   if (!classify(T, dv, S, careful, lane)) return kStNone;
+#if defined(LNG_LAB_STOP) && LNG_LAB_STOP == 1
+  return kStNone;                                // (lab builds only: stage timing)
+#endif
   int next = 0, nsp = 0, cur = 0, rlo = -1;
   for (;;) {
     if (cur + kLB > kLbdCap || nsp >= kMaxSpans) return kStNone;
@@ -2913,6 +2916,9 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
     cur += st_advance(tb);
   }
   gsync();
+#if defined(LNG_LAB_STOP) && LNG_LAB_STOP == 2
+  return kStNone;                                // (lab builds only: stage timing)
+#endif
   // span-parallel documents (more than kParMin spans): after the span table,
   // roff[nsp + 1] (first record of span j), rcnt[nsp], then the records --
   // at most tb / 16 + 8 DocTote adds per span (a chunk holds >= 20 base hits
