@@ -2874,11 +2874,15 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
 constexpr int kParMin = LNG_PAR_MIN, kParG = 16;   // span-parallel documents: > kParMin spans, kParG spans per group
 // Batches of pages (long documents of 8 KB and more on average, k_lspan)
 // split only documents of more than kParMinPages spans: scored whole, a
-// typical 200-span 16 KB page costs less than its groups plus their boost-ring
+// 200-760-span 16 KB page costs less than its groups plus their boost-ring
 // reconstruction, and the heavy-first lists keep it out of the tail (C3:
-// 73.0 -> 64.7 ms; C5, whose many-span documents stand out from the rest,
-// keeps kParMin: 400 there took 44.1 -> 45.8 ms; profiles/round5_par_ab.txt).
-constexpr int kParMinPages = 400;
+// 73.0 ms at 48, 64.7 at 400, 63.3 at 2000; C5, whose many-span documents
+// stand out from the rest, keeps kParMin: 400 there took 44.1 -> 45.8 ms;
+// profiles/round5_par_ab.txt).
+#ifndef LNG_PAR_MIN_PAGES
+#define LNG_PAR_MIN_PAGES 2000
+#endif
+constexpr int kParMinPages = LNG_PAR_MIN_PAGES;
 struct StHdr {
   uint32_t nsp, careful, tab;
   uint32_t par;                                  // span-parallel documents: offset of the record arrays, else 0
