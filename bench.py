@@ -11,9 +11,16 @@ host-memory path (cld_detect_batch: pinned staging, chunked upload / kernels /
 download on three streams) on C2 as "host_path".  --config c3/c4/c5 makes
 another config the headline instead.
 
-One process per GPU (torch.distributed, RCCL backend for the barrier and the
-max-over-ranks timing only -- the path itself has no collective): each rank
-scores its own shard of documents (weak scaling).  Rank 0 prints one JSON line.
+One process per GPU: `--gpus N` (N > 1) run without a torch.distributed
+environment starts N ranks itself -- it counts the visible GPUs (without
+initialising one), refuses N larger than that, and runs
+`python -m torch.distributed.run --nproc-per-node N` on this same command line
+as a child process, exiting with its code; under an existing launcher
+(WORLD_SIZE set) `--gpus` must equal WORLD_SIZE.  RCCL carries only the
+barrier, the max-over-ranks timing and the per-rank kernel times -- the path
+itself has no collective: each rank scores its own shard of documents (weak
+scaling).  Rank 0 prints one JSON line, with every rank's kernel time in
+"per_rank".
 
 Tables: the synthetic Q1 quadgram table, opted into explicitly
 (CLD_MI355X_TABLES) so every quadgram branch does work; the library's own
@@ -133,48 +140,110 @@ def pmc_summary(cfg):
         return json.load(f).get(cfg)
 
 
-def measure(cfg_name, n, steps, warmup, rank, dist, dev):
+class HipBackend:
+    """The product path on this rank's GPU: torch for HBM buffers and the
+    stream sync, the library's C ABI (cld_detect_batch_device) for the work."""
+    dist_backend = "nccl"
+
+    def __init__(self, local):
+        import torch
+        import cld_amd
+        self.torch, self.cld = torch, cld_amd
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        cld_amd.init_device(local)
+
+    @staticmethod
+    def device_count():
+        import torch
+        return torch.cuda.device_count()          # does not initialise a GPU on this image
+
+    def upload(self, arr):
+        return self.torch.from_numpy(arr).to(self.dev)
+
+    def empty(self, nbytes):
+        return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.dev)
+
+    def detect(self, d_buf, d_offs, n, d_out):
+        self.cld.detect_batch_device(0, d_buf.data_ptr(), d_offs.data_ptr(), n, d_out.data_ptr(), None)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def kernel_times(self):
+        return self.cld.kernel_times(0)
+
+    def last_stats(self):
+        return self.cld.last_stats(0)
+
+    def version(self):
+        return self.cld.version()
+
+
+def backend_class():
+    """HipBackend, or the class `Backend` of the file CLD_BENCH_MOCK names (the
+    CPU tests of the launcher and rank logic: tests/bench_mock.py)."""
+    mock = os.environ.get("CLD_BENCH_MOCK")
+    if not mock:
+        return HipBackend
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("cld_bench_mock", mock)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.Backend
+
+
+def measure(cfg_name, n, steps, warmup, rank, dist, be):
     import torch
     import cld_amd
     import corpus
     cfg = CONFIGS[cfg_name]
     buf, offs = corpus.GENERATORS[cfg_name](n, seed=corpus.SEEDS[cfg_name] + 7919 * rank)
-    d_buf = torch.from_numpy(buf).to(dev)
-    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-    d_out = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+    d_buf = be.upload(buf)
+    d_offs = be.upload(offs.view(np.int64))
+    d_out = be.empty(n * 40)
 
     def step():
-        cld_amd.detect_batch_device(0, d_buf.data_ptr(), d_offs.data_ptr(), n, d_out.data_ptr(), None)
+        be.detect(d_buf, d_offs, n, d_out)
 
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    cld_amd.kernel_times(0)                      # reset the event accumulator
+    be.sync()
+    be.kernel_times()                            # reset the event accumulator
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    be.sync()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
     elapsed = t1 - t0
+    ms, launches = be.kernel_times()
+    per = [m / max(1, launches) for m in ms]
+    per_rank = None
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=be.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ms, launches = cld_amd.kernel_times(0)
-    stats = cld_amd.last_stats(0)
-    per = [m / max(1, launches) for m in ms]
+        # every rank's own wall time and kernel times, for balance checks of a multi-GPU record
+        mine = torch.tensor([float(rank), t1 - t0] + per + [float(n), float(offs[-1])],
+                            dtype=torch.float64, device=be.dev)
+        allr = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": int(v[0]), "elapsed_s": float(v[1]), "wave_ms": float(v[2]), "long_ms": float(v[3]),
+                     "general_ms": float(v[4]), "docs": int(v[5]), "doc_bytes": int(v[6])}
+                    for v in (x.cpu().tolist() for x in allr)]
+    stats = be.last_stats()
     doc_bytes = int(offs[-1])
     alg_bytes = doc_bytes + ALG_BYTES_PER_DOC * n
     kern_ms = per[cfg["kernel"]]                 # the dominant kernel's average launch
-    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
     pmc = pmc_summary(cfg_name)
     traffic = issue = None
-    if pmc and pmc.get("docs") == n:
+    if pmc and pmc.get("docs") == n and kern_ms > 0:
         traffic = pmc.get("hbm_bytes_per_launch")
         c = pmc.get("counters_per_launch", {})
         if "SQ_INSTS_VALU" in c:
@@ -198,8 +267,9 @@ def measure(cfg_name, n, steps, warmup, rank, dist, dev):
         "roofline": {"bound": "hbm", "kernel": cfg["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes, "issue": issue},
+        "per_rank": per_rank,
     }
-    gpu_out = d_out.cpu().numpy().view(cld_amd.RESULT_DTYPE) if rank == 0 else None
+    gpu_out = (d_out.cpu().numpy().view(cld_amd.RESULT_DTYPE) if rank == 0 else None)
     del d_buf, d_offs, d_out
     return res, buf, offs, gpu_out
 
@@ -234,6 +304,24 @@ def host_path(n, steps, rank):
     return out
 
 
+def launch_ranks(n, Backend):
+    """`--gpus n` without a launcher: n ranks under torch.distributed.run, as a
+    child process (nothing here has touched a GPU), with this command line.
+    Returns the exit code."""
+    import socket
+    import subprocess
+    have = Backend.device_count()
+    if have < n:
+        print("bench.py: --gpus %d asked, but %d GPU(s) are visible; not measuring" % (n, have), file=sys.stderr)
+        return 3
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,26 +334,32 @@ def main():
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 sub-measurement of a C2 run")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory path measurement")
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    Backend = backend_class()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, Backend))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            sys.exit("bench.py: --gpus %d but the launcher started %d rank(s) (WORLD_SIZE); refusing a "
+                     "line whose n_gpus would not be what was asked" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    import cld_amd
-    cld_amd.init_device(local)
+        dist.init_process_group(backend=Backend.dist_backend)
+    be = Backend(local)
 
     cfg = CONFIGS[args.config]
     n = args.docs or cfg["docs"]
     steps = args.steps or cfg["steps"]
-    head, buf, offs, gpu_out = measure(args.config, n, steps, args.warmup, rank, dist, dev)
+    head, buf, offs, gpu_out = measure(args.config, n, steps, args.warmup, rank, dist, be)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, buf, offs, gpu_out, args.cpu_seconds,
@@ -275,16 +369,17 @@ def main():
     sub = None
     if args.config == "c2" and not args.no_sub:
         c3n = CONFIGS["c3"]["docs"] if not args.docs else max(1000, args.docs // 10)
-        r3, b3, o3, g3 = measure("c3", c3n, CONFIGS["c3"]["steps"], 1, rank, dist, dev)
+        r3, b3, o3, g3 = measure("c3", c3n, CONFIGS["c3"]["steps"], 1, rank, dist, be)
         sub = {"metric": "docs/sec", "value": r3["value"] * world, "unit": "docs/s",
                "workload": CONFIGS["c3"]["workload"], "docs_per_gpu": c3n, "steps": r3["steps"],
                "ms_per_step": r3["elapsed"] / r3["steps"] * 1e3, "input_GBps": r3["input_GBps"] * world,
                "passes_hist": r3["passes_hist"], "kernels": r3["kernels"], "roofline": r3["roofline"],
+               "per_rank": r3["per_rank"],
                "cpu_baseline": (cpu_baseline("c3", b3, o3, g3, args.cpu_seconds, 4_000)
                                 if rank == 0 and world == 1 and not args.no_cpu_baseline else None)}
         del b3, o3, g3
     host = None
-    if args.config == "c2" and not args.no_host and rank == 0:
+    if args.config == "c2" and not args.no_host and world == 1:
         host = host_path(n, 10, rank)
         host["kernel_only_docs_per_s"] = head["value"]
         host["pinned_vs_kernel_only"] = host["pinned"]["value"] / head["value"]
@@ -309,14 +404,16 @@ def main():
                 "the synthetic Q1 (the real quadchrome table is a missing blob))",
         "config": {"workload": cfg["workload"], "docs_per_gpu": n, "bytes_per_gpu": head["doc_bytes"],
                    "mean_doc_bytes": head["doc_bytes"] / n, "parallelism": "document shards, %d rank(s)" % world},
-        "input_GBps": head["input_GBps"] * world,
+        "input_GBps": (sum(r["doc_bytes"] for r in head["per_rank"]) * steps / head["elapsed"] / 1e9
+                       if head["per_rank"] else head["input_GBps"]),
         "passes_hist": head["passes_hist"],
         "kernels": head["kernels"],
         "roofline": head["roofline"],
+        "per_rank": head["per_rank"],
         "cpu_baseline": cpu,
         "c3": sub,
         "host_path": host,
-        "tables": cld_amd.version(),
+        "tables": be.version(),
     }
     print(json.dumps(line), flush=True)
     if dist:

@@ -48,23 +48,25 @@ struct CoReq {
   int rc = 0;
   enum { kWaiting = 0, kDone = 1, kLead = 2 };
   std::atomic<int> state{kWaiting};
-  std::atomic<bool> parked{false};   // asleep (or about to be) on cv: post() must notify
   std::mutex m;
   std::condition_variable cv;
   bool promoted = false;         // under the queue lock: already asked to lead
   CoReq* kid[2] = {nullptr, nullptr};
   CoReq(const uint8_t* b, const uint64_t* o, size_t n_, void* r, uint32_t f, bool t)
       : buf(b), offs(o), n(n_), out(r), flags(f), tiny(t) {}
-  // state and parked are sequentially consistent (a Dekker pair): post()
-  // stores state then reads parked, park() stores parked then reads state, so
-  // either the poster sees the sleeper or the sleeper sees the state.
+  // Lifetime rule: a CoReq lives on its caller's stack and dies when park()
+  // (or settle()) returns kDone, so the poster must be finished with the
+  // object by then.  post() stores the state and notifies while holding m,
+  // and the waiter always takes m once after it sees a new state (in cv.wait,
+  // or in settle() when the spin saw it), so it cannot return while a poster
+  // is still inside post().
   void post(int st) {
+    std::lock_guard<std::mutex> l(m);
     state.store(st);
-    if (parked.load()) {
-      std::lock_guard<std::mutex> l(m);
-      cv.notify_one();
-    }
+    cv.notify_one();
   }
+  // Waits for a poster that may still hold m (see above).
+  void settle() { std::lock_guard<std::mutex> l(m); }
   // Spins up to spin_us first (a GPU round trip is tens of microseconds: most
   // waits end before a sleep and a wake-up would), then sleeps.
   int park(int spin_us) {
@@ -78,17 +80,18 @@ struct CoReq {
         }
       }
     }
-    if (st == kWaiting) {
+    {
       std::unique_lock<std::mutex> l(m);
-      parked.store(true);
       cv.wait(l, [&] { return (st = state.load()) != kWaiting; });
-      parked.store(false);
     }
     // a lead request is consumed here; if a dispatcher ran the request in the
     // meantime its kDone stays (a plain store would lose it)
     if (st == kLead) {
       int expect = kLead;
-      if (!state.compare_exchange_strong(expect, kWaiting)) st = expect;
+      if (!state.compare_exchange_strong(expect, kWaiting)) {
+        st = expect;
+        if (st == kDone) settle();
+      }
     }
     return st;
   }
@@ -119,6 +122,7 @@ class Coalescer {
     for (;;) {
       if (me->done()) {                        // a promoted caller whose request another dispatcher ran
         lk.unlock();
+        me->settle();
         me->wake_kids();
         return me->rc;
       }
@@ -169,6 +173,10 @@ class Coalescer {
   bool form_group(std::vector<CoReq*>* grp) {
     const bool any_slot = active_ < slots_any.load(std::memory_order_relaxed);
     if (q_.empty() || !(any_slot || active_ < slots_tiny.load(std::memory_order_relaxed))) return false;
+    // Only tiny slots free and a non-tiny request at the head of the queue
+    // (the oldest): keep the slot, so that request takes the next free 'any'
+    // slot instead of waiting behind a stream of tiny groups.
+    if (!any_slot && !q_.front()->tiny) return false;
     const CoReq* first = nullptr;
     for (CoReq* r : q_)
       if (any_slot || r->tiny) {

@@ -806,8 +806,8 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       // (gcap each; a document whose groups find no room takes the fused kernel)
       const size_t np = std::max<size_t>(n, 1), gcap = std::max<size_t>(4 * np, 1u << 16);
       if (grow(&d->d_parlists, &d->parlists_cap, 2 * np + 4 * gcap)) return CLD_ENOMEM;
-      // a list of at most 4 documents per fused wave goes whole to the fused
-      // kernel: small batches keep its two-wave speculation (section 6)
+      // a list of at most small_long_list() documents (64) goes whole to the
+      // fused kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
                                priors, hbuf, hflag, hpos, hgap, d->fault_doc, small_long_list(d),
@@ -2391,7 +2391,17 @@ const char* detect_language(const char* text) {
   const char* t = text ? text : "";
   const uint64_t offs[2] = {0, (uint64_t)strlen(t)};
   cld_result res{};
-  const int rc = cld_detect_batch((const uint8_t*)t, offs, 1, &res, 0);
+  int rc = cld_detect_batch((const uint8_t*)t, offs, 1, &res, 0);
+  if (rc != CLD_OK && !(rc == CLD_EIO && res.summary_lang == CLD_LANG_FAILED)) {
+    // A coalesced call returns its whole group's code: a failure of the
+    // group (e.g. CLD_ENOMEM growing the pinned arena for other callers'
+    // batches) is not this document's.  Redo it alone, outside the coalescer,
+    // and abort only if that fails too.
+    std::shared_lock<std::shared_mutex> tl(g_swap_mu);
+    Picked p(pick_context());
+    res = cld_result{};
+    rc = run_host_shard_isolating(p.d, (const uint8_t*)t, offs, 1, &res, 0);
+  }
   std::shared_lock<std::shared_mutex> tl(g_swap_mu);
   if (rc == CLD_EIO && res.summary_lang == CLD_LANG_FAILED) {
     fprintf(stderr, "cld_mi355x: detect_language: no result for a document; answering \"en\"\n");

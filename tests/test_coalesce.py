@@ -29,3 +29,26 @@ def test_every_caller_gets_its_own_results(sim, callers, spin, wake):
     assert d["wrong"] == 0 and d["calls"] == callers * calls
     if callers >= 64:
         assert d["docs_per_group"] > 2          # requests did coalesce
+
+
+@pytest.fixture(scope="module")
+def sim_sanitized():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools"), "build/coalesce_sim_tsan",
+                    "build/coalesce_sim_asan"], check=True)
+    return {k: os.path.join(ROOT, "tools", "build", "coalesce_sim_" + k) for k in ("tsan", "asan")}
+
+
+@pytest.mark.parametrize("san,callers,spin,wake", [("tsan", 64, 50, "tree"), ("tsan", 32, 0, "direct"),
+                                                   ("asan", 128, 0, "direct"), ("asan", 64, 50, "tree")])
+def test_mixed_requests_under_sanitizers(sim_sanitized, san, callers, spin, wake):
+    """Tiny and non-tiny requests with two flag values, each request a heap
+    object freed the moment submit() returns: a poster still touching it (the
+    round-5 post()/park() race) is a report from ThreadSanitizer or
+    AddressSanitizer.  Non-tiny requests must not starve behind tiny groups."""
+    r = subprocess.run([sim_sanitized[san], str(callers), "40", "30", "sleep", "1", "2", str(spin), wake, "mixed"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "Sanitizer" not in r.stderr, r.stdout + r.stderr[-4000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["wrong"] == 0 and d["calls"] == callers * 40 and d["non_tiny_calls"] == callers // 4 * 40
+    # a non-tiny request waits for at most a few groups, not for the tiny stream to dry up
+    assert d["non_tiny_latency_us_p99"] < 4 * d["latency_us_p99"] + 20000
