@@ -8,6 +8,8 @@
 #   req    request-sized batch rates (tools/req_rate.py)
 #   rates  HTML and vector-mode rates
 #   gpus2  bench.py --gpus 2 on this 1-GPU box: must refuse (exit 3), print no line
+#   tabsize  C2 / C3 lines and L2 hit counters with Q1 and its larger-table variants
+#            (tools/synth_quad.py SYNQ_BUCKETS; language-detector_amd/data/variants/)
 # Every GPU step has its own limit; the first failure ends the script.
 set -u
 TAG=${TAG:-r6a}
@@ -45,6 +47,14 @@ for s in ${STEPS:-suite smoke bench}; do
       step 400 vec_rate.jsonl python3 tools/vec_rate.py ;;
     gpus2) timeout -k 10 120 python bench.py --gpus 2 --docs 1000 --steps 1 > $O/gpus2.txt 2>&1; rc=$?
            echo "rc=$rc" >> $O/gpus2.txt; cat $O/gpus2.txt; [ $rc -eq 3 ] || exit 1 ;;
+    tabsize)
+      for t in ${TABS:-language-detector_amd/data/cld2_synth_q1.cldt language-detector_amd/data/variants/cld2_synth_q1_b65536.cldt language-detector_amd/data/variants/cld2_synth_q1_b262144.cldt language-detector_amd/data/variants/cld2_synth_q1_b1048576.cldt}; do
+        b=$(basename $t .cldt)
+        step 300 tab_${b}_c2.json env CLD_MI355X_TABLES=$R/$t python bench.py --cpu-seconds 3 --no-host --no-sub
+        step 300 tab_${b}_c3.json env CLD_MI355X_TABLES=$R/$t python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
+        (cd /tmp && step 120 tab_${b}_pmc_c2.log env CLD_MI355X_TABLES=$R/$t rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_wave -d $O/tab_${b}_pmc_c2 -o c2 --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1
+        (cd /tmp && step 120 tab_${b}_pmc_c3.log env CLD_MI355X_TABLES=$R/$t rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_l(span|score|group|finish|rep|ong)" -d $O/tab_${b}_pmc_c3 -o c3 --output-format csv -- python3 $R/bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -21,6 +21,10 @@ data exists in this environment.  This tool derives a deterministic stand-in
 Outputs (all deterministic):
   language-detector_amd/data/cld2_synth_q1.cldt   base blob + QUAD/QUAD2 + provenance
   language-detector_amd/data/vocab.json         {lang_code: [words...]} for synthetic text
+
+Table-size variants (the same quads in a larger table, for the sensitivity of
+the probe gathers to table size): SYNQ_BUCKETS=<table-1
+buckets> SYNQ_OUT=<path> writes only that blob (table 2 keeps 8,192 buckets).
 """
 import json
 import os
@@ -37,7 +41,7 @@ import cldt  # noqa: E402
 REF = "/root/reference/cld2/internal"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-QUAD1_BUCKETS = 16384          # 256 KB of buckets; ~90% load -> real dual-table traffic
+QUAD1_BUCKETS = int(os.environ.get("SYNQ_BUCKETS", 16384))   # 256 KB of buckets; ~90% load -> real dual-table traffic
 QUAD2_BUCKETS = 8192
 KEYMASK = 0xFFFF0000
 # Quantised log-probs: calibrated so per-KB chunk scores sit near the reference's
@@ -178,8 +182,11 @@ def main():
     sections.append((cldt.QUAD2, cldt.table_section_bytes(size_one, QUAD2_BUCKETS, KEYMASK, 20261015, b2, ind)))
     sections.append((cldt.PROVENANCE, prov.encode()))
     sections.sort(key=lambda s: s[0])
-    out = os.path.join(ROOT, "language-detector_amd/data/cld2_synth_q1.cldt")
+    out = os.environ.get("SYNQ_OUT") or os.path.join(ROOT, "language-detector_amd/data/cld2_synth_q1.cldt")
     cldt.write_blob(out, sections)
+    if os.environ.get("SYNQ_OUT"):
+        print(prov)
+        return
 
     # Q0: the reference's own empty-table pattern (generated_distinct_bi_0.cc:22-48)
     empty = cldt.table_section_bytes(1, 1, 0xFFFFFFFF, 20130101, np.zeros((1, 4)), [0])
