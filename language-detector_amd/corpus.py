@@ -23,7 +23,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SEEDS = {"c2": 0xC1D20002, "c3": 0xC1D20003, "c4": 0xC1D20004, "c5": 0xC1D20005}
+SEEDS = {"c2": 0xC1D20002, "c3": 0xC1D20003, "c4": 0xC1D20004, "c5": 0xC1D20005, "c2n": 0xC1D20012}
 
 C2_LANGS = ["en", "fr", "de", "es", "it", "pt", "nl", "sv", "da", "no", "fi", "pl", "cs", "ro", "hu", "tr"]
 C3_SCRIPTS = {
@@ -287,13 +287,22 @@ HTML_ENTITIES = [b"&amp;", b"&lt;", b"&gt;", b"&quot;", b"&nbsp;", b"&eacute;", 
                  b"&lang", b"&lang;", b"&amp", b"&auml", b"&#150;", b"&#xFFFE;", b"&#55296;"]
 
 
-def html(n, seed=0xC1D20006, lo=200, hi=6000):
+# 4-byte characters for HTML pages (emoji, CJK extension B letters, Gothic and
+# mathematical alphanumeric letters), raw and as numeric entities
+FOUR_BYTE = ["\U0001F600", "\U0001F389", "\U0001F44D", "\u2764\uFE0F", "\U0001F1EB\U0001F1F7", "\U00020000",
+             "\U00020B9F\U0002A6A5", "\U00010330\U00010331\U00010332", "\U0001D400\U0001D401", "\U0001F4AF!"]
+FOUR_BYTE_ENT = [b"&#x1F600;", b"&#128512;", b"&#x20000;", b"&#x1D41A;", b"&#X1F389", b"&#x10330;"]
+
+
+def html(n, seed=0xC1D20006, lo=200, hi=6000, emoji=0.0):
     """HTML pages for the is_plain_text=false path (no BASELINE config names
     it): words of one c2/c3 language wrapped in tags, with
     <script>/<style>/<!-- --> blocks, quoted attributes (some with CR/LF),
     lang= / meta content-language attributes, named and numeric entities, and
     stray '<' / '>' -- every construct the reference's tag parser and entity
-    reader distinguish (getonescriptspan.cc:150-541)."""
+    reader distinguish (getonescriptspan.cc:150-541).  emoji: the fraction of
+    pages that also carry 4-byte characters (FOUR_BYTE, raw and as entities)
+    between their words."""
     rng = np.random.default_rng(seed)
     v = vocab()
     langs = [l for l in C2_LANGS + sum(C3_SCRIPTS.values(), []) if l in v]
@@ -305,9 +314,16 @@ def html(n, seed=0xC1D20006, lo=200, hi=6000):
         out = [b"<html lang=\"" + lang.encode() + b"\"><head><title>"]
         if rng.random() < 0.3:
             out.append(b'<meta http-equiv="content-language" content="' + lang.encode() + b'">')
+        four = emoji > 0 and rng.random() < emoji
         while sum(map(len, out)) < target:
             r = rng.random()
-            if r < 0.55:
+            if four and rng.random() < 0.08:
+                if rng.random() < 0.75:
+                    t = FOUR_BYTE[int(rng.integers(0, len(FOUR_BYTE)))].encode("utf-8")
+                    out.append(t + (b" " if rng.random() < 0.6 else b""))
+                else:
+                    out.append(FOUR_BYTE_ENT[int(rng.integers(0, len(FOUR_BYTE_ENT)))])
+            elif r < 0.55:
                 k = int(rng.integers(1, 9))
                 ws = [words[int(i)] for i in rng.integers(0, len(words), size=k)]
                 if rng.random() < 0.2:
@@ -348,4 +364,23 @@ def html(n, seed=0xC1D20006, lo=200, hi=6000):
     return (np.frombuffer(b"".join(docs), dtype=np.uint8).copy() if n else np.zeros(0, np.uint8)), offs
 
 
-GENERATORS = {"c2": c2, "c3": c3, "c4": c4, "c5": c5}
+def c2n(n, seed=SEEDS["c2n"]):
+    """C2's tweets with every ASCII letter of a document shifted by the same
+    random non-zero amount (a Caesar shift per document): the same lengths,
+    scripts and word shapes, but words the tables never saw -- nearly every
+    quadgram probe misses and lands on a uniformly random bucket, so the probe
+    gathers see the whole quad table (table-size sensitivity, DESIGN.md
+    section 7; not a BASELINE config)."""
+    buf, offs = c2(n, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    k = rng.integers(1, 26, size=n).astype(np.int16)
+    per = np.repeat(k, np.diff(offs).astype(np.int64))
+    b = buf.astype(np.int16)
+    lo = (b >= 97) & (b <= 122)
+    up = (b >= 65) & (b <= 90)
+    b[lo] = (b[lo] - 97 + per[lo]) % 26 + 97
+    b[up] = (b[up] - 65 + per[up]) % 26 + 65
+    return b.astype(np.uint8), offs
+
+
+GENERATORS = {"c2": c2, "c3": c3, "c4": c4, "c5": c5, "c2n": c2n}

@@ -20,8 +20,10 @@
 //     on an entity saw the raw '&' (script 0): the rewrite marks those
 //     positions in hflag, and the span builders read script 0 there;
 //   * the lowercaser's HTML half: a page holding a character whose HTML-mode
-//     lowering differs (kCptHtmlLower), a 4-byte or malformed character, or
-//     more than kHtmlRewriteMax bytes is not rewritten and stays on k_general;
+//     lowering differs (kCptHtmlLower; for 4-byte characters one flag for the
+//     whole range, k_build_cpt4 -- the reference's tables set neither), a
+//     malformed character, or more than kHtmlRewriteMax bytes is not
+//     rewritten and stays on k_general;
 //   * the span soft limit reads the raw bytes left (:814-819); it splits
 //     nothing below kMaxScriptBytes (40,928), and for longer pages the rewrite
 //     also records each output byte's page offset (hpos, with hgap after
@@ -76,11 +78,16 @@ constexpr int kHtmlStage = HTML_STAGE;  // pages up to this size are staged in L
 constexpr int kHtmlCands = HTML_CANDS;  // '<' / '&' candidates per segment of a page (round 5: any number per page)
 constexpr int kHtmlWPB = HTML_WPB;      // waves (pages) per workgroup
 
-// The character b0 b1 b2 (n bytes) lowers the same way in HTML mode as in plain text.
-__device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0, uint32_t b1, uint32_t b2, int n) {
-  if (n > 3) return false;
+// The character b0 b1 b2 b3 (n bytes) is well formed and lowers the same way
+// in HTML mode as in plain text: a property-table bit for 1-3 byte
+// characters, one flag for the whole 4-byte range (k_build_cpt4; never set by
+// the reference's tables, so pages with emoji and other 4-byte characters are
+// rewritten like any other page).
+__device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
+                                                int n) {
   if (n >= 2 && (b1 & 0xC0) != 0x80) return false;
-  if (n == 3 && (b2 & 0xC0) != 0x80) return false;
+  if (n >= 3 && (b2 & 0xC0) != 0x80) return false;
+  if (n == 4) return (b3 & 0xC0) == 0x80 && (gld(T.cpt + lng::kCptSize) & 1) == 0;
   return (gld(T.cpt + wave::cpt_index(b0, b1, b2, n)) & lng::kCptHtmlLower) == 0;
 }
 
@@ -201,7 +208,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
           kind = 1;
           ln = tlen;
           dec = (uint32_t)tmp[0] | ((uint32_t)tmp[1] << 8) | ((uint32_t)tmp[2] << 16) | ((uint32_t)tmp[3] << 24);
-          bd = !html_lower_same(T, tmp[0], tmp[1], tmp[2], plen) ||
+          bd = !html_lower_same(T, tmp[0], tmp[1], tmp[2], tmp[3], plen) ||
                (tmp[0] < 0x80 && (((tmp[0] < 64 ? am0 : am1) >> (tmp[0] & 63)) & 1));
         } else {
           kind = 2;                                            // undecodable: the '&' is dropped
@@ -300,8 +307,9 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
           ++conts;
         } else {
           const int mm = utf8_len((uint8_t)c);
-          const uint32_t b1 = txt_at<kStaged>(txt, p + 1, L), b2 = txt_at<kStaged>(txt, p + 2, L);
-          bad |= (p + mm > L || !html_lower_same(T, c, b1, b2, mm)) ? 1 : 0;
+          const uint32_t b1 = txt_at<kStaged>(txt, p + 1, L), b2 = txt_at<kStaged>(txt, p + 2, L),
+                         b3 = mm == 4 ? txt_at<kStaged>(txt, p + 3, L) : 0u;
+          bad |= (p + mm > L || !html_lower_same(T, c, b1, b2, b3, mm)) ? 1 : 0;
           need += mm - 1;
         }
       } else if (reached && kind == 0) {

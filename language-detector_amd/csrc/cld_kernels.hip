@@ -834,12 +834,32 @@ __global__ __launch_bounds__(256) void k_build_cpt(DevTables T, uint64_t* __rest
   out[i] = lng::cpt_eval(T, b, n);
 }
 
+// The flags word after the property table (T.cpt[kCptSize]): bit 0 = some
+// 4-byte sequence (lead F0-F7, three continuation bytes) lowers differently in
+// HTML mode than in plain text (the HTML half of a remap pair,
+// utf8statetable.cc:755-762).  The reference's tables have none, so HTML pages
+// with 4-byte characters take the rewrite (cld_html.hip html_lower_same).
+__global__ __launch_bounds__(256) void k_build_cpt4(DevTables T, uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 8 << 18) return;
+  const uint8_t b[4] = {(uint8_t)(0xF0 | (i >> 18)), (uint8_t)(0x80 | ((i >> 12) & 63)),
+                        (uint8_t)(0x80 | ((i >> 6) & 63)), (uint8_t)(0x80 | (i & 63))};
+  uint8_t lp[16], lh[16];
+  const int fp = lower_replace_sm(T.lower, b, 4, lp, 16, true), fh = lower_replace_sm(T.lower, b, 4, lh, 16, false);
+  bool diff = fp != fh;
+  for (int k = 0; k < fp && k < 16; ++k) diff |= lp[k] != lh[k];
+  if (diff) atomicOr(reinterpret_cast<unsigned int*>(out + lng::kCptSize), 1u);
+}
+
 }  // namespace cld
 
 extern "C" {
-size_t cld_cpt_entries() { return cld::lng::kCptSize; }
+size_t cld_cpt_entries() { return cld::lng::kCptSize + 1; }   // + the flags word (k_build_cpt4)
 hipError_t cld_build_cpt(const DevTables* T, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(cld::k_build_cpt, dim3((cld::lng::kCptSize + 255) / 256), dim3(256), 0, s, *T, out);
+  hipError_t e = hipMemsetAsync(out + cld::lng::kCptSize, 0, sizeof(uint64_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cld::k_build_cpt4, dim3((8 << 18) / 256), dim3(256), 0, s, *T, out);
   return hipGetLastError();
 }
 size_t cld_keytab_entries() { return 256 * 256; }

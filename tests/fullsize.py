@@ -27,7 +27,7 @@ CORPORA = {
     "c3": ("c3", 100_000),
     "c4": ("c4", 1_100_000),
     "c5": ("c5", 200_000),
-    "html": ("html", 100_000),      # HTML pages (is_plain_text = false), as tools/parity_scale.py sweeps them
+    "html": ("html", 100_000),      # HTML pages (is_plain_text = false), a quarter with 4-byte characters
 }
 
 
@@ -83,7 +83,7 @@ def _generate(name, outdir):
     import corpus
     gen, n = CORPORA[name]
     t0 = time.time()
-    buf, offs = corpus.html(n, seed=77) if gen == "html" else corpus.GENERATORS[gen](n)
+    buf, offs = corpus.html(n, seed=77, emoji=0.25) if gen == "html" else corpus.GENERATORS[gen](n)
     bp, op, done = (os.path.join(outdir, name + s) for s in (".buf.npy", ".offs.npy", ".done"))
     np.save(bp + ".tmp.npy", buf)
     np.save(op + ".tmp.npy", offs)

@@ -49,6 +49,31 @@ def test_gpu_equals_reference_html_hints(gpu, ref):
          "c5 hints")
 
 
+def test_gpu_html_four_byte_characters_on_parallel_kernels(gpu, ref):
+    """HTML pages with emoji and other 4-byte characters (raw and as numeric
+    entities, corpus.html emoji=1): rewritten on the GPU like any other page
+    (k_build_cpt4: no 4-byte character lowers differently in HTML mode) and
+    scored by k_wave / k_long -- none on the sequential kernel -- equal to the
+    reference, with and without chunk vectors."""
+    for lo, hi, n, seed in ((200, 6000, 3000, 41), (14000, 18000, 300, 42), (41000, 90000, 40, 43)):
+        buf, offs = corpus.html(n, seed=seed, lo=lo, hi=hi, emoji=1.0)
+        assert (np.asarray(buf) >= 0xF0).sum() >= n              # 4-byte lead bytes on the pages
+        got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
+        st = gpu.last_stats(0)
+        assert st.general_docs == 0, (lo, hi, st.general_docs)
+        same(got, ref.detect_batch(buf, offs, plain=np.zeros(n, np.uint8), threads=16), "html 4-byte %d-%d" % (lo, hi))
+    buf, offs = corpus.html(1000, seed=44, emoji=1.0)
+    n = len(offs) - 1
+    res, chunks, coffs = gpu.detect_batch_vec(buf=buf, offsets=offs, html=True)
+    st = gpu.last_stats(0)
+    rres, rch, rco = ref.detect_batch_vec(buf, offs, plain=np.zeros(n, np.uint8), threads=16)
+    same(res, rres, "html 4-byte vectors")
+    assert np.array_equal(coffs.astype(np.int64), rco.astype(np.int64))
+    for f in ("offset", "bytes", "lang1"):
+        assert np.array_equal(chunks[f], rch[f])
+    assert st.long_docs >= 0.99 * n, (st.long_docs, st.general_docs)
+
+
 @pytest.mark.parametrize("flags", [0x0100, 0x4000, 0x4100], ids=["score_as_quads", "best_effort", "both"])
 def test_gpu_equals_reference_with_flags(gpu, ref, ref_tables, golden, flags):
     """CLD2's result-affecting flags (compact_lang_det.h:343-349) through every

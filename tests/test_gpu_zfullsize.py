@@ -1,7 +1,8 @@
 """Full-size parity against the reference CLD2 itself, on the tree as built:
 every document of BASELINE's C2 (1M tweets), C3 (100K 16 KB pages) and C4
 (1.1M CJK-heavy documents), 200K documents of C5's stream, and 100K HTML pages
-(is_plain_text = false, cld_detect_batch_ex), through the
+(is_plain_text = false, cld_detect_batch_ex; a quarter of them with emoji and
+other 4-byte characters, raw and as entities), through the
 product's batch entry point (cld_detect_batch: routing, k_wave, k_long,
 k_general) and through oracle/_ref/librefcld2.so (the reference's own sources
 in dynamic-data mode, 16 host threads), every result field compared.  Twice:
@@ -54,6 +55,7 @@ def test_full_size_equals_reference(gpu, ref_tables, name):
     assert not bad.any(), "%s/%s: %d of %d differ, first %s" % (name, label, bad.sum(), n, np.nonzero(bad)[0][:5])
     assert ub.sum() == 0
     assert st.passes[3] == 0
+    assert st.general_docs == 0, "%s: %d documents on the sequential kernel" % (name, st.general_docs)
 
 
 @pytest.mark.timeout(900)

@@ -112,6 +112,11 @@ def test_oracle_equals_reference_html_and_hints(oracles):
     pr = priors_for(cld_amd, buf, offs, True, None)
     same(o.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=8),
          r.detect_batch(buf, offs, plain=np.zeros(n, np.uint8), threads=8), "html")
+    buf, offs = corpus.html(600, seed=24, emoji=1.0)               # 4-byte characters, raw and as entities
+    n = len(offs) - 1
+    pr = priors_for(cld_amd, buf, offs, True, None)
+    same(o.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=8),
+         r.detect_batch(buf, offs, plain=np.zeros(n, np.uint8), threads=8), "html with 4-byte characters")
     for cfg, n, seed in (("c2", 15000, 41), ("c3", 200, 42), ("c4", 4000, 43)):
         buf, offs = corpus.GENERATORS[cfg](n)
         hints = random_hints(cld_amd, n, seed)

@@ -1,5 +1,6 @@
 """HTML-mode throughput (is_plain_text = false) on synthetic HTML pages (sets:
-mixed 200-6000 B, 16k and 64k pages; HTML_RATE_SETS),
+mixed 200-6000 B, 16k and 64k pages, and the same with 4-byte characters on
+every page: emoji, emoji16k, emoji64k; HTML_RATE_SETS),
 inputs resident on the host (cld_detect_batch_ex): docs/s from the device
 timers (every kernel of the batch: the HTML rewrite, k_wave, k_long,
 k_general) and end to end, beside the reference CLD2 (oracle/_ref/librefcld2.so,
@@ -25,10 +26,11 @@ cld_amd.init_device(0)
 # Python; the rates do not depend on pages being distinct).
 SETS = {"mixed": (100_000, 200, 6000, 100_000), "16k": (100_000, 14_000, 18_000, 2000),
         "64k": (25_000, 56_000, 72_000, 500)}
+SETS.update({"emoji": SETS["mixed"], "emoji16k": SETS["16k"], "emoji64k": SETS["64k"]})
 
 
-def pages(npages, lo, hi, distinct):
-    b, o = corpus.html(distinct, seed=77, lo=lo, hi=hi)
+def pages(npages, lo, hi, distinct, emoji=0.0):
+    b, o = corpus.html(distinct, seed=77, lo=lo, hi=hi, emoji=emoji)
     if distinct == npages:
         return b, o
     idx = np.arange(npages) % distinct
@@ -48,7 +50,8 @@ except Exception as e:  # (the reference checker build is optional here)
 threads = int(os.environ.get("CLD_CPU_THREADS", "16"))
 for name in os.environ.get("HTML_RATE_SETS", "mixed").split(","):
     npages, lo, hi, distinct = SETS[name]
-    buf, offs = pages(npages, lo, hi, distinct)
+    emoji = 1.0 if name.startswith("emoji") else 0.0
+    buf, offs = pages(npages, lo, hi, distinct, emoji)
     print("set %s: %d pages, %d bytes" % (name, npages, int(offs[-1])), file=sys.stderr, flush=True)
     cld_amd.detect_batch_ex(buf=buf, offsets=offs, html=True)        # warm
     best = None
@@ -62,8 +65,9 @@ for name in os.environ.get("HTML_RATE_SETS", "mixed").split(","):
             best = (kms, wall, st.short_ms, st.long_ms, st.general_ms, int(st.general_docs), int(st.long_docs))
     n = len(offs) - 1
     kms, wall, wms, lms, gms, gdocs, ldocs = best
-    line = {"workload": "%dK synthetic HTML pages, %d-%d B (corpus.html seed 77, %d distinct)" % (n // 1000, lo, hi,
-                                                                                            distinct), "set": name,
+    line = {"workload": "%dK synthetic HTML pages, %d-%d B (corpus.html seed 77, %d distinct%s)"
+                        % (n // 1000, lo, hi, distinct, ", 4-byte characters on every page" if emoji else ""),
+            "set": name,
             "docs": n, "bytes": int(offs[-1]), "kernel_ms": kms, "rewrite_route_wave_ms": wms, "long_ms": lms,
             "general_ms": gms, "long_docs": ldocs, "general_docs": gdocs, "docs_per_s_kernel": n / (kms / 1e3),
             "docs_per_s_end_to_end": n / wall}

@@ -50,10 +50,11 @@ for s in ${STEPS:-suite smoke bench}; do
     tabsize)
       for t in ${TABS:-language-detector_amd/data/cld2_synth_q1.cldt language-detector_amd/data/variants/cld2_synth_q1_b65536.cldt language-detector_amd/data/variants/cld2_synth_q1_b262144.cldt language-detector_amd/data/variants/cld2_synth_q1_b1048576.cldt}; do
         b=$(basename $t .cldt)
-        step 300 tab_${b}_c2.json env CLD_MI355X_TABLES=$R/$t python bench.py --cpu-seconds 3 --no-host --no-sub
-        step 300 tab_${b}_c3.json env CLD_MI355X_TABLES=$R/$t python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
-        (cd /tmp && step 120 tab_${b}_pmc_c2.log env CLD_MI355X_TABLES=$R/$t rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_wave -d $O/tab_${b}_pmc_c2 -o c2 --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1
-        (cd /tmp && step 120 tab_${b}_pmc_c3.log env CLD_MI355X_TABLES=$R/$t rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_l(span|score|group|finish|rep|ong)" -d $O/tab_${b}_pmc_c3 -o c3 --output-format csv -- python3 $R/bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1
+        for c in ${TABCFG:-c2 c3}; do
+          if [ $c = c3 ]; then a="--steps 3 --warmup 1 --no-cpu-baseline"; k="k_l(span|score|group|finish|rep|ong)"; else a="--cpu-seconds 3"; k=k_wave; fi
+          step 300 tab_${b}_$c.json env CLD_MI355X_TABLES=$R/$t python bench.py --config $c $a --no-host --no-sub
+          (cd /tmp && step 120 tab_${b}_pmc_$c.log env CLD_MI355X_TABLES=$R/$t rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$k" -d $O/tab_${b}_pmc_$c -o $c --output-format csv -- python3 $R/bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-host --no-sub) || exit 1
+        done
       done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
