@@ -17,8 +17,9 @@ constexpr int kMaxLgProbScore = 16;
 
 
 // Device counter slots (three 64-byte lines, zeroed per batch)
-// kCtrRequeue/kCtrDequeue: wave kernel -> k_long list; kCtrRequeue2/kCtrDequeue2: k_long -> k_general;
-// kCtrSpecial: HTML / hinted documents the wave kernel sent straight to k_general.
+// kCtrRequeue/kCtrDequeue: the k_long list (documents longer than k_wave takes,
+// the ones it hands on, HTML pages the rewrite did not take);
+// kCtrSpecial: those HTML pages.  (kCtrRequeue2 / kCtrDequeue2: unused.)
 enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3 = 4, kCtrError = 5,
        kCtrRequeue2 = 6, kCtrDequeue2 = 7, kCtrWhy = 8 /* 8 slots: k_long re-queue reasons */,
        kCtrSpecial = 16, kCtrSpecTake = 17 /* k_long: speculative pass-2 results taken */,
@@ -31,39 +32,28 @@ enum { kCtrRequeue = 0, kCtrDequeue = 1, kCtrPass1 = 2, kCtrPass2 = 3, kCtrPass3
        kCtrStG1 = 28, kCtrStDqG1 = 29, kCtrStPar1 = 30, kCtrStDqF1 = 31,
        kCtrStG2 = 32, kCtrStDqG2 = 33, kCtrStPar2 = 34, kCtrStDqF2 = 35,
        // heavy (many-span) entries of the stored and pass-2 lists, filled from the top
-       kCtrStOkH = 36, kCtrStP2H = 37, kCtrSlots = 48 };
+       kCtrStOkH = 36, kCtrStP2H = 37,
+       kCtrSeq = 38 /* k_long: documents scored on the sequential span source (cld_seq.hip) */, kCtrSlots = 48 };
 // Per-document routing bits of cld_detect_batch_ex (special[i])
 // kSpecialRewritten: an HTML document k_html_rewrite turned into plain text
-// (hbuf / hflag); k_general, should it get it back, scores the original page.
-// kSpecialNoVec (vec mode): a rewritten page whose offset map the parallel
-// vec kernel cannot reproduce (cld_html.hip); it keeps the sequential kernel.
+// (hbuf / hflag); k_long scores the original page if it needs the sequential
+// span source.  kSpecialNoVec (vec mode): a rewritten page whose offset map the
+// parallel span builder cannot reproduce (cld_html.hip); k_long<VEC> scans the
+// original page with the sequential span source.
 enum : uint8_t { kSpecialHtml = 1, kSpecialPriors = 2, kSpecialRewritten = 4, kSpecialNoVec = 8 };
 // k_long: waves per workgroup
 constexpr int kLongWPB = 4;
 
 extern "C" {
-size_t cld_general_work_bytes();
-size_t cld_vec_work_bytes();
-// ResultChunkVector mode: all n documents in k_general_vec; document i builds
-// its vector in pool[pool_off[i] .. pool_off[i+1]) and writes its size (or -1)
-// to n_chunks[i]; counters[kCtrDequeue2] must be zero.
-// count (nullable): run only the *count documents listed in `order` (the
-// parallel vec path's hand-ons), else all n (order: optional permutation).
-hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
-                                  cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
-                                  const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
-                                  const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
-                                  const uint32_t* count, hipStream_t s);
-// ResultChunkVector mode on the parallel kernels: k_route_vec lists plain
-// documents under counters[kCtrRequeue] (long_list) and HTML pages under
-// counters[kCtrRequeue2] (gen_list); k_long<VEC> then scores the first list
-// with one VecSlot per resident wave (vslots: n_slots * cld_vec_slot_bytes())
-// and appends what it cannot reproduce to requeue2 (= gen_list).
+// ResultChunkVector mode: k_route_vec lists every document under
+// counters[kCtrRequeue]; k_long<VEC> then scores them with one VecSlot per
+// resident wave (vslots: n_slots * cld_vec_slot_bytes()); document i builds
+// its vector in pool[pool_off[i] .. pool_off[i+1]) and writes its size (or
+// -1: it outgrew its region, or has no result) to n_chunks[i].
 size_t cld_vec_slot_bytes();
-hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counters, uint32_t* long_list,
-                                uint32_t* gen_list, hipStream_t s);
+hipError_t cld_launch_route_vec(int n, uint32_t* counters, uint32_t* long_list, hipStream_t s);
 hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
-                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
+                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* seq_list,
                                uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
                                const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos, const uint32_t* hgap,
                                cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s);
@@ -106,11 +96,6 @@ hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, con
                                    uint8_t* special, uint8_t* hbuf, uint8_t* hflag, uint32_t* hpos, uint32_t* hgap,
                                    int hpos_min, unsigned long long* prof, hipStream_t s);
 size_t cld_wave_smem_bytes();
-hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
-                              const uint32_t* list, cld_result* out, uint8_t* arena,
-                              uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, uint32_t fault_doc,
-                              hipStream_t s);
 // (hist2: zeroed by k_route when cld_launch_wave was given it: zeroed = true)
 hipError_t cld_launch_order_long(const uint64_t* offs, const uint32_t* list, const uint32_t* counters,
                                  uint8_t* key, uint32_t* hist2, uint32_t* sorted, bool zeroed, hipStream_t s);
@@ -130,13 +115,16 @@ hipError_t cld_launch_strip_offsets(const uint8_t* buf, const uint64_t* offs, in
                                     uint64_t* out_offs, void* scratch, hipStream_t s);
 hipError_t cld_launch_strip_write(const uint8_t* buf, const uint64_t* offs, int n, uint32_t flags,
                                   const uint64_t* out_offs, uint8_t* out, hipStream_t s);
-// fault_doc (k_long, k_general): test hook, batch index of a document made to
-// fail (0xFFFFFFFF: none).  k_long hands it on, k_general marks it failed.
+// fault_doc (k_long): test hook, batch index of a document made to fail
+// (0xFFFFFFFF: none): it gets no result (summary CLD_LANG_FAILED).
+// seq_list (n entries, counters[kCtrRequeue2]): the documents k_long hands to
+// its SEQ instantiation (the sequential span source, cld_seq.hip), which the
+// launch runs right after it.
 // d_T: the device's DevTables copy in HBM (k_long reads the table set through
 // it: holding the by-value kernel argument in registers made the kernel spill
 // it to scratch and reload table fields from there at every probe)
 hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
-                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
+                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* seq_list,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
@@ -163,7 +151,7 @@ int cld_staged_waves_per_simd();
 hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
-                             uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
+                             uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
                              const uint32_t* hgap, uint32_t fault_doc, uint32_t small_total, const uint32_t* hist,
                              uint32_t heavy_kb, uint32_t* par_lists, size_t n, size_t gcap, hipStream_t s);

@@ -4,9 +4,8 @@
 //  k_long        one wavefront per document of any length up to lng::kDocCap,
 //                per-wave slot in HBM; persistent grid over the wave kernel's
 //                re-queue list.
-//  k_general     any document, all passes, per-lane state in a global arena;
-//                persistent grid pulling documents from the re-queue list
-//                with one atomic dequeue per document.
+//                Documents the parallel span builder cannot formulate take
+//                its sequential span source (cld_seq.hip) in the same wave.
 #include "cld_kernels.h"
 // The A/B knobs of earlier rounds that gave wrong results by design are gone;
 // refuse a build that still asks for one.
@@ -21,139 +20,12 @@
 static_assert(kHtmlSoftMin == cld::kMaxScriptBytes, "kHtmlSoftMin is kMaxScriptBytes");
 static_assert(kLongDocCap == (uint64_t)cld::lng::kDocCap, "kLongDocCap is lng::kDocCap");
 
-#ifndef GEN_LANES_PER_WAVE
-// k_general / k_general_vec: documents per wavefront.  One per wave: the
-// sequential per-document code then never diverges between documents in a
-// wave (64 per wave ran every document's branches for all of them: HTML pages
-// 52K -> 185K docs/s).
-#define GEN_LANES_PER_WAVE 1
-#endif
-// waves per SIMD the sequential kernels are compiled for (their register
-// budget); 0: the compiler's choice
-#ifndef GEN_WPE
-#define GEN_WPE 0
-#endif
-#if GEN_WPE > 0
-#define GEN_OCC __attribute__((amdgpu_waves_per_eu(GEN_WPE, GEN_WPE)))
-#else
-#define GEN_OCC
-#endif
-
 namespace cld {
 
-using GeneralWork = Work<kMaxScriptBuffer, kMaxScriptLowerBuffer, kMaxScoringHits + 8, true>;
-
-__global__ __launch_bounds__(64) GEN_OCC void k_general(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
-                                               const uint64_t* __restrict__ offs,
-                                               const uint32_t* __restrict__ list,
-                                               cld_result* __restrict__ out,
-                                               uint8_t* __restrict__ arena, uint64_t stride,
-                                               uint32_t* __restrict__ counters, int ctr_count, int ctr_deq,
-                                               const uint8_t* __restrict__ special,
-                                               const uint32_t* __restrict__ priors, uint32_t cflags,
-                                               uint32_t fault_doc) {
-  const DevTables& T = *Tp;
-#if GEN_LANES_PER_WAVE == 1
-  // one document per wavefront (lane 0): no divergence between documents
-  if (threadIdx.x != 0) return;
-  const int lane = blockIdx.x;
-#else
-  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
-#endif
-  GeneralWork& w = *reinterpret_cast<GeneralWork*>(arena + (uint64_t)lane * stride);
-  const uint32_t total = __hip_atomic_load(&counters[ctr_count], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // nothing re-queued (every C2 / C4 batch): leave before touching the shared
-  // dequeue counter, so an empty launch costs its dispatch and nothing more
-  const uint32_t done0 = __hip_atomic_load(&counters[ctr_deq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (done0 >= total) return;
-  for (;;) {
-    uint32_t k = atomicAdd(&counters[ctr_deq], 1u);
-    if (k >= total) break;                       // every lane reaches this exit
-    const uint32_t i = list[k];
-    const uint64_t a = offs[i], b = offs[i + 1];
-    Status st{false};
-    DocView d{buf + a, (int)(b - a)};
-    // cld_detect_batch_ex: HTML documents (special bit 0) and per-document
-    // ApplyHints priors (16 langprobs each, bit 1)
-    const uint8_t sp = special ? special[i] : 0;
-    int passes = detect_doc(T, d, w, &out[i], st, !(sp & (kSpecialHtml | kSpecialRewritten)),
-                            (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, nullptr, cflags);
-    if (i == fault_doc) passes = 0;              // fault injection (CLD_FAULT_DOC, tests only)
-    if (passes >= 1 && passes <= 3) {
-      atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
-    } else {
-      // No result for this document: it is marked (summary CLD_LANG_FAILED) and
-      // counted; the host redoes it alone, the rest of the batch stands.
-      atomicAdd(&counters[kCtrError], 1u);
-      mark_failed(T, &out[i]);
-    }
-  }
-}
-
-// ResultChunkVector mode (cld_detect_batch_vec): every document runs the
-// exact sequential pipeline with its offset maps and chunk vector, one lane
-// per document, in its own arena.  Capacities: map2original_ gets at most ~3
-// ranges per span byte (kMaxScriptBuffer), map2uplow_ at most ~2 per lowered
-// byte; a document that would exceed one (or its pool region) reports -1.
-constexpr int kMapOrigCap = 3 * kMaxScriptBuffer + 4096;
-constexpr int kMapLowCap = 2 * kMaxScriptLowerBuffer + 4096;
-struct VecWork {
-  GeneralWork g;
-  VecOut vo;
-  uint8_t map_o[kMapOrigCap];
-  uint8_t map_l[kMapLowCap];
-};
-
-__global__ __launch_bounds__(64) GEN_OCC void k_general_vec(const DevTables* __restrict__ Tp, const uint8_t* __restrict__ buf,
-                                                   const uint64_t* __restrict__ offs, int n,
-                                                   cld_result* __restrict__ out,
-                                                   uint8_t* __restrict__ arena, uint64_t stride,
-                                                   uint32_t* __restrict__ counters,
-                                                   const uint8_t* __restrict__ special,
-                                                   const uint32_t* __restrict__ priors,
-                                                   cld_chunk* __restrict__ pool, const uint64_t* __restrict__ pool_off,
-                                                   int32_t* __restrict__ n_chunks, const uint32_t* __restrict__ order,
-                                                   uint32_t cflags, const uint32_t* __restrict__ count) {
-  const DevTables& T = *Tp;
-#if GEN_LANES_PER_WAVE == 1
-  if (threadIdx.x != 0) return;
-  const int lane = blockIdx.x;
-#else
-  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
-#endif
-  VecWork& w = *reinterpret_cast<VecWork*>(arena + (uint64_t)lane * stride);
-  // count (nullable): the list `order` holds *count documents (the ones the
-  // parallel vec kernel handed on), else every document 0..n-1
-  const uint32_t total = count ? __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (uint32_t)n;
-  for (;;) {
-    const uint32_t k = atomicAdd(&counters[kCtrDequeue2], 1u);
-    if (k >= total) break;                       // every lane reaches this exit
-    const uint32_t i = order ? order[k] : k;     // longest documents first
-    const uint64_t a = offs[i], b = offs[i + 1];
-    VecOut& vo = w.vo;
-    vo.orig.d = w.map_o; vo.orig.cap = kMapOrigCap; vo.orig.n = 0; vo.orig.over = false;
-    vo.low.d = w.map_l; vo.low.cap = kMapLowCap; vo.low.n = 0; vo.low.over = false;
-    dm_clear(vo.orig); dm_clear(vo.low);
-    const uint64_t reg = pool_off[i + 1] - pool_off[i];
-    vo.v = pool + pool_off[i]; vo.cap = reg > 0x7FFFFFFFull ? 0x7FFFFFFF : (int)reg; vo.n = 0; vo.over = false;
-    vo.doc = buf + a; vo.doc_len = (int)(b - a);
-    Status st{false};
-    DocView d{buf + a, (int)(b - a)};
-    const uint8_t sp = special ? special[i] : 0;
-    const int passes = detect_doc(T, d, w.g, &out[i], st, !(sp & (kSpecialHtml | kSpecialRewritten)),
-                                  (sp & kSpecialPriors) ? priors + 16ull * i : nullptr, &vo, cflags);
-    const bool bad = passes < 1 || passes > 3 || st.requeue || vo.over || vo.orig.over || vo.low.over;
-    n_chunks[i] = bad ? -1 : vo.n;
-    if (!bad) atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
-    else atomicAdd(&counters[kCtrError], 1u);
-  }
-}
-
-// Vec-mode routing: plain documents to k_long<VEC>'s list, HTML pages to the
-// sequential kernel's (one atomic per wavefront each).
-__global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restrict__ special,
-                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ long_list,
-                                                  uint32_t* __restrict__ gen_list);
+// Vec-mode routing: every document to k_long<VEC>'s list (one atomic per
+// wavefront); k_long reads each one's routing bits itself.
+__global__ __launch_bounds__(256) void k_route_vec(int n, uint32_t* __restrict__ counters,
+                                                  uint32_t* __restrict__ long_list);
 
 // Compaction of the per-document pool regions into document order.
 __global__ __launch_bounds__(256) void k_vec_gather(const cld_chunk* __restrict__ pool,
@@ -200,7 +72,7 @@ __global__ __launch_bounds__(64 * WPB, WAVE_WPS) void k_wave(DevTables T, const 
   const int per = ((n + WPB - 1) / WPB + 7) >> 3;          // blocks per XCD slice
   const int i = ((int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3)) * WPB + wv;
   if (i >= n) return;
-  // k_route has already listed the HTML documents (for k_general) and those
+  // k_route has already listed the HTML documents (for k_long) and those
   // longer than CAP (for k_long); hinted plain ones are scored here with their
   // ApplyHints priors
   const uint8_t sp = special ? special[i] : (uint8_t)0;
@@ -240,22 +112,16 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t* ctr, uint32_t* 
   if (pred) list[base + __popcll(m & wave::lanemask_lt(lane))] = val;
 }
 
-__global__ __launch_bounds__(256) void k_route_vec(int n, const uint8_t* __restrict__ special,
-                                                  uint32_t* __restrict__ counters, uint32_t* __restrict__ long_list,
-                                                  uint32_t* __restrict__ gen_list) {
+__global__ __launch_bounds__(256) void k_route_vec(int n, uint32_t* __restrict__ counters,
+                                                  uint32_t* __restrict__ long_list) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  // HTML pages the rewrite did not take (still kSpecialHtml) or whose offset
-  // map it flagged (kSpecialNoVec) go to the sequential kernel
-  const uint8_t sp = (i < n && special) ? special[i] : (uint8_t)0;
-  const bool seq = i < n && (sp & (kSpecialHtml | kSpecialNoVec));
-  wave_append(seq, &counters[kCtrRequeue2], gen_list, (uint32_t)i, &counters[kCtrSpecial]);
-  wave_append(i < n && !seq, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
+  wave_append(i < n, &counters[kCtrRequeue], long_list, (uint32_t)i, nullptr);
 }
 
 constexpr int kLenBuckets = 64;
 
 // Routing before k_wave, one thread per document: HTML documents to
-// k_general's list, documents longer than k_wave's CAP to k_long's, each with
+// k_long's list, documents longer than k_wave's CAP to k_long's, each with
 // one atomic per wavefront instead of one per document (a batch of 100K pages
 // used to queue every page through the same counter from k_wave).  Block 0
 // also zeroes k_len_hist's histogram and cursors (hist2, nullable): one
@@ -279,7 +145,8 @@ __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs
 // One wavefront per long document, persistent: each wave owns slot
 // blockIdx.x * WPB + wave and pulls documents from the wave kernel's re-queue
 // list (one atomic per document) until the list is drained -- every wave
-// reaches that exit.  Documents it cannot reproduce go to the k_general list.
+// reaches that exit.  Documents the parallel span builder cannot formulate
+// are scored again from the sequential span source (cld_seq.hip).
 // LNG_WPS waves per SIMD.  The kernel is latency-bound on its HBM slots:
 // more resident waves beat the extra spills (C3, 30K pages: 4 -> 496K, 5 ->
 // 538K, 6 -> 553K, 7 -> 578K, 8 -> 541K docs/s; profiles/round1e_*).  After
@@ -293,13 +160,15 @@ __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ offs
 // kSpecBatchWaves documents per resident wave (a full batch is throughput-
 // bound and keeps one wave per document).
 constexpr uint32_t kSpecShare = 8, kSpecBatchWaves = 4;
-template <int WPB, bool DIAG, bool VEC>
+// SEQ: the instantiation that drains seq_list (the documents the parallel
+// one hands on): their spans come from the sequential span source.
+template <int WPB, bool DIAG, bool VEC, bool SEQ = false>
 __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __restrict__ Tp,
                                                   const uint8_t* __restrict__ buf,
                                                   const uint64_t* __restrict__ offs,
                                                   const uint32_t* __restrict__ list,
                                                   cld_result* __restrict__ out, uint8_t* __restrict__ slots,
-                                                  uint32_t* __restrict__ requeue2,
+                                                  uint32_t* __restrict__ seq_list,
                                                   uint32_t* __restrict__ counters, uint32_t* trace,
                                                   uint32_t* dbg, uint32_t dbg_doc,
                                                   unsigned long long* prof, uint32_t cflags,
@@ -329,7 +198,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
   // The last wave to leave takes pass 2's result for every document whose
   // pass 1 was not good enough (spec_take).
   const uint32_t nwaves = gridDim.x * WPB;
-  const uint32_t nspec = (!VEC && spec_out && total <= kSpecBatchWaves * nwaves) ? min(total, nwaves / kSpecShare) : 0u;
+  const uint32_t nspec =
+      (!VEC && !SEQ && spec_out && total <= kSpecBatchWaves * nwaves) ? min(total, nwaves / kSpecShare) : 0u;
   const uint32_t entries = total + nspec;
   if constexpr (DIAG) lng::trace(tr, lane, 0xFFFFFFFFu, 97, 0);
   const bool exact = lng::space_lowers_to_space(T);
@@ -359,11 +229,24 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
     const bool hbig = rw && hpos && len >= (uint64_t)kMaxScriptBytes;
     const uint32_t* hp = hbig ? hpos + a : nullptr;
     const uint32_t* hg = hbig ? hgap + a : nullptr;
+    const uint32_t* pri = (spi & kSpecialPriors) ? priors + 16ull * i : nullptr;
+    // The sequential span source (cld_seq.hip) over the page as given: for a
+    // page the HTML rewrite did not take (still kSpecialHtml), one whose
+    // rewritten offsets vec mode cannot use (kSpecialNoVec), a document past
+    // the slot's bitmap, a table set whose lowercaser does not keep ' ', and
+    // -- after the parallel attempt -- any document that attempt could not
+    // formulate.  Those go to seq_list, which the SEQ instantiation drains;
+    // the span-level stages are the same either way.
+    const bool html_raw = (spi & kSpecialHtml) != 0;
+    const bool fault = i == fault_doc;               // fault injection (CLD_FAULT_DOC, tests only)
+    const bool to_seq = !SEQ && !fault &&
+                        (!exact || html_raw || (VEC && (spi & kSpecialNoVec)) || len > (uint64_t)lng::kDocCap);
+    cld_result* o = (!VEC && mode == lng::kPassRepeatsOnly) ? spec_out + k : &out[i];
+    lng::VecState V;
     if constexpr (VEC) {
       // ResultChunkVector mode (cld_detect_batch_vec): the vector goes to the
       // document's pool region; a vector that outgrows it reports -1 (the host
       // redoes the document with a larger region)
-      lng::VecState V;
       V.vs = reinterpret_cast<lng::VecSlot*>(vslots + (uint64_t)(blockIdx.x * WPB + wv) * sizeof(lng::VecSlot));
       const uint64_t reg = pool_off[i + 1] - pool_off[i];
       V.v = pool + pool_off[i];
@@ -373,41 +256,50 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
       V.doc = buf + a;                           // (the page as given: the vector maps into it)
       V.L = (int)len;
       V.last_off = V.last_bytes = V.last_lang = 0;
-      V.hpos = rw ? hpos + a : nullptr;           // a rewritten HTML page: rewritten byte -> page offset
-      V.hgap = rw ? hgap + a : nullptr;
-      if (exact && len <= (uint64_t)lng::kDocCap)
-        passes = lng::detect<DIAG, true>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, &out[i], tr, i,
-                                         cflags, (spi & kSpecialPriors) ? priors + 16ull * i : nullptr,
-                                         rw ? hflag + a : nullptr, &V, lng::kPassesAll, hp, hg);
-      if (lane == 0 && passes >= 1 && passes <= 3) n_chunks[i] = V.over ? -1 : V.n;
-    } else {
-      cld_result* o = mode == lng::kPassRepeatsOnly ? spec_out + k : &out[i];
-      if (exact && len <= (uint64_t)lng::kDocCap)
-        passes = lng::detect<DIAG>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, o, tr, i, cflags,
-                                   (spi & kSpecialPriors) ? priors + 16ull * i : nullptr, rw ? hflag + a : nullptr,
-                                   nullptr, mode, hp, hg);
+      V.hpos = (rw && !SEQ) ? hpos + a : nullptr;   // a rewritten HTML page: rewritten byte -> page offset
+      V.hgap = (rw && !SEQ) ? hgap + a : nullptr;
+      V.seq = SEQ;
+    }
+    if (!fault && !to_seq) {
+      if constexpr (SEQ) {
+        const lng::SeqDoc sq{buf + a, (int)len, !(spi & (kSpecialHtml | kSpecialRewritten | kSpecialNoVec))};
+        passes = lng::detect<DIAG, VEC, true>(T, buf + a, (int)len, S, smem[wv], lane, o, tr, i, cflags, pri, nullptr,
+                                              VEC ? &V : nullptr, lng::kPassesAll, nullptr, nullptr, &sq);
+        if (lane == 0) atomicAdd(&counters[kCtrSeq], 1u);
+      } else {
+        passes = lng::detect<DIAG, VEC>(T, (rw ? hbuf : buf) + a, (int)len, S, smem[wv], lane, o, tr, i, cflags,
+                                        pri, rw ? hflag + a : nullptr, VEC ? &V : nullptr, VEC ? lng::kPassesAll : mode,
+                                        hp, hg);
+      }
     }
     if constexpr (DIAG) lng::trace(tr, lane, i, 99, passes);
     passes = wave::ufl(passes);
-    if (i == fault_doc) passes = -lng::kWhyLength;   // fault injection (CLD_FAULT_DOC): on to k_general
-    if (mode == lng::kPassRepeatsOnly) {            // pass 2 in spec_out[k]; taken or not by its pass-1 wave
-      if (lane == 0 && !(passes >= 1 && passes <= 3)) {
-        spec_out[k].summary_lang = CLD_LANG_FAILED;
-        spec_out[k].text_bytes = min(max(-passes, 0), 7);   // the re-queue reason
-      }
+    const bool good = passes >= 1 && passes <= 3 && !fault;
+    // handed on: the SEQ instantiation redoes the document whole (a pass-2
+    // speculative wave's failure is handed on by its pass-1 wave's taker)
+    const bool hand_on = !SEQ && !fault && !good && passes != lng::kNeedsRepeats;
+    if constexpr (VEC) {
+      if (lane == 0 && !hand_on) n_chunks[i] = (good && !V.over) ? V.n : -1;
+    }
+    if (!VEC && mode == lng::kPassRepeatsOnly) {   // pass 2 in spec_out[k]; taken or not by its pass-1 wave
+      if (lane == 0 && !good) spec_out[k].summary_lang = CLD_LANG_FAILED;
       continue;
     }
-    if (passes == lng::kNeedsRepeats) {
+    if (passes == lng::kNeedsRepeats && !fault) {
       if (lane == 0) spec_take[atomicAdd(&counters[kCtrSpecTake], 1u)] = k;
       continue;
     }
     if (lane == 0) {
-      if (passes >= 1 && passes <= 3) {
+      if (good) {
         atomicAdd(&counters[kCtrPass1 + passes - 1], 1u);
+      } else if (hand_on) {
+        seq_list[atomicAdd(&counters[kCtrRequeue2], 1u)] = i;
+        if (!to_seq) atomicAdd(&counters[kCtrWhy + min(max(-passes, 0), 7)], 1u);
       } else {
-        const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);
-        requeue2[q] = i;
-        atomicAdd(&counters[kCtrWhy + min(max(-passes, 0), 7)], 1u);
+        // No result for this document: it is marked (summary CLD_LANG_FAILED)
+        // and counted; the host redoes it alone, the rest of the batch stands.
+        atomicAdd(&counters[kCtrError], 1u);
+        mark_failed(T, &out[i]);
       }
     }
   }
@@ -422,10 +314,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
       for (uint32_t p = lane; p < nt; p += 64) {
         const uint32_t k = spec_take[p], i = list[k];
         const cld_result r = spec_out[k];
-        if (r.summary_lang == CLD_LANG_FAILED) {      // pass 2 could not run here: k_general redoes it all
-          const uint32_t q = atomicAdd(&counters[kCtrRequeue2], 1u);
-          requeue2[q] = i;
-          atomicAdd(&counters[kCtrWhy + r.text_bytes], 1u);
+        if (r.summary_lang == CLD_LANG_FAILED) {      // pass 2 could not run here: the SEQ kernel redoes it
+          seq_list[atomicAdd(&counters[kCtrRequeue2], 1u)] = i;
         } else {
           out[i] = r;
           atomicAdd(&counters[kCtrPass2], 1u);
@@ -446,7 +336,8 @@ __global__ __launch_bounds__(64 * WPB, LNG_WPS) void k_long(const DevTables* __r
 // 86.1 ms; staged at 5/5/5 waves and a 5 KB window 77.0 ms, at 5/6/5 and 3 KB
 // 73.6 ms (gpurun_out/r5j), at 6/7/5 and 2 KB ~72 ms (r5k).  A block of a span
 // wider than the window (win_text) sends the document to the fused kernel,
-// whose window is 6 KB (a 1 KB window sent 81% of C3 to k_general).
+// whose window is 6 KB (a 1 KB window sent 81% of C3 to the sequential kernel
+// of earlier rounds).
 #ifndef LNG_ST_WPS
 #define LNG_ST_WPS 7
 #endif
@@ -540,10 +431,13 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_SPAN_WPS) void k_lspan(
     const uint32_t* hp = hbig ? hpos + a : nullptr;
     const uint32_t* hg = hbig ? hgap + a : nullptr;
     uint64_t at = lng::kStNone;
-    if (exact && L <= (uint64_t)(lng::kDocCap - 64) && i != fault_doc) {
+    // (pages the HTML rewrite did not take go to the fused kernel, whose
+    // sequential span source scans them in HTML mode)
+    const bool take = exact && !(spi & kSpecialHtml) && i != fault_doc;
+    if (take && L <= (uint64_t)(lng::kDocCap - 64)) {
       const DocView dv{(rw ? hbuf : buf) + a, (int)L, rw ? hflag + a : nullptr, hp, hg};
       at = lng::st_spans(T, dv, S, pool, units, &counters[kCtrStPool], lane, par_min);
-    } else if (exact && L <= lng::kStBigMax && i != fault_doc) {   // over kDocCap: a worst-case region
+    } else if (take && L <= lng::kStBigMax) {   // over kDocCap: a worst-case region
       const uint64_t u = (lng::st_big_bytes(L) + 15) >> 4;
       uint32_t got = 0;
       if (lane == 0) got = atomicAdd(&counters[kCtrStPool], (uint32_t)u);
@@ -605,7 +499,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lscore(
     const uint32_t k = st_get(in_list, nh, n, e);
     if (P2 && (k & 0x80000000u)) continue;       // a span-parallel document: k_lgroup / k_lfinish
     const uint64_t at = meta[k];
-    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
+    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to the fused k_long
     const uint32_t i = list[k];
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const int r = lng::st_score(T, S, smem[wv], pool + at, P2, &out[i], cflags,
@@ -655,7 +549,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lgroup(
     if (it == ~0ull) continue;
     const uint32_t k = (uint32_t)it, g = (uint32_t)(it >> 32);
     const uint64_t at = meta[k];
-    if (at == lng::kStNone) continue;            // (pass 2: k_lrep handed it to k_general)
+    if (at == lng::kStNone) continue;            // (pass 2: k_lrep handed it to the fused k_long)
     const uint32_t i = list[k];
     const uint8_t spi = special ? special[i] : (uint8_t)0;
     const int nsp = (int)wave::uflu(gld(&reinterpret_cast<const lng::StHdr*>(pool + at)->nsp));
@@ -683,7 +577,7 @@ __global__ __launch_bounds__(64 * kStWPB, LNG_ST_WPS) void k_lfinish(
     if (e >= total) break;                       // every wave reaches this exit
     const uint32_t k = in_list[e];
     const uint64_t at = meta[k];
-    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to k_general
+    if (P2 && at == lng::kStNone) continue;      // k_lrep handed it to the fused k_long
     const uint32_t i = list[k];
     const int r = lng::st_par_finish(T, smem[wv], pool + at, P2, &out[i], cflags, lane);
     if (r == 0 && !P2) {                         // pass 2: Repeats (k_lrep), then its groups again
@@ -714,7 +608,7 @@ __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __rest
                                                          uint8_t* __restrict__ slots, uint8_t* __restrict__ pool,
                                                          uint64_t* __restrict__ meta,
                                                          const uint32_t* __restrict__ p2_list,
-                                                         uint32_t* __restrict__ requeue2,
+                                                         uint32_t* __restrict__ fall_list,
                                                          uint32_t* __restrict__ counters, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint16_t pred[kPredictionTableSize];
   const int lane = threadIdx.x & 63;
@@ -726,9 +620,9 @@ __global__ __launch_bounds__(64, LNG_REP_WPS) void k_lrep(const uint32_t* __rest
     const uint32_t e = wave::uflu(atomicAdd(&counters[kCtrStDqRep], lane == 0 ? 1u : 0u));
     if (e >= total) break;                       // every wave reaches this exit
     const uint32_t k = st_get(p2_list, nh, n, e) & 0x7FFFFFFFu;   // (bit 31: a span-parallel document)
-    if (!lng::st_rep(pred, S, pool + meta[k], lane) && lane == 0) {
+    if (!lng::st_rep(pred, S, pool + meta[k], lane) && lane == 0) {   // (the fused kernel redoes it whole)
       meta[k] = lng::kStNone;
-      requeue2[atomicAdd(&counters[kCtrRequeue2], 1u)] = list[k];
+      fall_list[atomicAdd(&counters[kCtrStFall], 1u)] = list[k];
       atomicAdd(&counters[kCtrWhy + lng::kWhySpan], 1u);
     }
   }
@@ -896,7 +790,7 @@ size_t cld_long_slot_bytes() { return sizeof(cld::lng::Slot); }
 int cld_long_waves_per_simd() { return LNG_WPS; }
 
 hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
-                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* requeue2,
+                           cld_result* out, uint8_t* slots, int n_slots, uint32_t* seq_list,
                            uint32_t* counters, uint32_t* trace, uint32_t* dbg, uint32_t dbg_doc,
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
@@ -905,19 +799,31 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
-  // they cost the production kernel registers even when switched off
-  if (trace || dbg || prof)
+  // they cost the production kernel registers even when switched off.  Then
+  // the documents it handed on (seq_list, counters[kCtrRequeue2]), on the
+  // sequential span source.
+  if (trace || dbg || prof) {
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
-  else
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false, true>), grid, block, 0, s, d_T, buf, offs, seq_list, out,
+                       slots, seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, nullptr, nullptr, kCtrRequeue2,
+                       kCtrDequeue2);
+  } else {
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                       requeue2, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
+    hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false, true>), grid, block, 0, s, d_T, buf, offs, seq_list, out,
+                       slots, seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
+                       fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, nullptr, nullptr, kCtrRequeue2,
+                       kCtrDequeue2);
+  }
   return hipGetLastError();
 }
+
 size_t cld_long_spec_docs(int n_slots) { return (size_t)n_slots / cld::kSpecShare; }
 
 int cld_staged_waves_per_simd() {
@@ -928,7 +834,7 @@ int cld_staged_waves_per_simd() {
 hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
                              cld_result* out, uint8_t* slots, int n_waves, uint8_t* pool, uint64_t pool_bytes,
                              uint64_t* meta, uint32_t* ok_list, uint32_t* p2_list, uint32_t* fall_list,
-                             uint32_t* requeue2, uint32_t* counters, uint32_t cflags, const uint8_t* special,
+                             uint32_t* counters, uint32_t cflags, const uint8_t* special,
                              const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
                              const uint32_t* hgap, uint32_t fault_doc, uint32_t small_total, const uint32_t* hist,
                              uint32_t heavy_kb, uint32_t* par_lists,
@@ -951,7 +857,7 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
   hipLaunchKernelGGL(cld::k_lfinish<false>, gst, bst, 0, s, d_T, list, out, pool, meta, par_lists, nn, gl2, gc,
                      p2_list, fall_list, counters, cflags);
   hipLaunchKernelGGL(cld::k_lrep, dim3(cus * 4 * LNG_REP_WPS), dim3(64), 0, s, list, slots, pool, meta, p2_list,
-                     requeue2, counters, nn);
+                     fall_list, counters, nn);
   hipLaunchKernelGGL(cld::k_lscore<true>, gst, bst, 0, s, d_T, list, out, slots, pool, meta, p2_list, p2_list,
                      fall_list, counters, cflags, special, priors, nn);
   hipLaunchKernelGGL(cld::k_lgroup<true>, gst, bst, 0, s, d_T, list, slots, pool, meta, gl2, gc, counters, cflags,
@@ -963,44 +869,27 @@ hipError_t cld_launch_staged(const DevTables* d_T, const uint8_t* buf, const uin
 
 size_t cld_vec_slot_bytes() { return sizeof(cld::lng::VecSlot); }
 
-hipError_t cld_launch_route_vec(int n, const uint8_t* special, uint32_t* counters, uint32_t* long_list,
-                                uint32_t* gen_list, hipStream_t s) {
+hipError_t cld_launch_route_vec(int n, uint32_t* counters, uint32_t* long_list, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cld::k_route_vec, dim3((n + 255) / 256), dim3(256), 0, s, n, special, counters, long_list,
-                     gen_list);
+  hipLaunchKernelGGL(cld::k_route_vec, dim3((n + 255) / 256), dim3(256), 0, s, n, counters, long_list);
   return hipGetLastError();
 }
 
 hipError_t cld_launch_long_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, const uint32_t* list,
-                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* requeue2,
+                               cld_result* out, uint8_t* slots, uint8_t* vslots, int n_slots, uint32_t* seq_list,
                                uint32_t* counters, uint32_t cflags, const uint8_t* special, const uint32_t* priors,
                                const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos, const uint32_t* hgap,
                                cld_chunk* pool, const uint64_t* pool_off, int32_t* n_chunks, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
-                     requeue2, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
+                     seq_list, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
                      hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap, nullptr, nullptr, kCtrRequeue,
                      kCtrDequeue);
-  return hipGetLastError();
-}
-
-size_t cld_general_work_bytes() { return sizeof(cld::GeneralWork); }
-size_t cld_vec_work_bytes() { return sizeof(cld::VecWork); }
-
-hipError_t cld_launch_general_vec(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs, int n,
-                                  cld_result* out, uint8_t* arena, uint64_t stride, int lanes, uint32_t* counters,
-                                  const uint8_t* special, const uint32_t* priors, cld_chunk* pool,
-                                  const uint64_t* pool_off, int32_t* n_chunks, const uint32_t* order, uint32_t cflags,
-                                  const uint32_t* count, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-#if GEN_LANES_PER_WAVE == 1
-  dim3 grid(lanes), block(64);
-#else
-  dim3 grid(lanes / 64), block(64);
-#endif
-  hipLaunchKernelGGL(cld::k_general_vec, grid, block, 0, s, d_T, buf, offs, n, out, arena, stride, counters, special,
-                     priors, pool, pool_off, n_chunks, order, cflags, count);
+  hipLaunchKernelGGL((cld::k_long<kLongWPB, false, true, true>), grid, block, 0, s, d_T, buf, offs, seq_list, out,
+                     slots, seq_list, counters, nullptr, nullptr, 0xFFFFFFFFu, nullptr, cflags, special, priors, hbuf,
+                     hflag, 0xFFFFFFFFu, vslots, pool, pool_off, n_chunks, hpos, hgap, nullptr, nullptr, kCtrRequeue2,
+                     kCtrDequeue2);
   return hipGetLastError();
 }
 
@@ -1046,18 +935,4 @@ hipError_t cld_launch_html_rewrite(const DevTables* d_T, const uint8_t* buf, con
   return hipGetLastError();
 }
 
-hipError_t cld_launch_general(const DevTables* d_T, const uint8_t* buf, const uint64_t* offs,
-                              const uint32_t* list, cld_result* out, uint8_t* arena,
-                              uint64_t stride, int lanes, uint32_t* counters, int ctr_count, int ctr_deq,
-                              const uint8_t* special, const uint32_t* priors, uint32_t cflags, uint32_t fault_doc,
-                              hipStream_t s) {
-#if GEN_LANES_PER_WAVE == 1
-  dim3 grid(lanes), block(64);                   // `lanes` documents in flight, one per wavefront
-#else
-  dim3 grid(lanes / 64), block(64);
-#endif
-  hipLaunchKernelGGL(cld::k_general, grid, block, 0, s, d_T, buf, offs, list, out, arena, stride,
-                     counters, ctr_count, ctr_deq, special, priors, cflags, fault_doc);
-  return hipGetLastError();
-}
 }

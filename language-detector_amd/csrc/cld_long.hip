@@ -219,6 +219,7 @@ struct VecState {                                      // wave-uniform
   int last_off, last_bytes, last_lang;                 // v[n - 1], mirrored
   const uint32_t* hpos;                                // a rewritten HTML page: byte -> page offset, else null
   const uint32_t* hgap;                                //   and where dropped '&'s before a byte began
+  bool seq;                                            // spans from seq_span (cld_seq.hip): omap covers any span
 };
 
 // Stage cycle accounting: 0 classify, 1 span+lowercase, 2 squeeze test,
@@ -305,6 +306,8 @@ __device__ __forceinline__ void gsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+#include "cld_seq.hip"   // spans of the documents the parallel span builder cannot formulate
+
 // LDS window over a lowered span for the hit stages (score_span): s.text
 // holds span bytes [w0, w1).  A span longer than the LDS text buffer stays in
 // the slot (g); every block of those stages first makes its byte range
@@ -324,10 +327,11 @@ __device__ __forceinline__ const uint8_t* win_text(Win& w, SM& s, int lo, int hi
   lo = lo > 0 ? lo : 0;
   if (lo < w.w0 || hi > w.w1) {
     const int a = (lo - 32 > 0 ? lo - 32 : 0) & ~15;
-    if (!w.g || hi > a + (int)sizeof(s.text) - 15) {   // (a block wider than the buffer: k_general takes it)
+    if (!w.g) {                                  // (outside a span held whole in LDS: never read)
       ok = false;
       return s.text - w.w0;
     }
+    if (hi > a + (int)sizeof(s.text) - 15) return w.g;   // a block wider than the window: read in place
     const int b = min(w.len, a + (int)sizeof(s.text) - 15);
     const int n16 = (b - a + 15) >> 4;
     wsync();                                     // every lane is done with the previous window
@@ -1008,6 +1012,17 @@ __device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, i
 }
 
 // ------------------------------------------------------ predictor (squeeze/repeats)
+// The predictor's character code: a lead byte and the bytes its value claims,
+// continuation bytes or not, big-endian; *incr = their count
+// (compact_lang_det_impl.cc:641-667, the same decode in CountPredictedBytes).
+__device__ __forceinline__ int next_char_code(const uint8_t* src, int* incr) {
+  const uint32_t c = src[0];
+  const int n = c < 0xC0 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4;
+  *incr = n;
+  uint32_t v = c;
+  for (int k = 1; k < n; ++k) v = (v << 8) | src[k];
+  return (int)v;
+}
 // A fresh predictor table: a new epoch makes every older entry read as 0.
 __device__ uint32_t new_epoch(uint32_t& epoch, uint64_t* tbl, int lane) {
   uint32_t e = uflu(epoch) + 1u;
@@ -1200,9 +1215,15 @@ __device__ __forceinline__ int rep_span_lds(uint16_t* tbl, uint64_t* ovf, uint8_
     }
     D = bD + __popcll(km);
   }
-  // a last character claiming bytes past the span would make the reference
-  // copy pad bytes too: k_general takes that (malformed) document
-  ok = carry == 0;
+  // a last character claiming bytes past the span (a span cut inside a
+  // character, malformed text): the reference copies the bytes it claims,
+  // the pad bytes after the span included (:640-662)
+  if (carry > 0) {
+    if (lane == 0)
+      for (int k = 0; k < carry; ++k) text[D + k] = text[len + k];
+    D += carry;
+  }
+  ok = true;
   // "   \0" if at least 4 bytes went, else a single ' ' if any went (:684-689)
   if (D < len - 3) {
     if (lane < 4) text[D + lane] = lane < 3 ? ' ' : 0;
@@ -1288,10 +1309,10 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     }
   }
   gsync();
-  // a last character claiming bytes past the span would make the reference
-  // copy pad bytes too: k_general takes that (malformed) document
-  ok = carry == 0;
-  if (!ok) return len;
+  // a last character claiming bytes past the span (a span cut inside a
+  // character, malformed text) copies the bytes it claims, pads included, and
+  // the text grows by them (:640-662; the open piece is never deleted)
+  ok = true;
   if constexpr (OW) {
     for (int w = 0; w < nw; ++w) {
       const int x = (w << 6) + lane;
@@ -1310,7 +1331,7 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     if (dst != src)
       for (int k = lane; k < 48; k += 64) dst[len + k] = src[len + k];   // pads as they are (:758-767)
     gsync();
-    return len;
+    return len + carry;
   }
   int dpos = 0;
   for (int w = 0; w < nw; ++w) {
@@ -1329,6 +1350,13 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     const uint64_t km = __ballot(keep);
     if (keep) dst[dpos + __popcll(km & lanemask_lt(lane))] = src[x];
     dpos += __popcll(km);
+  }
+  if (carry > 0) {                               // (positions >= dpos are not written yet: in place is safe)
+    gsync();
+    if (lane == 0)
+      for (int k = 0; k < carry; ++k) dst[dpos + k] = src[len + k];
+    dpos += carry;
+    gsync();
   }
   // in place, the bytes from dpos on keep their old values; then "   \0" if
   // at least 4 bytes went, else a single ' ' if any went (:684-689)
@@ -2566,7 +2594,7 @@ __device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, SM& s, W
     wsync();
     if constexpr (VEC) {
       // JustOneItemToVector (:513-548): the span after its leading space
-      if (tb < 1) return false;                      // (a span of one cut character: the sequential kernel)
+      if (tb < 1 && !V->seq) return false;           // (a span of one cut character: the sequential spans)
       const int moff = vec_map_back(*V, 1);
       vec_item(*V, default_language(T, ulscript), moff, vec_map_back(*V, tb) - moff, lane);
     }
@@ -2655,11 +2683,15 @@ __device__ __noinline__ void vec_move_lang(VecState* V, int from_lang, int to_la
 // run on two waves at once and the document costs the longer, not the sum.
 constexpr int kPassesAll = 0, kPassFirstOnly = 1, kPassRepeatsOnly = 2;
 constexpr int kNeedsRepeats = 4;
-template <bool D, bool VEC = false>
+// SEQ: the sequential span source (cld_seq.hip) over page *seqd instead of
+// classify() + next_span() over g (g / L are then that page); its own
+// instantiation, so the parallel one carries none of its registers.
+template <bool D, bool VEC = false, bool SEQ = false>
 __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int L, Slot& S, Smem& s, int lane,
                       cld_result* __restrict__ out, uint32_t* tr, uint32_t doc, uint32_t cflags,
                       const uint32_t* __restrict__ pri, const uint8_t* __restrict__ hf, VecState* V = nullptr,
-                      int mode = kPassesAll, const uint32_t* hp = nullptr, const uint32_t* hg = nullptr) {
+                      int mode = kPassesAll, const uint32_t* hp = nullptr, const uint32_t* hg = nullptr,
+                      const SeqDoc* seqd = nullptr) {
   const int unk = (int)T.unknown_lang;
   // ApplyHints priors (ScoreBoosts, scoreonescriptspan.cc:125-152): boosts as tote adds, whacks as keys
   if (lane == 0) s.has_pri = pri != nullptr;
@@ -2678,14 +2710,15 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
     }
     return 1;
   }
-  if (L > kDocCap - 64) return -kWhyLength;
+  if (!SEQ && L > kDocCap - 64) return -kWhyLength;
   const DocView dv{g, L, hf, hp, hg};
   if constexpr (D) trace(tr, lane, doc, 1, L);
   long long t = (D && s.prof) ? (long long)clock64() : 0;
 
-  bool careful;                                  // a cut last character: span text may be malformed
-  if (!classify(T, dv, S, careful, lane))
-    return -kWhyClassify;
+  bool careful = true;                           // a cut last character: span text may be malformed
+  if constexpr (!SEQ) {
+    if (!classify(T, dv, S, careful, lane)) return -kWhyClassify;
+  }
   if constexpr (D) mark(s, lane, 0, t);
   if constexpr (D) trace(tr, lane, doc, 2, 0);
   // Passes (compact_lang_det_impl.cc:1848-2105): 1 = flags 0; the Squeeze
@@ -2740,10 +2773,13 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         const bool rec = pass == 1 && cache_ok && cur + kLB <= kLbdCap && nsp < kMaxSpans;
         if (pass == 1 && !rec) cache_ok = false;
         if (rec) lb = S.lbd + cur;
-        tb = dv.hp ? next_span<VEC, true>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
-                                          VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr, nullptr, &rlo)
-                   : next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
-                                    VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr);
+        if constexpr (SEQ)
+          tb = seq_span<VEC>(T, *seqd, S, lb, next, ul, st, VEC ? V->vs->omap : nullptr, lane);
+        else
+          tb = dv.hp ? next_span<VEC, true>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
+                                            VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr, nullptr, &rlo)
+                     : next_span<VEC>(T, dv, S, lb, next, ul, st, lane, VEC ? V->vs->omap : nullptr,
+                                      VEC ? V->hpos : nullptr, VEC ? V->hgap : nullptr);
         if (st == 0) break;
         if (st < 0) return -kWhySpan;
         if (rec) {

@@ -209,12 +209,16 @@ __device__ int scan_to_letter_or_special(const DevTables& T, const DocView& d, i
 // `olen` is the reference's logical output capacity (kMaxScriptLowerBuffer);
 // the physical buffer only needs 1.5x the input (max per-char expansion of
 // this table, verified by tests/test_tables.py) plus padding.
-struct DevMap;
-__device__ void dm_copy(DevMap& m, int b);
-__device__ void dm_insert(DevMap& m, int b);
-__device__ void dm_delete(DevMap& m, int b);
+// om (nullable): the map2uplow_ offset map being built (ResultChunkVector
+// mode), any type with copy / insert / del (cld_seq.hip RangeStream).
+struct NoMap {
+  __device__ void copy(int) {}
+  __device__ void insert(int) {}
+  __device__ void del(int) {}
+};
+template <class M = NoMap>
 __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
-                                bool plain = true, DevMap* om = nullptr) {
+                                bool plain = true, M* om = nullptr) {
   const int sh = (int)sm.shift;
   const int nEntries = 1 << sh;
   int total_filled = 0;
@@ -252,16 +256,16 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
         switch (e) {
           case kExitReplace31:
             dst -= 2;
-            if (om) { dm_copy(*om, (int)(src - copystart) - 2); dm_delete(*om, 2); copystart = src; }
+            if (om) { om->copy((int)(src - copystart) - 2); om->del(2); copystart = src; }
             dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace32:
             dst -= 1;
-            if (om) { dm_copy(*om, (int)(src - copystart) - 1); dm_delete(*om, 1); copystart = src; }
+            if (om) { om->copy((int)(src - copystart) - 1); om->del(1); copystart = src; }
             dst[-2] = (uint8_t)sm8(sm, tb + c + nEntries * 2);
             dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace21:
             dst -= 1;
-            if (om) { dm_copy(*om, (int)(src - copystart) - 1); dm_delete(*om, 1); copystart = src; }
+            if (om) { om->copy((int)(src - copystart) - 1); om->del(1); copystart = src; }
             dst[-1] = (uint8_t)sm8(sm, tb + c + nEntries * 1); break;
           case kExitReplace3:
             dst[-3] = (uint8_t)sm8(sm, tb + c + nEntries * 3);
@@ -298,9 +302,9 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
             dst += add_len;
             if (om) {
               if (add_len > del_len) {
-                dm_copy(*om, (int)(src - copystart)); dm_insert(*om, add_len - del_len); copystart = src;
+                om->copy((int)(src - copystart)); om->insert(add_len - del_len); copystart = src;
               } else if (add_len < del_len) {
-                dm_copy(*om, (int)(src - copystart) + add_len - del_len); dm_delete(*om, del_len - add_len);
+                om->copy((int)(src - copystart) + add_len - del_len); om->del(del_len - add_len);
                 copystart = src;
               }
             }
@@ -328,7 +332,7 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
       } else {
         e = kExitOK;
       }
-      if (om && src > copystart) { dm_copy(*om, (int)(src - copystart)); copystart = src; }
+      if (om && src > copystart) { om->copy((int)(src - copystart)); copystart = src; }
     }
     int consumed = (int)(src - in), filled = (int)(dst - out);
     total_filled += filled;
@@ -338,10 +342,6 @@ __device__ int lower_replace_sm(const DevSM& sm, const uint8_t* in0, int ilen, u
   return total_filled;
 }
 
-__device__ __forceinline__ int lower_replace(const DevTables& T, const uint8_t* in0, int ilen, uint8_t* out0, int olen,
-                                             bool plain = true, DevMap* om = nullptr) {
-  return lower_replace_sm(T.lower, in0, ilen, out0, olen, plain, om);
-}
 
 // ------------------------------------------------------------ lang/script
 __device__ __forceinline__ int rtype_of(const DevTables& T, int s) {        // lang_script.cc:154-160
@@ -488,44 +488,6 @@ __device__ __forceinline__ uint32_t octa_lookup(const DevTbl& t, uint64_t h) {
 __device__ __forceinline__ uint32_t ind_at(const DevTbl& t, uint32_t i) { return i < t.n_ind ? gld(t.ind + i) : 0u; }
 
 // ------------------------------------------------------------------ totes
-struct Tote {                                                 // tote.h:33-61
-  uint16_t score[256];      // first: 8-byte aligned groups of four keys
-  uint64_t in_use;
-  int score_count;
-  __device__ void reinit() { in_use = 0; score_count = 0; }
-  __device__ void add(uint8_t key, int delta) {              // tote.cc:52-61
-    int g = key >> 2;
-    uint64_t m = 1ull << g;
-    if (!(in_use & m)) {
-      *reinterpret_cast<uint64_t*>(&score[g * 4]) = 0;
-      in_use |= m;
-    }
-    score[key] = (uint16_t)(score[key] + delta);
-  }
-  __device__ void top3(int* key3) const {                    // tote.cc:65-101
-    key3[0] = key3[1] = key3[2] = -1;
-    int s0 = -1, s1 = -1, s2 = -1;
-    uint64_t m = in_use;
-    while (m) {
-      int g = __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      for (int i = 0; i < 4; ++i) {
-        int k = g * 4 + i;
-        int v = score[k];
-        if (v > s2) {
-          if (v > s1) {
-            s2 = s1; key3[2] = key3[1];
-            if (v > s0) { s1 = s0; key3[1] = key3[0]; s0 = v; key3[0] = k; }
-            else { s1 = v; key3[1] = k; }
-          } else {
-            s2 = v; key3[2] = k;
-          }
-        }
-      }
-    }
-  }
-};
-
 struct DocTote {                                              // tote.h:65-107
   int incr_count;
   int sorted;
@@ -579,17 +541,6 @@ struct DocTote {                                              // tote.h:65-107
   }
 };
 
-struct Boosts { int n; uint32_t lp[kMaxBoosts]; };            // scoreonescriptspan.h:116-120
-
-// ProcessProbV2Tote cldutil.cc:128-138
-__device__ __forceinline__ void add_lang_prob(const DevTables& T, uint32_t lp, Tote& t) {
-  const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
-  uint8_t k1 = (lp >> 8) & 0xFF, k2 = (lp >> 16) & 0xFF, k3 = (lp >> 24) & 0xFF;
-  if (k1) t.add(k1, e[5]);
-  if (k2) t.add(k2, e[6]);
-  if (k3) t.add(k3, e[7]);
-}
-
 // ReliabilityDelta cldutil.cc:553-571
 __device__ int reliability_delta(int v1, int v2, int grams) {
   int maxr = grams < 8 ? 12 * grams : 100;
@@ -611,142 +562,6 @@ __device__ int reliability_expected(int actual, int expected) {
   double num = __dmul_rn(100.0, 4.0 - ratio);
   return (int)__ddiv_rn(num, 2.5);
 }
-
-// ------------------------------------------------------------- workspaces
-// Per-lane state.  Capacities are template constants so the short kernel can
-// keep everything in private memory; the general kernel instantiates the
-// reference maxima in a global per-lane arena.
-template <int SB_, int LB_, int HB_, bool MULTIPASS_>
-struct Work {
-  static constexpr int SB = SB_, LB = LB_, HB = HB_;
-  static constexpr bool MULTIPASS = MULTIPASS_;
-  uint8_t sbuf[SB + 16];
-  uint8_t lbuf[LB + 16];
-  uint16_t b_off[HB + 1]; uint32_t b_ind[HB + 1];
-  uint16_t d_off[HB + 1]; uint32_t d_ind[HB + 1];
-  uint16_t x_off[HB + 1]; uint32_t x_ind[HB + 1];
-  Tote tote;
-  int predict[MULTIPASS_ ? kPredictionTableSize : 1];
-  int sqz[MULTIPASS_ ? kPredictionTableSize : 1];
-};
-
-struct Span { uint8_t* text; int text_bytes; int ulscript; };
-
-// Thrown (as a flag) when a short-kernel capacity would be exceeded or more
-// passes are needed: the document is re-queued for the general kernel.
-struct Status { bool requeue; };
-
-// ------------------------------------------------- ResultChunkVector mode
-// OffsetMap (offsetmap.cc:43-453): copy / insert / delete ranges from the
-// document (A) to the text built from it (A'), one byte per range in the
-// reference's coding (2-bit op, 6-bit length, prefix bytes for long ranges,
-// adjacent copies merged).  Built by the scanner (map2original_) and the
-// lowercaser (map2uplow_) only when a document asks for its chunk vector.
-enum { DM_PREFIX = 0, DM_COPY = 1, DM_INSERT = 2, DM_DELETE = 3 };
-struct DevMap {
-  uint8_t* d; int n, cap;
-  int pend_op, pend_len, max_a, max_ap;
-  bool over;                                  // capacity exceeded: the document reports an error
-  // MapBack's resume point: the start (byte index, A and A' offsets) of the
-  // range the last lookup settled on.  Entries before it never change (the
-  // map only grows at its end), and every range before it ends at or below
-  // its A' offset, so a lookup at or past that offset may start there: the
-  // summary buffer maps its chunks in increasing order, which made MapBack
-  // quadratic in the span length when every lookup walked from the start.
-  int cur_i, cur_a, cur_ap;
-};
-__device__ void dm_push(DevMap& m, int op, int len) {           // Emit :203-206
-  if (m.n >= m.cap) { m.over = true; return; }
-  m.d[m.n++] = (uint8_t)((op << 6) | (len & 0x3F));
-}
-__device__ void dm_clear(DevMap& m) {
-  m.n = 0; m.pend_op = DM_COPY; m.pend_len = 0; m.max_a = 0; m.max_ap = 0;
-  m.cur_i = 0; m.cur_a = 0; m.cur_ap = 0;
-}
-__device__ void dm_flush(DevMap& m) {                           // Flush :158-187
-  if (m.pend_len == 0) return;
-  if (m.pend_op == DM_COPY && m.n > 0) {
-    const uint8_t c = m.d[m.n - 1];
-    if ((c >> 6) == DM_COPY && (c & 0x3F) + m.pend_len <= 0x3F) {
-      m.d[m.n - 1] = (uint8_t)(c + m.pend_len);
-      m.pend_len = 0;
-      return;
-    }
-  }
-  if (m.pend_len > 0x3F) {
-    bool nz = false;
-    for (int shift = 30; shift > 0; shift -= 6) {
-      const int prefix = (m.pend_len >> shift) & 0x3F;
-      if (prefix > 0 || nz) { dm_push(m, DM_PREFIX, prefix); nz = true; }
-    }
-  }
-  dm_push(m, m.pend_op, m.pend_len & 0x3F);
-  m.pend_len = 0;
-}
-__device__ void dm_copy(DevMap& m, int b) {                     // Copy :107-118
-  if (b == 0) return;
-  m.max_a += b; m.max_ap += b;
-  if (m.pend_op == DM_COPY) m.pend_len += b;
-  else { dm_flush(m); m.pend_op = DM_COPY; m.pend_len = b; }
-}
-__device__ void dm_insert(DevMap& m, int b) {                   // Insert :122-138
-  if (b == 0) return;
-  m.max_ap += b;
-  if (m.pend_op == DM_INSERT) m.pend_len += b;
-  else if (b == 1 && m.pend_op == DM_DELETE && m.pend_len == 1) m.pend_op = DM_COPY;
-  else { dm_flush(m); m.pend_op = DM_INSERT; m.pend_len = b; }
-}
-__device__ void dm_delete(DevMap& m, int b) {                   // Delete :141-156
-  if (b == 0) return;
-  m.max_a += b;
-  if (m.pend_op == DM_DELETE) m.pend_len += b;
-  else if (b == 1 && m.pend_op == DM_INSERT && m.pend_len == 1) m.pend_op = DM_COPY;
-  else { dm_flush(m); m.pend_op = DM_DELETE; m.pend_len = b; }
-}
-__device__ void dm_reset(DevMap& m) {                           // Reset -> MaybeFlushAll :190-200
-  if (0 < m.pend_len || m.n == 0) { dm_copy(m, 1); dm_flush(m); }
-}
-// MapBack :428-452: the range of non-zero A' width that holds ap (the
-// reference's window walk settles on the same one).
-__device__ int dm_map_back(DevMap& m, int ap) {
-  dm_reset(m);
-  if (ap < 0) return 0;
-  if (m.max_ap <= ap) return (ap - m.max_ap) + m.max_a;
-  int lo_a = 0, lo_ap = 0, i = 0;
-  if (m.cur_ap <= ap) { i = m.cur_i; lo_a = m.cur_a; lo_ap = m.cur_ap; }
-  while (i < m.n) {
-    const int i0 = i;
-    int op = DM_PREFIX, len = 0;
-    while (i < m.n && op == DM_PREFIX) {
-      const uint8_t c = m.d[i++];
-      op = c >> 6;
-      len = (len << 6) + (c & 0x3F);
-    }
-    if (op == DM_PREFIX) break;
-    const int hi_a = lo_a + (op == DM_INSERT ? 0 : len), hi_ap = lo_ap + (op == DM_DELETE ? 0 : len);
-    if (ap < hi_ap) {
-      m.cur_i = i0; m.cur_a = lo_a; m.cur_ap = lo_ap;
-      const int a = ap - (lo_ap - lo_a);
-      return a >= hi_a ? hi_a : a;
-    }
-    lo_a = hi_a; lo_ap = hi_ap;
-  }
-  return (ap - m.max_ap) + m.max_a;
-}
-
-// SetChunkSummary's fields (scoreonescriptspan.h:240-252) as the vector path keeps them
-struct ChunkSum { uint16_t offset, chunk_start, lang1, lang2, score1, bytes; uint8_t rd, rs; };
-constexpr int kVecLinear = 4 * (kMaxScoringHits + 8) + 8;
-
-// Per-document vector state (in the lane's arena) for k_general_vec.
-struct VecOut {
-  DevMap orig, low;                           // map2original_, map2uplow_
-  cld_chunk* v; int n, cap; bool over;        // the document's ResultChunkVector (its pool region)
-  const uint8_t* doc; int doc_len;            // the original document (SummaryBufferToVector backs up in it)
-  uint32_t lin_lp[kVecLinear];                // this round's linear[] langprobs and offsets
-  uint16_t lin_off[kVecLinear];
-  ChunkSum sb[kMaxSummaries + 1];             // the round's summary buffer + the dummy off the end
-};
 
 // ------------------------------------------------------------ HTML mode
 // IsSpecial (getonescriptspan.cc:470-477)
@@ -953,634 +768,10 @@ struct BufView {
   __device__ __forceinline__ uint8_t at(int i) const { return p[i]; }
 };
 
-// ------------------------------------------------------------- scanner
-// ScriptScanner::SkipToFrontOfSpan: getonescriptspan.cc:592-642
-__device__ int skip_to_front_of_span(const DevTables& T, const DocView& d, int start, int len, int* script,
-                                     bool plain) {
-  int sc = 0, skip = 0, tlen = 0, plen = 0;
-  while (skip < len) {
-    skip += scan_to_letter_or_special(T, d, start + skip, len - skip);
-    if (skip >= len) { *script = sc; return len; }
-    const uint8_t c = d.at(start + skip);
-    if (!plain && is_special(c)) {
-      if (c == '<') {
-        tlen = scan_to_possible_letter(d, start + skip, len - skip);
-        sc = 0;
-      } else if (c == '>') {
-        tlen = 1;
-        sc = 0;
-      } else {                                   // '&': expand, no advance
-        uint8_t tmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        entity_to_buffer(T, d, start + skip, len - skip, tmp, &tlen, &plen);
-        if (plen > 0) sc = script_num(T, BufView{tmp}, 0);
-      }
-    } else {
-      tlen = utf8_len(c);
-      sc = script_num(T, d, start + skip);
-    }
-    if (sc != 0) break;
-    skip += tlen;
-  }
-  *script = sc;
-  return skip;
-}
-
-// ScriptScanner::GetOneScriptSpan: getonescriptspan.cc:799-1027 (HTML mode
-// when !plain: tags skipped, entities decoded into the span).
-// `next`/`remaining` are next_byte_ - start_byte_ and byte_length_.
-template <class W>
-__device__ bool get_one_script_span(const DevTables& T, const DocView& d, int& next, int& remaining,
-                                    W& w, Span& span, Status& st, bool plain = true, DevMap* mo = nullptr) {
-  const int common = (int)T.common, inherited = (int)T.inherited;
-  span.text = w.sbuf; span.text_bytes = 0; span.ulscript = 0;
-  if (mo) { dm_clear(*mo); dm_delete(*mo, next); }    // map2original_: MapBack(0) = span offset (:835-836)
-  int put_soft_limit = kMaxScriptBytes - kWithinScriptTail;
-  if (kMaxScriptBytes <= remaining && remaining < 2 * kMaxScriptBytes) put_soft_limit = remaining / 2;
-  int spanscript, sc = 0, tlen = 0, plen = 0;
-  uint8_t* sb = w.sbuf;
-  sb[0] = ' '; sb[1] = 0;
-  int take = 0, put = 1;
-  int skip = skip_to_front_of_span(T, d, next, remaining, &spanscript, plain);
-  next += skip; remaining -= skip;
-  if (mo) {
-    if (skip != 1) { dm_delete(*mo, skip); dm_insert(*mo, 1); }
-    else dm_copy(*mo, 1);
-  }
-  if (remaining <= 0) { if (mo) dm_reset(*mo); return false; }
-  span.ulscript = spanscript;
-  const int base = next, bl = remaining;
-  while (take < bl) {
-    bool need_break = false;
-    while (take < bl) {
-      uint8_t c0 = d.at(base + take);
-      if (put + 4 > W::SB) { st.requeue = true; return false; }
-      if (!plain && is_special(c0)) {
-        if (c0 == '<' || c0 == '>') { sc = 0; break; }
-        entity_to_buffer(T, d, base + take, bl - take, sb + put, &tlen, &plen);   // '&': copy entity, no advance
-        if (plen > 0) sc = script_num(T, BufView{sb + put}, 0);
-      } else {
-        tlen = plen = utf8_len(c0);
-        if (take < bl - 3) {
-          sb[put] = c0; sb[put + 1] = d.at(base + take + 1);
-          sb[put + 2] = d.at(base + take + 2); sb[put + 3] = d.at(base + take + 3);
-        } else {
-          for (int k = 0; k < plen; ++k) sb[put + k] = d.at(base + take + k);
-        }
-        sc = script_num(T, d, base + take);
-      }
-      if (sc != spanscript && sc != inherited) {
-        if (sc == common) {
-          need_break = true;
-        } else {
-          int sc2 = script_num(T, d, base + take + tlen);
-          if (sc2 != common && sc2 != spanscript) need_break = true;
-        }
-      }
-      if (need_break) break;
-      take += tlen; put += plen;
-      if (mo) {
-        if (tlen == plen) dm_copy(*mo, tlen);
-        else if (tlen < plen) { dm_copy(*mo, tlen); dm_insert(*mo, plen - tlen); }
-        else { dm_copy(*mo, plen); dm_delete(*mo, tlen - plen); }
-      }
-      if (put >= kMaxScriptBytes) break;
-    }
-    while (take < bl) {
-      tlen = scan_to_letter_or_special(T, d, base + take, bl - take);
-      take += tlen;
-      if (mo) dm_delete(*mo, tlen);
-      if (take >= bl) break;
-      const uint8_t c1 = d.at(base + take);
-      if (!plain && is_special(c1)) {
-        if (c1 == '<') {
-          tlen = scan_to_possible_letter(d, base + take, bl - take);
-          sc = 0;
-        } else if (c1 == '>') {
-          tlen = 1;
-          sc = 0;
-        } else {                                 // '&': expand, no advance
-          if (put + 4 > W::SB) { st.requeue = true; return false; }
-          entity_to_buffer(T, d, base + take, bl - take, sb + put, &tlen, &plen);
-          if (plen > 0) sc = script_num(T, BufView{sb + put}, 0);
-        }
-      } else {
-        tlen = utf8_len(c1);
-        sc = script_num(T, d, base + take);
-      }
-      if (sc != 0) break;
-      take += tlen;
-      if (mo) dm_delete(*mo, tlen);
-    }
-    if (put + 1 > W::SB) { st.requeue = true; return false; }
-    sb[put++] = ' ';
-    if (mo) dm_insert(*mo, 1);
-    if (sc != spanscript && sc != inherited) break;
-    if (put >= put_soft_limit) break;
-  }
-  while (0 < take && take < bl && (d.at(base + take) & 0xC0) == 0x80) { --take; --put; }
-  next += take; remaining -= take;
-  if (put + 4 > W::SB) { st.requeue = true; return false; }
-  sb[put] = ' '; sb[put + 1] = ' '; sb[put + 2] = ' '; sb[put + 3] = 0;
-  if (mo) { dm_insert(*mo, 4); dm_reset(*mo); }
-  span.text_bytes = put;
-  return true;
-}
-
-// ScriptScanner::LowerScriptSpan getonescriptspan.cc:1033-1054
-template <class W>
-__device__ void lower_script_span(const DevTables& T, W& w, Span& span, Status& st, bool plain = true,
-                                  DevMap* ml = nullptr) {
-  int ilen = span.text_bytes + 3;
-  // HTML mode may map a character to more bytes (the &amp;-style half of a
-  // remap pair): then only the reference's own capacity bounds it
-  if ((plain ? (ilen * 3) / 2 + 4 : kMaxScriptLowerBuffer) > W::LB) { st.requeue = true; return; }
-  if (ml) dm_clear(*ml);
-  int filled = lower_replace(T, span.text, ilen, w.lbuf, kMaxScriptLowerBuffer, plain, ml);
-  w.lbuf[filled] = 0; w.lbuf[filled + 1] = 0; w.lbuf[filled + 2] = 0; w.lbuf[filled + 3] = 0;
-  span.text = w.lbuf;
-  span.text_bytes = filled - 3;
-  if (ml) dm_reset(*ml);
-}
-
-// ---------------------------------------------------------- squeezing
-__device__ int backscan_to_space(const uint8_t* src, int limit) {        // :491-504
-  int n = 0;
-  if (limit > 32) limit = 32;
-  while (n < limit) { if (src[-n - 1] == ' ') return n; ++n; }
-  n = 0;
-  while (n < limit) { if ((src[-n] & 0xC0) != 0x80) return n; ++n; }
-  return 0;
-}
-__device__ int forwardscan_to_space(const uint8_t* src, int limit) {     // :509-522
-  int n = 0;
-  if (limit > 32) limit = 32;
-  while (n < limit) { if (src[n] == ' ') return n + 1; ++n; }
-  n = 0;
-  while (n < limit) { if ((src[n] & 0xC0) != 0x80) return n; ++n; }
-  return 0;
-}
-__device__ __forceinline__ int next_char_code(const uint8_t* src, int* incr) {
-  int c = src[0];
-  *incr = 1;
-  if (c < 0xC0) {
-  } else if ((c & 0xE0) == 0xC0) { c = (c << 8) | src[1]; *incr = 2; }
-  else if ((c & 0xF0) == 0xE0) { c = (c << 16) | (src[1] << 8) | src[2]; *incr = 3; }
-  else { c = (int)(((uint32_t)c << 24) | ((uint32_t)src[1] << 16) | ((uint32_t)src[2] << 8) | src[3]); *incr = 4; }
-  return c;
-}
-__device__ int count_predicted_bytes(const uint8_t* src, int len, int* hash, int* tbl) {  // :541-580
-  int p_count = 0, h = *hash;
-  const uint8_t* lim = src + len;
-  while (src < lim) {
-    int incr;
-    int c = next_char_code(src, &incr);
-    src += incr;
-    int p = tbl[h];
-    tbl[h] = c;
-    if (c == p) p_count += incr;
-    h = ((h << 4) ^ c) & 0xFFF;
-  }
-  *hash = h;
-  return p_count;
-}
-__device__ int count_spaces4(const uint8_t* src, int len) {              // :586-595
-  int s = 0;
-  for (int i = 0; i < (len & ~3); i += 4)
-    s += (src[i] == ' ') + (src[i + 1] == ' ') + (src[i + 2] == ' ') + (src[i + 3] == ' ');
-  return s;
-}
-__device__ int cheap_rep_words_inplace(uint8_t* isrc, int src_len, int* hash, int* tbl) {  // :610-692
-  const uint8_t* src = isrc;
-  const uint8_t* lim = isrc + src_len;
-  uint8_t* dst = isrc;
-  int h = *hash;
-  uint8_t* word_dst = dst;
-  int good = 0, wlen = 0;
-  while (src < lim) {
-    int c = src[0];
-    *dst++ = (uint8_t)c;
-    if (c == ' ') {
-      if (good * 2 > wlen) dst = word_dst;
-      word_dst = dst; good = 0; wlen = 0;
-    }
-    int incr = 1;
-    if (c < 0xC0) {
-    } else if ((c & 0xE0) == 0xC0) { *dst++ = src[1]; c = (c << 8) | src[1]; incr = 2; }
-    else if ((c & 0xF0) == 0xE0) { *dst++ = src[1]; *dst++ = src[2]; c = (c << 16) | (src[1] << 8) | src[2]; incr = 3; }
-    else {
-      *dst++ = src[1]; *dst++ = src[2]; *dst++ = src[3];
-      c = (int)(((uint32_t)c << 24) | ((uint32_t)src[1] << 16) | ((uint32_t)src[2] << 8) | src[3]); incr = 4;
-    }
-    src += incr;
-    wlen += incr;
-    int p = tbl[h];
-    tbl[h] = c;
-    if (c == p) good += incr;
-    h = ((h << 4) ^ c) & 0xFFF;
-  }
-  *hash = h;
-  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
-  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
-  return (int)(dst - isrc);
-}
-__device__ int cheap_squeeze_inplace(uint8_t* isrc, int src_len, int* tbl) {  // :785-865
-  uint8_t* src = isrc;
-  uint8_t* dst = src;
-  uint8_t* lim = src + src_len;
-  bool skipping = false;
-  int hash = 0;
-  for (int i = 0; i < kPredictionTableSize; ++i) tbl[i] = 0;
-  const int chunksize = 48, space_thresh = (48 * 25) / 100, predict_thresh = (48 * 40) / 100;
-  while (src < lim) {
-    int remaining = (int)(lim - src);
-    int len = remaining < chunksize ? remaining : chunksize;
-    while ((src[len] & 0xC0) == 0x80) ++len;
-    int space_n = count_spaces4(src, len);
-    int predb_n = count_predicted_bytes(src, len, &hash, tbl);
-    if (space_n >= space_thresh || predb_n >= predict_thresh) {
-      if (!skipping) {
-        int n = backscan_to_space(dst, (int)(dst - isrc));
-        dst -= n;
-        if (dst == isrc) *dst++ = ' ';
-        skipping = true;
-      }
-    } else {
-      if (skipping) {
-        int n = forwardscan_to_space(src, len);
-        src += n; remaining -= n; len -= n;
-        skipping = false;
-      }
-      if (len > 0) {
-        for (int k = 0; k < len; ++k) dst[k] = src[k];   // memmove, dst <= src
-        dst += len;
-      }
-    }
-    src += len;
-  }
-  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
-  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
-  return (int)(dst - isrc);
-}
-// ResultChunkVector mode keeps offsets: the Overwrite variants turn the
-// dropped text into '.' runs in place (:697-765, :869-939).
-__device__ int cheap_rep_words_inplace_overwrite(uint8_t* isrc, int src_len, int* hash, int* tbl) {
-  const uint8_t* src = isrc;
-  const uint8_t* lim = isrc + src_len;
-  uint8_t* dst = isrc;
-  int h = *hash;
-  uint8_t* word_dst = dst;
-  int good = 0, wlen = 0;
-  while (src < lim) {
-    int c = src[0];
-    *dst++ = (uint8_t)c;
-    if (c == ' ') {
-      if (good * 2 > wlen)
-        for (uint8_t* q = word_dst; q < dst - 1; ++q) *q = '.';
-      word_dst = dst; good = 0; wlen = 0;
-    }
-    int incr = 1;
-    if (c < 0xC0) {
-    } else if ((c & 0xE0) == 0xC0) { *dst++ = src[1]; c = (c << 8) | src[1]; incr = 2; }
-    else if ((c & 0xF0) == 0xE0) { *dst++ = src[1]; *dst++ = src[2]; c = (c << 16) | (src[1] << 8) | src[2]; incr = 3; }
-    else {
-      *dst++ = src[1]; *dst++ = src[2]; *dst++ = src[3];
-      c = (int)(((uint32_t)c << 24) | ((uint32_t)src[1] << 16) | ((uint32_t)src[2] << 8) | src[3]); incr = 4;
-    }
-    src += incr;
-    wlen += incr;
-    int p = tbl[h];
-    tbl[h] = c;
-    if (c == p) good += incr;
-    h = ((h << 4) ^ c) & 0xFFF;
-  }
-  *hash = h;
-  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
-  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
-  return (int)(dst - isrc);
-}
-__device__ int cheap_squeeze_inplace_overwrite(uint8_t* isrc, int src_len, int* tbl) {
-  uint8_t* src = isrc;
-  uint8_t* dst = src;
-  uint8_t* lim = src + src_len;
-  bool skipping = false;
-  int hash = 0;
-  for (int i = 0; i < kPredictionTableSize; ++i) tbl[i] = 0;
-  const int chunksize = 48, space_thresh = (48 * 25) / 100, predict_thresh = (48 * 40) / 100;
-  ++src; ++dst;                                      // always keep the leading space
-  while (src < lim) {
-    int remaining = (int)(lim - src);
-    int len = remaining < chunksize ? remaining : chunksize;
-    while ((src[len] & 0xC0) == 0x80) ++len;
-    int space_n = count_spaces4(src, len);
-    int predb_n = count_predicted_bytes(src, len, &hash, tbl);
-    if (space_n >= space_thresh || predb_n >= predict_thresh) {
-      if (!skipping) {
-        int n = backscan_to_space(dst, (int)(dst - isrc));
-        for (uint8_t* q = dst - n; q < dst; ++q) *q = '.';
-        skipping = true;
-      }
-      for (uint8_t* q = dst; q < dst + len; ++q) *q = '.';
-      dst[len - 1] = ' ';
-    } else if (skipping) {
-      int n = forwardscan_to_space(src, len);
-      for (uint8_t* q = dst; q < dst + n - 1; ++q) *q = '.';
-      skipping = false;
-    }
-    dst += len;
-    src += len;
-  }
-  if ((dst - isrc) < (src_len - 3)) { dst[0] = ' '; dst[1] = ' '; dst[2] = ' '; dst[3] = 0; }
-  else if ((dst - isrc) < src_len) { dst[0] = ' '; }
-  return (int)(dst - isrc);
-}
-__device__ bool cheap_squeeze_trigger_test(const uint8_t* src, int src_len, int* tbl) {  // :952-971
-  const int testsize = 256;
-  if (src_len < testsize) return false;
-  if (count_spaces4(src, testsize) >= (testsize * 25) / 100) return true;
-  for (int i = 0; i < kPredictionTableSize; ++i) tbl[i] = 0;
-  int hash = 0;
-  return count_predicted_bytes(src, testsize, &hash, tbl) >= (testsize * 67) / 100;
-}
-
-// ------------------------------------------------------------ hit streams
-// GetQuadHits cldutil.cc:315-405
-template <class W>
-__device__ int get_quad_hits(const DevTables& T, const uint8_t* text, int off, int limit, W& w, int& nb, Status& st) {
-  const uint8_t* src = text + off;
-  const uint8_t* lim = text + limit;
-  int npq = 0;
-  uint32_t pq0 = 0, pq1 = 0;
-  if (src[0] == ' ') ++src;
-  while (src < lim) {
-    const uint8_t* e = src;
-    e += adv_but_space(e[0]); e += adv_but_space(e[0]);
-    const uint8_t* mid = e;
-    e += adv_but_space(e[0]); e += adv_but_space(e[0]);
-    uint32_t h = quad_hash_v2(src, (int)(e - src));
-    if (h != pq0 && h != pq1) {
-      uint32_t flag = 0;
-      const DevTbl* hit = &T.quad;
-      uint32_t probs = quad_lookup(T.quad, h);
-      if (probs == 0 && T.quad2.size != 0) {
-        flag = 0x80000000u; hit = &T.quad2;
-        probs = quad_lookup(T.quad2, h);
-      }
-      if (probs != 0) {
-        if (npq == 0) pq0 = h; else pq1 = h;
-        npq ^= 1;
-        if (nb >= W::HB) { st.requeue = true; return 0; }
-        w.b_off[nb] = (uint16_t)(src - text);
-        w.b_ind[nb] = (probs & ~hit->key_mask) | flag;
-        ++nb;
-      }
-    }
-    src = (e[0] == ' ') ? e : mid;
-    if (src < lim) src += adv_space_vowel(src[0]);
-    else src = lim;
-    if (nb >= kMaxScoringHits) break;
-  }
-  w.b_off[nb] = (uint16_t)(src - text);
-  w.b_ind[nb] = 0;
-  return (int)(src - text);
-}
-
-// GetOctaHits cldutil.cc:416-533
-template <class W>
-__device__ void get_octa_hits(const DevTables& T, const uint8_t* text, int off, int limit, W& w,
-                              int& nd, int& nx, Status& st) {
-  const uint8_t* src = text + off;
-  const uint8_t* lim = text + limit + 1;
-  int npo = 0;
-  uint64_t po[2] = {0, 0};
-  int charcount = 0;
-  if (src[0] == ' ') ++src;
-  const uint8_t* prior_word_start = src;
-  const uint8_t* word_start = src;
-  const uint8_t* word_end = src;
-  while (src < lim) {
-    if (src[0] == ' ') {
-      uint64_t wh = octa_hash40(word_start, (int)(word_end - word_start));
-      if (wh != po[0] && wh != po[1]) {
-        po[npo] = wh; npo = 1 - npo;
-        uint64_t tph = po[npo];
-        if (nx + 2 > W::HB || nd + 1 > W::HB) { st.requeue = true; return; }
-        if (tph != 0 && tph != wh) {
-          uint32_t probs = octa_lookup(T.distinctocta, pair_hash(tph, wh));
-          if (probs) {
-            w.x_off[nx] = (uint16_t)(prior_word_start - text);
-            w.x_ind[nx] = probs & ~T.distinctocta.key_mask;
-            ++nx;
-          }
-        }
-        uint32_t probs = octa_lookup(T.distinctocta, wh);
-        if (probs) {
-          w.x_off[nx] = (uint16_t)(word_start - text);
-          w.x_ind[nx] = probs & ~T.distinctocta.key_mask;
-          ++nx;
-        }
-        probs = octa_lookup(T.deltaocta, wh);
-        if (probs) {
-          w.d_off[nd] = (uint16_t)(word_start - text);
-          w.d_ind[nd] = probs & ~T.deltaocta.key_mask;
-          ++nd;
-        }
-      }
-      charcount = 0;
-      prior_word_start = word_start;
-      word_start = src + 1;
-      word_end = word_start;
-    } else {
-      ++charcount;
-    }
-    src += utf8_len(src[0]);
-    if (charcount <= 8) word_end = src;
-    if (nd >= kMaxScoringHits) break;
-    if (nx >= kMaxScoringHits - 1) break;
-  }
-  uint16_t dummy = (uint16_t)(src - text);
-  w.d_off[nd] = dummy; w.d_ind[nd] = 0;
-  w.x_off[nx] = dummy; w.x_ind[nx] = 0;
-}
-
-// GetUniHits cldutil.cc:201-244
-template <class W>
-__device__ int get_uni_hits(const DevTables& T, const uint8_t* text, int off, int limit, W& w, int& nb, Status& st) {
-  const uint8_t* src = text + off;
-  const uint8_t* lim = text + limit;
-  if (src[0] == ' ') ++src;
-  while (src < lim) {
-    const uint8_t* us = src;
-    int len = utf8_len(us[0]);
-    src += len;
-    int propval = uni_prop(T, us, len);
-    if (propval > 0) {
-      if (nb >= W::HB) { st.requeue = true; return 0; }
-      w.b_off[nb] = (uint16_t)(src - text);
-      w.b_ind[nb] = (uint32_t)propval;
-      ++nb;
-    }
-    if (nb >= kMaxScoringHits) break;
-  }
-  w.b_off[nb] = (uint16_t)(src - text);
-  w.b_ind[nb] = 0;
-  return (int)(src - text);
-}
-
-// GetBiHits cldutil.cc:248-310
-template <class W>
-__device__ void get_bi_hits(const DevTables& T, const uint8_t* text, int off, int limit, W& w,
-                            int& nd, int& nx, Status& st) {
-  const uint8_t* src = text + off;
-  const uint8_t* lim = text + limit;
-  while (src < lim) {
-    int len = utf8_len(src[0]);
-    int len2 = utf8_len(src[len]) + len;
-    if (6 <= len2) {
-      uint32_t bh = bi_hash_v2(src, len2);
-      if (nd + 1 > W::HB || nx + 1 > W::HB) { st.requeue = true; return; }
-      uint32_t probs = quad_lookup(T.deltabi, bh);
-      if (probs) {
-        w.d_off[nd] = (uint16_t)(src - text); w.d_ind[nd] = probs & ~T.deltabi.key_mask; ++nd;
-      }
-      probs = quad_lookup(T.distinctbi, bh);
-      if (probs) {
-        w.x_off[nx] = (uint16_t)(src - text); w.x_ind[nx] = probs & ~T.distinctbi.key_mask; ++nx;
-      }
-    }
-    src += len;
-    if (nd >= kMaxScoringHits) break;
-    if (nx >= kMaxScoringHits - 1) break;
-  }
-  uint16_t dummy = (uint16_t)(src - text);
-  w.d_off[nd] = dummy; w.d_ind[nd] = 0;
-  w.x_off[nx] = dummy; w.x_ind[nx] = 0;
-}
-
-// ------------------------------------------------- linearize + chunk (fused)
-// LinearizeAll (scoreonescriptspan.cc:856-975) as a generator: yields the
-// linear[] entries in order without materialising the array.
-struct LinearEntry { int offset; int type; uint32_t langprob; };
-
-template <class W>
-struct Linearizer {
-  const DevTables* T;
-  const W* w;
-  const DevTbl *base_obj, *base_obj2, *delta_obj, *distinct_obj;
-  int base_hit;
-  int bi, di, xi, bl, dl, xl;
-  bool seed_pending;
-  uint32_t seed_lp;
-  int seed_off;
-  bool pend2;                 // second langprob of a two-langprob base hit
-  LinearEntry pend;
-
-  __device__ void init(const DevTables& TT, const W& ww, bool cjk, int nb, int nd, int nx, int lowest,
-                       uint32_t seed) {
-    T = &TT; w = &ww;
-    if (cjk) { base_obj = &TT.compat; base_obj2 = &TT.compat; delta_obj = &TT.deltabi; distinct_obj = &TT.distinctbi; base_hit = UNIHIT; }
-    else { base_obj = &TT.quad; base_obj2 = &TT.quad2; delta_obj = &TT.deltaocta; distinct_obj = &TT.distinctocta; base_hit = QUADHIT; }
-    bi = di = xi = 0; bl = nb; dl = nd; xl = nx;
-    seed_pending = true; seed_lp = seed; seed_off = lowest; pend2 = false;
-  }
-
-  __device__ bool next(LinearEntry& e) {
-    if (seed_pending) {
-      seed_pending = false;
-      e.offset = seed_off; e.type = base_hit; e.langprob = seed_lp;
-      return true;
-    }
-    if (pend2) { pend2 = false; e = pend; return true; }
-    while (bi < bl || di < dl || xi < xl) {
-      int boff = w->b_off[bi], doff = w->d_off[di], xoff = w->x_off[xi];
-      if (di < dl && doff <= boff && doff <= xoff) {
-        uint32_t lp = ind_at(*delta_obj, w->d_ind[di]);
-        ++di;
-        if (lp > 0) { e.offset = doff; e.type = DELTAHIT; e.langprob = lp; return true; }
-      } else if (xi < xl && xoff <= boff && xoff <= doff) {
-        uint32_t lp = ind_at(*distinct_obj, w->x_ind[xi]);
-        ++xi;
-        if (lp > 0) { e.offset = xoff; e.type = DISTINCTHIT; e.langprob = lp; return true; }
-      } else {
-        uint32_t ind = w->b_ind[bi];
-        const DevTbl* lb = base_obj;
-        if (ind & 0x80000000u) { lb = base_obj2; ind &= ~0x80000000u; }
-        ++bi;
-        if (ind < lb->size_one) {
-          uint32_t lp = ind_at(*lb, ind);
-          if (lp > 0) { e.offset = boff; e.type = base_hit; e.langprob = lp; return true; }
-        } else {
-          ind += ind - lb->size_one;
-          uint32_t lp = ind_at(*lb, ind), lp2 = ind_at(*lb, ind + 1);
-          if (lp > 0 && lp2 > 0) {
-            e.offset = boff; e.type = base_hit; e.langprob = lp;
-            pend.offset = boff; pend.type = base_hit; pend.langprob = lp2; pend2 = true;
-            return true;
-          }
-          if (lp > 0) { e.offset = boff; e.type = base_hit; e.langprob = lp; return true; }
-          if (lp2 > 0) { e.offset = boff; e.type = base_hit; e.langprob = lp2; return true; }
-        }
-      }
-    }
-    return false;
-  }
-};
-
-struct Ctx {
-  int ulscript;
-  Boosts latn, othr;        // ScoringContext::distinct_boost (scoreonescriptspan.h:139)
-  // ApplyHints result (compact_lang_det_impl.cc:1645-1684): langprior_boost
-  // latn[4] othr[4], then langprior_whack latn[4] othr[4]; null for none
-  const uint32_t* priors;
-  VecOut* vo;               // ResultChunkVector being built (k_general_vec), else null
-  int flags;                // the caller's public flags (kCLDFlagScoreAsQuads / kCLDFlagBestEffort)
-};
-
-// SetChunkSummary scoreonescriptspan.cc:60-96
-__device__ ChunkSum chunk_summary(const DevTables& T, int ulscript, int lo, int hi, int first_linear, const Tote& t) {
-  int key3[3];
-  t.top3(key3);
-  int lang1 = from_per_script_number(T, ulscript, (uint8_t)key3[0]);
-  int lang2 = from_per_script_number(T, ulscript, (uint8_t)key3[1]);
-  int len = hi - lo;
-  int sc1 = key3[0] >= 0 ? t.score[key3[0]] : 0;
-  int sc2 = key3[1] >= 0 ? t.score[key3[1]] : 0;
-  int actual = 0;
-  if (len > 0) actual = (int)((uint32_t)sc1 << 10) / len;
-  int esub = lang1 * 4 + lscript4(T, ulscript);
-  int expected = (esub >= 0 && (uint32_t)esub < T.n_expected) ? gld(T.expected + (esub)) : 0;
-  ChunkSum cs;
-  cs.offset = (uint16_t)lo;
-  cs.chunk_start = (uint16_t)first_linear;
-  cs.lang1 = (uint16_t)lang1;
-  cs.lang2 = (uint16_t)lang2;
-  cs.score1 = (uint16_t)sc1;
-  cs.bytes = (uint16_t)len;
-  uint16_t grams = (uint16_t)t.score_count;
-  int rd = (uint8_t)reliability_delta((uint16_t)sc1, (uint16_t)sc2, grams);
-  int c1 = close_set(T, lang1);
-  if (c1 != 0 && c1 == close_set(T, lang2)) rd = 100;
-  cs.rd = (uint8_t)rd;
-  cs.rs = (uint8_t)reliability_expected(actual, expected);
-  return cs;
-}
-// SummaryBufferToDocTote :305-315, one entry
-__device__ __forceinline__ void chunk_to_doc(const ChunkSum& cs, DocTote& dt) {
-  int rel = cs.rd < cs.rs ? cs.rd : cs.rs;
-  dt.add(cs.lang1, cs.bytes, cs.score1, rel);
-}
-
-// ---------------------------------------------- chunk vector (vec mode)
+// ------------------------------------------------------- close sets
 __device__ __forceinline__ bool same_close_set(const DevTables& T, int l1, int l2) {   // :44-56
   int c1 = close_set(T, l1);
   return c1 != 0 && c1 == close_set(T, l2);
-}
-__device__ int get_lang_score(const DevTables& T, uint32_t lp, uint8_t pslang) {     // cldutil.cc:141-152
-  const uint8_t* e = T.lgprob + 8 * (lp & 0xFF);
-  int r = 0;
-  if (((lp >> 8) & 0xFF) == pslang) r += e[5];
-  if (((lp >> 16) & 0xFF) == pslang) r += e[6];
-  if (((lp >> 24) & 0xFF) == pslang) r += e[7];
-  return r;
 }
 __device__ uint8_t per_script_number(const DevTables& T, int ulscript, int lang) {  // lang_script.cc:320-326
   if (ulscript < 0 || (uint32_t)ulscript >= T.n_scripts) return 0;
@@ -1589,322 +780,11 @@ __device__ uint8_t per_script_number(const DevTables& T, int ulscript, int lang)
   return gld(T.l2p + (lang));
 }
 // BetterBoundary scoreonescriptspan.cc:671-720
-__device__ int better_boundary(const DevTables& T, const VecOut& vo, uint8_t ps0, uint8_t ps1, int lin0, int lin1,
-                               int lin2) {
-  if (lin2 - lin0 <= 8) return lin1;
-  int running = 0, diff[8];
-  for (int i = lin0; i < lin0 + 8; ++i) {
-    uint32_t lp = vo.lin_lp[i];
-    diff[i & 7] = get_lang_score(T, lp, ps0) - get_lang_score(T, lp, ps1);
-    if (i < lin0 + 4) running += diff[i & 7]; else running -= diff[i & 7];
-  }
-  int best_value = 0, best = lin1;
-  for (int i = lin0; i < lin2 - 8; ++i) {
-    if (best_value < running) {
-      bool plus = false, minus = false;
-      for (int kk = 0; kk < 8; ++kk) { plus |= diff[kk] > 0; minus |= diff[kk] < 0; }
-      if (plus && minus) { best_value = running; best = i + 4; }
-    }
-    uint32_t lp = vo.lin_lp[i + 8];
-    int nd = get_lang_score(T, lp, ps0) - get_lang_score(T, lp, ps1);
-    int md = diff[(i + 4) & 7], od = diff[i & 7];
-    diff[i & 7] = nd;
-    running += 2 * md - od - nd;
-  }
-  return best;
-}
-// SharpenBoundaries :764-829 over vo.sb[0..n] (sb[n] = the dummy off the end)
-__device__ void sharpen_boundaries(const DevTables& T, VecOut& vo, int ulscript, int n) {
-  int prior_linear = vo.sb[0].chunk_start;
-  uint16_t prior_lang = vo.sb[0].lang1;
-  for (int i = 1; i < n; ++i) {
-    ChunkSum& cs = vo.sb[i];
-    const uint16_t this_lang = cs.lang1;
-    if (this_lang == prior_lang) { prior_linear = cs.chunk_start; continue; }
-    const int this_linear = cs.chunk_start, next_linear = vo.sb[i + 1].chunk_start;
-    if (same_close_set(T, prior_lang, this_lang)) { prior_linear = this_linear; prior_lang = this_lang; continue; }
-    const uint8_t ps0 = per_script_number(T, ulscript, prior_lang), ps1 = per_script_number(T, ulscript, this_lang);
-    const int better = better_boundary(T, vo, ps0, ps1, prior_linear, this_linear, next_linear);
-    const int old_off = vo.lin_off[this_linear], new_off = vo.lin_off[better];
-    cs.chunk_start = (uint16_t)better;
-    cs.offset = (uint16_t)new_off;
-    cs.bytes = (uint16_t)(cs.bytes - (new_off - old_off));
-    vo.sb[i - 1].bytes = (uint16_t)(vo.sb[i - 1].bytes + (new_off - old_off));
-    prior_linear = better;
-    prior_lang = this_lang;
-  }
-}
-__device__ __forceinline__ int scanner_map_back(VecOut& vo, int t) {      // ScriptScanner::MapBack :1076-1078
-  return dm_map_back(vo.orig, dm_map_back(vo.low, t));
-}
-__device__ void item_to_vector(VecOut& vo, int new_lang, int mapped_offset, int mapped_len) {  // ItemToVector :322-355
-  if (vo.n > 0) {
-    cld_chunk& prior = vo.v[vo.n - 1];
-    if (new_lang == prior.lang1) { prior.bytes = (mapped_offset + mapped_len) - prior.offset; return; }
-  }
-  if (vo.n >= vo.cap) { vo.over = true; return; }
-  cld_chunk rc;
-  rc.offset = mapped_offset; rc.bytes = mapped_len; rc.lang1 = (uint16_t)new_lang; rc.pad = 0;
-  vo.v[vo.n++] = rc;
-}
-// SummaryBufferToVector :386-495
-__device__ void summary_buffer_to_vector(const DevTables& T, VecOut& vo, int n) {
-  const int unk = (int)T.unknown_lang;
-  for (int i = 0; i < n; ++i) {
-    const ChunkSum cs = vo.sb[i];
-    const int unmapped_offset = cs.offset, unmapped_len = cs.bytes;
-    int mapped_offset = scanner_map_back(vo, unmapped_offset);
-    if (mapped_offset > 0) {
-      const int prior_size = vo.n > 0 ? vo.v[vo.n - 1].bytes : 0;
-      int n_limit = prior_size - 3 < mapped_offset ? prior_size - 3 : mapped_offset;
-      if (n_limit > 12) n_limit = 12;
-      auto at = [&](int k) -> uint8_t {           // us[-k - 1] in the original document
-        const int q = mapped_offset - k - 1;
-        return (unsigned)q < (unsigned)vo.doc_len ? vo.doc[q] : 0;
-      };
-      int k = 0;
-      while (k < n_limit && at(k) >= 0x41) ++k;
-      if (k >= n_limit) k = 0;
-      if (k < n_limit) {
-        const uint8_t ch = at(k);
-        if (ch == '\'' || ch == '"' || ch == '#' || ch == '@') ++k;
-      }
-      if (k > 0) { vo.v[vo.n - 1].bytes -= k; mapped_offset -= k; }
-    }
-    const int mapped_len = scanner_map_back(vo, unmapped_offset + unmapped_len) - mapped_offset;
-    int new_lang = cs.lang1;
-    bool delta_bad = cs.rd < 75, score_bad = cs.rs < 75;       // kUnreliablePercentThreshold (:33)
-    const uint16_t prior_lang = vo.n > 0 ? vo.v[vo.n - 1].lang1 : (uint16_t)unk;
-    if (prior_lang == cs.lang1) delta_bad = false;
-    if (same_close_set(T, cs.lang1, prior_lang)) { new_lang = prior_lang; delta_bad = false; }
-    if (same_close_set(T, cs.lang1, cs.lang2) && prior_lang == cs.lang2) { new_lang = prior_lang; delta_bad = false; }
-    const uint16_t next_lang = (i + 1 >= n) ? (uint16_t)unk : vo.sb[i + 1].lang1;
-    if (delta_bad && prior_lang == cs.lang2 && next_lang == cs.lang2) { new_lang = prior_lang; delta_bad = false; }
-    if (delta_bad || score_bad) new_lang = unk;
-    item_to_vector(vo, new_lang, mapped_offset, mapped_len);
-  }
-}
-__device__ void just_one_item_to_vector(VecOut& vo, int lang1, int unmapped_offset, int unmapped_len) {  // :499-530
-  const int mapped_offset = scanner_map_back(vo, unmapped_offset);
-  const int mapped_len = scanner_map_back(vo, unmapped_offset + unmapped_len) - mapped_offset;
-  item_to_vector(vo, lang1, mapped_offset, mapped_len);
-}
-// MoveLang1ToLang2's vector half (compact_lang_det_impl.cc:1122-1147)
-__device__ void move_lang1_to_lang2_vec(const DevTables& T, VecOut& vo, int lang1, int lang2) {
-  int k = 0;
-  uint16_t prior_lang = (uint16_t)T.unknown_lang;
-  for (int i = 0; i < vo.n; ++i) {
-    cld_chunk rc = vo.v[i];
-    if (rc.lang1 == lang1) rc.lang1 = (uint16_t)lang2;
-    if (rc.lang1 == prior_lang && k > 0) {
-      vo.v[k - 1].bytes += rc.bytes;
-    } else {
-      vo.v[k] = rc;
-      ++k;
-    }
-    prior_lang = rc.lang1;
-  }
-  vo.n = k;
-}
-
-// ProcessHitBuffer (:1067-1116) for one round: LinearizeAll + ChunkAll +
-// ScoreAllHits (+ScoreOneChunk/ScoreBoosts/AddDistinctBoost2) + doc tote.
-template <class W>
-__device__ void score_round(const DevTables& T, Ctx& cx, W& w, bool cjk, int nb, int nd, int nx,
-                            int lowest, int ulscript, DocTote& dt) {
-  Linearizer<W> lin;
-  uint32_t seed = ((uint32_t)per_script_number_latin(T, default_language(T, cx.ulscript)) << 8) | 0u;
-  // MakeLangProb(lang, 1): kLgProbV2TblBackmap[1] == 0 (cldutil_shared.h:310-313)
-  lin.init(T, w, cjk, nb, nd, nx, lowest, seed);
-  const int chunksize = cjk ? kChunksizeUnis : kChunksizeQuads;
-  const int base_hit = cjk ? UNIHIT : QUADHIT;
-  const int dummy_off = w.b_off[nb];      // linear[next_linear].offset
-  Boosts& db = ((uint32_t)cx.ulscript == T.latin) ? cx.latn : cx.othr;
-  Tote& t = w.tote;
-
-  LinearEntry cur;
-  bool have = lin.next(cur);               // the seed always exists
-  int left = nb;
-  int nchunks = 0;
-  VecOut* vo = cx.vo;
-  int li = 0;                              // linear[] subscript (chunk_start values)
-  int nsb = 0;
-  // ChunkAll: with no base hits, one dummy chunk holding every entry
-  bool single = (left <= 0);
-  while (single || left > 0) {
-    int blen = chunksize;
-    if (left < chunksize + (chunksize >> 1)) blen = left;
-    else if (left < 2 * chunksize) blen = (left + 1) >> 1;
-    bool last = single || (left - blen <= 0);
-    t.reinit();
-    int lo = have ? cur.offset : dummy_off;
-    const int first_li = li;
-    int cnt = 0;
-    while (have && (last || cnt < blen)) {
-      if (vo) { vo->lin_lp[li] = cur.langprob; vo->lin_off[li] = (uint16_t)cur.offset; }
-      ++li;
-      add_lang_prob(T, cur.langprob, t);
-      if (cur.type <= QUADHIT) t.score_count++;
-      if (cur.type == DISTINCTHIT) { db.lp[db.n] = cur.langprob; db.n = (db.n + 1) & (kMaxBoosts - 1); }
-      if (cur.type == base_hit) ++cnt;
-      have = lin.next(cur);
-    }
-    // ScoreBoosts (scoreonescriptspan.cc:125-152): prior boosts, distinct
-    // boosts, then the prior whacks zero their languages (ZeroPSLang :39-42)
-    const int so = ((uint32_t)cx.ulscript == T.latin) ? 0 : 4;
-    if (cx.priors)
-      for (int k = 0; k < kMaxBoosts; ++k) if (cx.priors[so + k] > 0) add_lang_prob(T, cx.priors[so + k], t);
-    for (int k = 0; k < kMaxBoosts; ++k) if (db.lp[k] > 0) add_lang_prob(T, db.lp[k], t);
-    if (cx.priors)
-      for (int k = 0; k < kMaxBoosts; ++k)
-        if (cx.priors[8 + so + k] > 0) t.score[(cx.priors[8 + so + k] >> 8) & 0xFF] = 0;
-    int hi = have ? cur.offset : dummy_off;
-    if (nchunks < kMaxSummaries) {
-      const ChunkSum cs = chunk_summary(T, ulscript, lo, hi, first_li, t);
-      if (vo) vo->sb[nsb++] = cs;
-      else chunk_to_doc(cs, dt);
-    }
-    ++nchunks;
-    if (single) break;
-    left -= blen;
-  }
-  if (vo) {
-    // ProcessHitBuffer with a vector (:1097-1115): dummy entry off the end
-    // (ScoreAllHits :289-297), SharpenBoundaries, then the doc tote and the vector
-    ChunkSum& dm = vo->sb[nsb];
-    dm = ChunkSum{};
-    dm.offset = (uint16_t)dummy_off;
-    dm.chunk_start = (uint16_t)li;
-    vo->lin_off[li] = (uint16_t)dummy_off;
-    sharpen_boundaries(T, *vo, cx.ulscript, nsb);
-    for (int i = 0; i < nsb; ++i) chunk_to_doc(vo->sb[i], dt);
-    summary_buffer_to_vector(T, *vo, nsb);
-  }
-}
-
-// ScoreOneScriptSpan :1302-1333 with ScoreEntireScriptSpan :1132-1160,
-// ScoreCJKScriptSpan :1163-1214, ScoreQuadScriptSpan :1231-1277
-template <class W>
-__device__ void score_one_script_span(const DevTables& T, Ctx& cx, W& w, const Span& span, DocTote& dt, Status& st) {
-  int rt = rtype_of(T, span.ulscript);
-  if ((cx.flags & kCLDFlagScoreAsQuads) && rt != RTypeCJK) rt = RTypeMany;   // :1318-1320
-  if (rt == RTypeNone || rt == RTypeOne) {
-    int bytes = span.text_bytes;
-    dt.add((uint16_t)default_language(T, span.ulscript), bytes, bytes, 100);
-    if (cx.vo) just_one_item_to_vector(*cx.vo, default_language(T, span.ulscript), 1, bytes - 1);
-    return;
-  }
-  const bool cjk = (rt == RTypeCJK);
-  int off = 1;
-  int lowest = off;
-  const int limit = span.text_bytes;
-  while (off < limit) {
-    int nb = 0, nd = 0, nx = 0, next;
-    if (cjk) {
-      next = get_uni_hits(T, span.text, off, limit, w, nb, st);
-      if (st.requeue) return;
-      get_bi_hits(T, span.text, off, next, w, nd, nx, st);
-    } else {
-      next = get_quad_hits(T, span.text, off, limit, w, nb, st);
-      if (st.requeue) return;
-      get_octa_hits(T, span.text, off, next, w, nd, nx, st);
-    }
-    if (st.requeue) return;
-    score_round(T, cx, w, cjk, nb, nd, nx, lowest, span.ulscript, dt);
-    lowest = next;        // SpliceHitBuffer :1118-1127
-    off = next;
-  }
-}
-
 // ------------------------------------------------------ document level
 // RefineScoredClosePairs + MoveLang1ToLang2 compact_lang_det_impl.cc:1105-1203
-__device__ __forceinline__ void refine_scored_close_pairs(const DevTables& T, DocTote& d, VecOut* vo = nullptr) {
-  for (int s = 0; s < 24; ++s) {
-    int cs = close_set(T, d.key[s]);
-    if (cs == 0) continue;
-    for (int s2 = s + 1; s2 < 24; ++s2) {
-      if (close_set(T, d.key[s2]) == cs) {
-        int from, to;
-        if (d.value[s] < d.value[s2]) { from = s; to = s2; } else { from = s2; to = s; }
-        const int from_lang = d.key[from], to_lang = d.key[to];
-        d.value[to] += d.value[from]; d.score[to] += d.score[from]; d.rel[to] += d.rel[from];
-        d.key[from] = kUnusedKey; d.score[from] = 0; d.rel[from] = 0;
-        if (vo) move_lang1_to_lang2_vec(T, *vo, from_lang, to_lang);
-        break;
-      }
-    }
-  }
-}
-// RemoveUnreliableLanguages :997-1101 (score field receives newbytes, as there)
-__device__ __forceinline__ void remove_unreliable_languages(const DevTables& T, DocTote& d) {
-  for (int s = 0; s < 24; ++s) {
-    int lang = d.key[s];
-    if (lang == kUnusedKey) continue;
-    int bytes = d.value[s], reli = d.rel[s];
-    if (bytes == 0) continue;
-    int rp = reli / bytes;
-    if (rp >= 41) continue;
-    int alt = (int)T.unknown_lang;
-    if ((uint32_t)lang <= T.hawaiian && (uint32_t)lang < T.n_closest) alt = gld(T.closest + (lang));
-    if (alt == (int)T.unknown_lang) continue;
-    int as = d.find((uint16_t)alt);
-    if (as < 0) continue;
-    int bytes2 = d.value[as], reli2 = d.rel[as];
-    if (bytes2 == 0) continue;
-    int rp2 = reli2 / bytes2;
-    int to = as, from = s;
-    if (rp2 < rp || (rp2 == rp && lang < alt)) { to = s; from = as; }
-    int np = rp > rp2 ? rp : rp2;
-    if (np < 41) np = 41;
-    int nbytes = bytes + bytes2;
-    d.key[from] = kUnusedKey; d.score[from] = 0; d.rel[from] = 0;
-    d.score[to] = nbytes; d.rel[to] = np * nbytes;
-  }
-  for (int s = 0; s < 24; ++s) {
-    if (d.key[s] == kUnusedKey) continue;
-    int bytes = d.value[s], reli = d.rel[s];
-    if (bytes == 0) continue;
-    if (reli / bytes >= 41) continue;
-    d.key[s] = kUnusedKey; d.score[s] = 0; d.rel[s] = 0;
-  }
-}
-
 struct Extract { int lang3[3], pct3[3], rp3[3], text_bytes; bool reliable; double ns3[3]; };
 
 // ExtractLangEtc :1276-1384 with GetNormalizedScore :1269-1273
-__device__ __forceinline__ void extract_lang_etc(const DevTables& T, const DocTote& d, int total, Extract& x) {
-  const int unk = (int)T.unknown_lang;
-  int bc[3] = {0, 0, 0};
-  for (int i = 0; i < 3; ++i) { x.rp3[i] = 0; x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; }
-  x.reliable = false;
-  for (int i = 0; i < 3; ++i) {
-    int k = d.key[i];
-    if (k != kUnusedKey && k != unk) {
-      x.lang3[i] = k;
-      bc[i] = d.value[i];
-      x.rp3[i] = d.rel[i] / (bc[i] ? bc[i] : 1);
-      x.ns3[i] = bc[i] <= 0 ? 0.0 : (double)((int32_t)((uint32_t)d.score[i] << 10) / bc[i]);
-    }
-  }
-  int t12 = bc[0] + bc[1], t123 = t12 + bc[2];
-  if (total < t123) total = t123;
-  int div = total > 1 ? total : 1;
-  x.pct3[0] = (bc[0] * 100) / div;
-  x.pct3[1] = (t12 * 100) / div;
-  x.pct3[2] = (t123 * 100) / div;
-  x.pct3[2] -= x.pct3[1];
-  x.pct3[1] -= x.pct3[0];
-  if (x.pct3[1] < x.pct3[2]) { ++x.pct3[1]; --x.pct3[2]; }
-  if (x.pct3[0] < x.pct3[1]) { ++x.pct3[0]; --x.pct3[1]; }
-  x.text_bytes = total;
-  int k0 = d.key[0];
-  if (k0 != kUnusedKey && k0 != unk) {
-    int b0 = d.value[0];
-    x.reliable = (d.rel[0] / (b0 ? b0 : 1)) >= 41;
-  }
-  if (100 - (x.pct3[0] + x.pct3[1] + x.pct3[2]) > 20) x.reliable = false;
-}
-
 __device__ __forceinline__ bool is_figs(const DevTables& T, int l) {
   return l == (int)T.french || l == (int)T.italian || l == (int)T.german || l == (int)T.spanish;
 }
@@ -1980,100 +860,6 @@ __device__ void mark_failed(const DevTables& T, cld_result* r) {
   r->summary_lang = (uint16_t)CLD_LANG_FAILED;
   r->is_reliable = 0;
   r->text_bytes = 0;
-}
-
-// DetectLanguageSummaryV2 compact_lang_det_impl.cc:1707-2106 (HTML mode when
-// !plain, the ApplyHints priors when given, a ResultChunkVector when vo;
-// cflags: the caller's public flags, kCLDFlagScoreAsQuads / kCLDFlagBestEffort);
-// recursion unrolled into passes.  Returns the number of passes, or 0 with
-// st.requeue set.
-template <class W>
-__device__ int detect_doc(const DevTables& T, const DocView& d, W& w, cld_result* out, Status& st,
-                          bool plain = true, const uint32_t* priors = nullptr, VecOut* vo = nullptr,
-                          uint32_t cflags = 0) {
-  const int unk = (int)T.unknown_lang;
-  int flags = (int)(cflags & (kCLDFlagScoreAsQuads | kCLDFlagBestEffort));
-  int passes = 0;
-  Extract x;
-  if (vo) vo->n = 0;
-  if (d.len == 0) {
-    for (int i = 0; i < 3; ++i) { x.lang3[i] = unk; x.pct3[i] = 0; x.ns3[i] = 0.0; x.rp3[i] = 0; }
-    x.text_bytes = 0;
-    write_result(out, x, unk, false);
-    return 1;
-  }
-  for (;;) {
-    ++passes;
-    DocTote dt;
-    dt.init();
-    Ctx cx;
-    cx.ulscript = 0;
-    cx.latn.n = 0; cx.othr.n = 0;
-    cx.priors = priors;
-    cx.vo = vo;
-    cx.flags = flags;
-    if (vo) vo->n = 0;                       // resultchunkvector->clear() (:1730-1732)
-    for (int k = 0; k < kMaxBoosts; ++k) { cx.latn.lp[k] = 0; cx.othr.lp[k] = 0; }
-    int next = 0, remaining = d.len;
-    int hash = 0;
-    if constexpr (W::MULTIPASS) {
-      if (flags & kCLDFlagRepeats) for (int i = 0; i < kPredictionTableSize; ++i) w.predict[i] = 0;
-    }
-    int total = 0;
-    bool restart = false;
-    Span span;
-    while (get_one_script_span(T, d, next, remaining, w, span, st, plain, vo ? &vo->orig : nullptr)) {
-      lower_script_span(T, w, span, st, plain, vo ? &vo->low : nullptr);
-      if (st.requeue) return 0;
-      if (flags & kCLDFlagSqueeze) {
-        if constexpr (W::MULTIPASS)
-          span.text_bytes = vo ? cheap_squeeze_inplace_overwrite(span.text, span.text_bytes, w.sqz)
-                               : cheap_squeeze_inplace(span.text, span.text_bytes, w.sqz);
-      } else if (2048 < span.text_bytes && !(flags & kCLDFlagFinish)) {
-        if constexpr (W::MULTIPASS) {
-          if (cheap_squeeze_trigger_test(span.text, span.text_bytes, w.sqz)) {
-            flags |= kCLDFlagSqueeze; restart = true; break;
-          }
-        } else {
-          st.requeue = true; return 0;
-        }
-      }
-      if (flags & kCLDFlagRepeats) {
-        if constexpr (W::MULTIPASS)
-          span.text_bytes = vo ? cheap_rep_words_inplace_overwrite(span.text, span.text_bytes, &hash, w.predict)
-                               : cheap_rep_words_inplace(span.text, span.text_bytes, &hash, w.predict);
-      }
-      cx.ulscript = span.ulscript;
-      score_one_script_span(T, cx, w, span, dt, st);
-      if (st.requeue) return 0;
-      total += span.text_bytes;
-    }
-    if (st.requeue) return 0;
-    if (restart) continue;
-    refine_scored_close_pairs(T, dt, vo);
-    dt.sort3();
-    extract_lang_etc(T, dt, total, x);
-    bool good = (flags & kCLDFlagFinish) || total <= 256 ||
-                (x.reliable && x.pct3[0] >= 70) || (x.reliable && x.pct3[0] + x.pct3[1] >= 93);
-    if (good) {
-      if (!(flags & kCLDFlagBestEffort)) remove_unreliable_languages(T, dt);   // :1998-2000
-      dt.sort3();
-      extract_lang_etc(T, dt, total, x);
-      bool rel;
-      int summary = calc_summary_lang(T, total, x, rel, (flags & kCLDFlagBestEffort) != 0);
-      write_result(out, x, summary, rel);
-      if (vo && vo->n > 0) {                 // FinishResultVector(0, buffer_length) (:1688-1702)
-        cld_chunk& a = vo->v[0];
-        if (a.offset > 0) { a.bytes += a.offset; a.offset = 0; }
-        cld_chunk& z = vo->v[vo->n - 1];
-        if (z.offset + z.bytes < d.len) z.bytes += d.len - (z.offset + z.bytes);
-      }
-      return passes;
-    }
-    if constexpr (!W::MULTIPASS) { st.requeue = true; return 0; }
-    flags |= kCLDFlagTop40 | kCLDFlagRepeats | kCLDFlagFinish;
-    if (total < 256) flags |= kCLDFlagShort | kCLDFlagUseWords;
-  }
 }
 
 }  // namespace cld

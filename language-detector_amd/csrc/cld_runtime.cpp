@@ -616,26 +616,20 @@ int init_device(Device* d) {
   if (const char* e = getenv("CLD_LONG_ORDER")) d->long_order = atoi(e) != 0;
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, d->id));
-  d->stride = (cld_general_work_bytes() + 255) & ~(uint64_t)255;
-  int lanes = prop.multiProcessorCount * 32;     // k_general documents in flight (one per wavefront)
-  if (const char* e = getenv("CLD_GENERAL_LANES")) lanes = atoi(e);
-  lanes = std::max(64, (lanes / 64) * 64);
-  while ((uint64_t)lanes * d->stride > (8ull << 30) && lanes > 64) lanes -= 64;
-  d->lanes = lanes;
   if (const char* e = getenv("CLD_PROFILE_STAGES")) {
     if (atoi(e) > 0) {
       HIP_OK(hipMalloc(&d->d_prof, 16 * sizeof(unsigned long long)));
       HIP_OK(hipMemset(d->d_prof, 0, 16 * sizeof(unsigned long long)));
     }
   }
-  HIP_OK(hipMalloc(&d->d_arena, (uint64_t)lanes * d->stride));
-  // k_long: one slot per resident wavefront of its persistent grid
+  // k_long: one slot per resident wavefront of its persistent grid; every
+  // document longer than k_wave takes, or that k_wave hands on, runs there
   int waves = 4 * cld_long_waves_per_simd();   // fill every SIMD at the kernel's occupancy
-  if (const char* e = getenv("CLD_LONG_WAVES")) waves = atoi(e);
-  if (const char* e = getenv("CLD_LONG")) if (atoi(e) == 0) waves = 0;
+  if (const char* e = getenv("CLD_LONG_WAVES")) waves = std::max(1, atoi(e));
   int n_slots = (prop.multiProcessorCount * waves / kLongWPB) * kLongWPB;
   const uint64_t slot = cld_long_slot_bytes();
-  while (n_slots > 0 && (uint64_t)n_slots * slot > (8ull << 30)) n_slots -= kLongWPB;
+  while (n_slots > kLongWPB && (uint64_t)n_slots * slot > (8ull << 30)) n_slots -= kLongWPB;
+  if (n_slots < kLongWPB) return CLD_ENOMEM;
   int alloc_slots = n_slots;
   if (n_slots > 0 && !(getenv("CLD_LONG_STAGED") && atoi(getenv("CLD_LONG_STAGED")) == 0)) {
     const int st = prop.multiProcessorCount * 4 * cld_staged_waves_per_simd();
@@ -774,14 +768,12 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     HIP_OK(cld_launch_html_rewrite(d->d_T, buf, offs, (int)n, const_cast<uint8_t*>(special), const_cast<uint8_t*>(hbuf),
                                    const_cast<uint8_t*>(hflag), hpos, hgap, kHtmlSoftMin,
                                    d->d_prof ? d->d_prof + 7 : nullptr, s));
-  // special documents join k_general's list: d_requeue2 behind k_long, else d_requeue
-  uint32_t* sp_list = d->n_slots > 0 ? d->d_requeue2 : d->d_requeue;
-  const int sp_ctr = d->n_slots > 0 ? kCtrRequeue2 : kCtrRequeue;
-  HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, ctr, d->d_prof, special, sp_list,
-                         sp_ctr, cflags, priors, hbuf, hflag,
-                         (d->n_slots > 0 && d->long_order) ? d->d_lhist : nullptr, s));
+  // HTML pages the rewrite did not take join k_long's list (its sequential
+  // span source scans them in HTML mode, cld_seq.hip)
+  HIP_OK(cld_launch_wave(&d->T, buf, offs, (int)n, out, d->d_requeue, ctr, d->d_prof, special, d->d_requeue,
+                         kCtrRequeue, cflags, priors, hbuf, hflag, d->long_order ? d->d_lhist : nullptr, s));
   HIP_OK(hipEventRecord(ev[1], s));
-  if (d->n_slots > 0) {
+  {
     const uint32_t* list = d->d_requeue;
     if (d->long_order) {
       HIP_OK(cld_launch_order_long(offs, d->d_requeue, ctr, d->d_lkey, d->d_lhist, d->d_lsorted, n > 0, s));
@@ -809,25 +801,18 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       // a list of at most small_long_list() documents (64) goes whole to the
       // fused kernel: small batches keep its two-wave speculation (section 6)
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
-                               d->d_meta, d->d_stlists, d->d_stlists + c, fall, d->d_requeue2, ctr, cflags, special,
+                               d->d_meta, d->d_stlists, d->d_stlists + c, fall, ctr, cflags, special,
                                priors, hbuf, hflag, hpos, hgap, d->fault_doc, small_long_list(d),
                                d->long_order ? d->d_lhist : nullptr, heavy_kb(), d->d_parlists, np, gcap, s));
       list = fall;
       ctr_total = kCtrStFall;
       ctr_deq = kCtrStDqFall;
     }
-    HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2,
-                           ctr, d->h_trace, d->d_dbg, d->dbg_doc,
+    HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2, ctr, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, hpos, hgap,
                            d->fault_doc,
                            d->d_spec_out, d->d_spec_take, ctr_total, ctr_deq, s));
     HIP_OK(hipEventRecord(ev[2], s));
-    HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue2, out, d->d_arena, d->stride, d->lanes,
-                              ctr, kCtrRequeue2, kCtrDequeue2, special, priors, cflags, d->fault_doc, s));
-  } else {
-    HIP_OK(hipEventRecord(ev[2], s));
-    HIP_OK(cld_launch_general(d->d_T, buf, offs, d->d_requeue, out, d->d_arena, d->stride, d->lanes,
-                              ctr, kCtrRequeue, kCtrDequeue, special, priors, cflags, d->fault_doc, s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -838,15 +823,15 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
 }
 
 // Adds one batch's device counters to st (docs = documents of that batch).
+// short_docs: finished by k_wave; long_docs: by k_long (or the staged path)
+// on the parallel span builder; general_docs: by k_long on the sequential
+// span source (cld_seq.hip).
 void add_counters(Device* d, const uint32_t* c, uint64_t docs, cld_batch_stats* st) {
-  const uint32_t to_general = d->n_slots > 0 ? c[kCtrRequeue2] : c[kCtrRequeue];
-  // special (HTML / hinted) documents sit in the k_general list directly: in
-  // d_requeue2 with k_long, in d_requeue without it
-  const uint32_t sp2 = d->n_slots > 0 ? c[kCtrSpecial] : 0;
-  const uint64_t shorts = docs - c[kCtrRequeue] - sp2;
+  (void)d;
+  const uint64_t shorts = docs - c[kCtrRequeue];
   st->docs += docs;
-  st->general_docs += to_general;
-  st->long_docs += c[kCtrRequeue] - (to_general - sp2);
+  st->general_docs += c[kCtrSeq];
+  st->long_docs += c[kCtrRequeue] - c[kCtrSeq];
   st->short_docs += shorts;
   st->passes[0] += shorts + c[kCtrPass1];
   st->passes[1] += c[kCtrPass2];
@@ -1434,25 +1419,13 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_OK(hipSetDevice(d->id));
   Device::Vec& V = d->vec;
-  if (!V.arena) {
-    hipDeviceProp_t prop;
-    HIP_OK(hipGetDeviceProperties(&prop, d->id));
-    V.stride = (cld_vec_work_bytes() + 255) & ~(uint64_t)255;
-    int lanes = prop.multiProcessorCount * 32;
-    if (const char* e = getenv("CLD_VEC_LANES")) lanes = atoi(e);
-    lanes = std::max(64, (lanes / 64) * 64);
-    while ((uint64_t)lanes * V.stride > (8ull << 30) && lanes > 64) lanes -= 64;
-    if (hipMalloc(&V.arena, (uint64_t)lanes * V.stride) != hipSuccess) { V.arena = nullptr; return CLD_ENOMEM; }
-    V.lanes = lanes;
+  // k_long<VEC> builds every vector (the parallel span builder, or for the
+  // documents it cannot formulate the sequential span source), one VecSlot per
+  // resident wave, allocated on the first vector call
+  if (!V.vslots && hipMalloc(&V.vslots, (uint64_t)d->n_slots * cld_vec_slot_bytes()) != hipSuccess) {
+    V.vslots = nullptr;
+    return CLD_ENOMEM;
   }
-  // The parallel kernels build the vectors (k_long<VEC>); documents they
-  // cannot reproduce, and HTML pages, run the sequential kernel.
-  // CLD_VEC_PARALLEL=0: the sequential kernel for every document (A/B).
-  static const bool parallel_env = !(getenv("CLD_VEC_PARALLEL") && atoi(getenv("CLD_VEC_PARALLEL")) == 0);
-  if (parallel_env && d->n_slots > 0 && !V.vslots) {
-    if (hipMalloc(&V.vslots, (uint64_t)d->n_slots * cld_vec_slot_bytes()) != hipSuccess) V.vslots = nullptr;
-  }
-  const bool parallel = parallel_env && V.vslots != nullptr;
   // Sub-batches as large as memory allows: a launch lasts at least as long as
   // its longest document (one wave runs it start to end), so every sub-batch
   // pays that tail once -- 32 MB sub-batches held C5 to 76K docs/s, one launch
@@ -1468,9 +1441,7 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
   // + 256); results to res, vector sizes to nch (-1: the document overflowed
   // its pool region or an offset map), the vectors to ch in document order.
   std::vector<uint64_t> pool_off, pos;
-  std::vector<uint32_t> order, bstart;
   cld_batch_stats vst{};
-  static const bool no_order = getenv("CLD_VEC_ORDER") && atoi(getenv("CLD_VEC_ORDER")) == 0;   // (A/B only)
   auto sub = [&](const uint8_t* b, const uint64_t* o, size_t m, cld_result* res, const uint8_t* sp,
                  const uint32_t* pr, bool big, std::vector<int32_t>& nch, std::vector<cld_chunk>& ch) -> int {
     const uint64_t base = o[0], bytes = o[m] - base;
@@ -1485,19 +1456,6 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
       return CLD_ENOMEM;
     if (sp && grow(&V.sp, &V.sp_cap, m)) return CLD_ENOMEM;
     if (pr && grow(&V.pri, &V.pri_cap, 16 * m)) return CLD_ENOMEM;
-    // Longest documents first: a wave runs one document start to end, so with
-    // more documents than waves a long one dequeued late sets the batch's end.
-    // A counting sort by bit length of the size (descending).
-    const bool ordered = !parallel && !no_order && m > (size_t)V.lanes;
-    if (ordered) {
-      if (grow(&V.order, &V.order_cap, m)) return CLD_ENOMEM;
-      bstart.assign(66, 0);
-      auto bucket = [&](size_t i) { return 64 - __builtin_clzll((o[i + 1] - o[i]) | 1); };   // 1..64
-      for (size_t i = 0; i < m; ++i) ++bstart[65 - bucket(i)];
-      for (int k = 1; k < 66; ++k) bstart[k] += bstart[k - 1];
-      order.resize(m);
-      for (size_t i = 0; i < m; ++i) order[bstart[64 - bucket(i)]++] = (uint32_t)i;
-    }
     hipStream_t s = d->stream;
     HIP_OK(hipStreamWaitEvent(s, d->done, 0));
     if (bytes) HIP_OK(hipMemcpyAsync(V.in, b + base, bytes, hipMemcpyHostToDevice, s));
@@ -1505,9 +1463,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     HIP_OK(hipMemcpyAsync(V.pool_off, pool_off.data(), (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     if (sp) HIP_OK(hipMemcpyAsync(V.sp, sp, m, hipMemcpyHostToDevice, s));
     if (pr) HIP_OK(hipMemcpyAsync(V.pri, pr, 16 * m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    if (ordered) HIP_OK(hipMemcpyAsync(V.order, order.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_OK(hipMemsetAsync(d->d_counters, 0, kCtrSlots * sizeof(uint32_t), s));
-    if (parallel) {
+    {
       if (grow(&d->d_requeue, &d->requeue_cap, m) || grow(&d->d_requeue2, &d->requeue2_cap, m) ||
           grow(&d->d_lsorted, &d->lsorted_cap, m) || grow(&d->d_lkey, &d->lkey_cap, m))
         return CLD_ENOMEM;
@@ -1530,18 +1487,11 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
                                        const_cast<uint8_t*>(hf), const_cast<uint32_t*>(hpz),
                                        const_cast<uint32_t*>(hgz), 0, nullptr, s));
       }
-      HIP_OK(cld_launch_route_vec((int)m, sp ? V.sp : nullptr, d->d_counters, d->d_requeue, d->d_requeue2, s));
+      HIP_OK(cld_launch_route_vec((int)m, d->d_counters, d->d_requeue, s));
       HIP_OK(cld_launch_order_long(V.offs, d->d_requeue, d->d_counters, d->d_lkey, d->d_lhist, d->d_lsorted, false, s));
       HIP_OK(cld_launch_long_vec(d->d_T, V.in - base, V.offs, d->d_lsorted, V.out, d->d_slots, V.vslots, d->n_slots,
-                                 d->d_requeue2, d->d_counters, cflags & kCldFlags, sp ? V.sp : nullptr,
-                                 pr ? V.pri : nullptr, hb, hf, hpz, hgz, V.pool, V.pool_off, V.nch, s));
-      HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes,
-                                    d->d_counters, sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off,
-                                    V.nch, d->d_requeue2, cflags & kCldFlags, d->d_counters + kCtrRequeue2, s));
-    } else {
-      HIP_OK(cld_launch_general_vec(d->d_T, V.in - base, V.offs, (int)m, V.out, V.arena, V.stride, V.lanes,
-                                    d->d_counters, sp ? V.sp : nullptr, pr ? V.pri : nullptr, V.pool, V.pool_off,
-                                    V.nch, ordered ? V.order : nullptr, cflags & kCldFlags, nullptr, s));
+                                 d->d_requeue2, d->d_counters, cflags & kCldFlags, sp ? V.sp : nullptr, pr ? V.pri : nullptr, hb, hf,
+                                 hpz, hgz, V.pool, V.pool_off, V.nch, s));
     }
     nch.resize(m);
     uint32_t ctr[kCtrSlots];
@@ -1552,8 +1502,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     // statistics (cld_last_batch_stats): documents the parallel kernel finished
     // (long_docs) and those the sequential kernel took (general_docs)
     vst.docs += m;
-    vst.general_docs += parallel ? ctr[kCtrRequeue2] : m;
-    vst.long_docs += parallel ? m - ctr[kCtrRequeue2] : 0;
+    vst.general_docs += ctr[kCtrSeq];
+    vst.long_docs += m - ctr[kCtrSeq];
     for (int k = 0; k < 3; ++k) vst.passes[k] += ctr[kCtrPass1 + k];
     vst.passes[3] += ctr[kCtrError];
     pos.assign(m, 0);

@@ -4,7 +4,7 @@ mode (oracle/_ref/librefcld2.so, ExtDetectLanguageSummary with a
 ResultChunkVector) on 16 host threads timed beside it and compared result for
 result, chunk for chunk.  Plain documents run the parallel kernels
 (k_long<VEC>); HTML pages and hand-ons the sequential kernel (k_general_vec).
-One JSON line per workload.  CLD_VEC_PARALLEL=0 forces the sequential kernel."""
+One JSON line per workload."""
 import json
 import os
 import sys
