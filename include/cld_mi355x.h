@@ -128,13 +128,14 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
 
 /* Sum of kernel durations (HIP events on the stream the kernels ran on) of
  * every batch enqueued on context `ctx` since the previous call; resets.
- * short_ms = wavefront kernel; general_ms = long-document + sequential kernels. */
+ * short_ms = wavefront kernel; general_ms = the long-document kernels (k_long, both instantiations). */
 int cld_kernel_time(int ctx, double* short_ms, double* general_ms, int* launches);
 
 /* Same accounting split per kernel stage: ms[0] the wavefront kernel (k_wave),
  * (with HTML pages: the GPU rewrite of the pages into plain text, k_html_rewrite,
- * is counted in ms[0]), ms[1] the long-document stage (length ordering + k_long), ms[2] the
- * sequential kernel (k_general).  Sums since the previous call of either
+ * is counted in ms[0]), ms[1] the long-document stage (length ordering + k_long on the
+ * parallel span builder), ms[2] k_long's documents on the sequential span source (its SEQ
+ * instantiation, cld_seq.hip).  Sums since the previous call of either
  * function; resets. */
 int cld_kernel_times(int ctx, double* ms3, int* launches);
 

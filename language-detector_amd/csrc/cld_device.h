@@ -59,7 +59,7 @@ extern "C" {
 // Per-document status written next to the result
 enum {
   CLD_ST_DONE = 0,
-  CLD_ST_REQUEUE = 1,     // short kernel could not finish: general kernel redoes it
+  CLD_ST_REQUEUE = 1,     // short kernel could not finish: k_long redoes it
   CLD_ST_ERROR = 2
 };
 

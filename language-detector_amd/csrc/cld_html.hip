@@ -23,14 +23,14 @@
 //     lowering differs (kCptHtmlLower; for 4-byte characters one flag for the
 //     whole range, k_build_cpt4 -- the reference's tables set neither), a
 //     malformed character, or more than kHtmlRewriteMax bytes is not
-//     rewritten and stays on k_general;
+//     rewritten and is scanned by k_long's sequential span source (cld_seq.hip);
 //   * the span soft limit reads the raw bytes left (:814-819); it splits
 //     nothing below kMaxScriptBytes (40,928), and for longer pages the rewrite
 //     also records each output byte's page offset (hpos, with hgap after
 //     dropped '&'s), from which the span builders read it (cld_long.hip
 //     next_span).
-// A rewritten page that k_wave / k_long re-queue goes to k_general, which
-// scores the original page in HTML mode.
+// A rewritten page that k_long hands on goes to its SEQ instantiation, which
+// scans the original page in HTML mode.
 //
 // One wavefront per page, in three steps (the reference's own pass is
 // sequential, but only its '<' / '&' stops carry state):
@@ -59,7 +59,7 @@ using wave::wshr1;
 using wave::wsum;
 using wave::wsync;
 
-constexpr int kHtmlRewriteMax = 64 << 20;  // (lng::kStBigMax) larger pages stay on k_general
+constexpr int kHtmlRewriteMax = 64 << 20;  // (lng::kStBigMax) larger pages stay HTML (cld_seq.hip)
 // LDS per wave (the page stage + the candidate lists) sets the resident waves
 // of this latency-bound kernel: an 8 KB stage and 1,024 candidates per
 // segment left 1.5 waves/SIMD; 2 KB and 256 (5.4 KB per wave) give 8, and
@@ -277,7 +277,7 @@ __device__ __forceinline__ void rewrite_page(const DevTables& T, const TagTables
       // byte start + k (Copy(plen), then Delete(tlen - plen)).  An entity whose
       // Delete is a single byte, or that grows (Insert), could merge with the
       // run's closing Insert(1) into a Copy (offsetmap.cc:122-156): such pages
-      // keep the sequential kernel in vec mode (kSpecialNoVec).
+      // keep the sequential span source in vec mode (kSpecialNoVec).
       // the first byte after dropped '&'s also records where they began (hpos
       // second half, read where hflag bit 1 is set): a run ending there has its
       // gap start at the first of them (they merge into the gap's Delete)
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * kHtmlWPB) void k_html_rewrite(const DevTables*
     if (!(sp & kSpecialHtml)) continue;
     const uint64_t a = offs[i];
     const int64_t len64 = (int64_t)(offs[i + 1] - a);
-    if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: k_general
+    if (len64 > kHtmlRewriteMax) continue;                       // stays HTML: cld_seq.hip
     const int L = (int)len64;
     if (L > kHtmlStage) {
       rewrite_page<false>(T, tt, S, buf + a, L, a, i, sp, special, hbuf, hflag, hpos, hgap, hpos_min, prof, am0, am1,

@@ -129,7 +129,7 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
                            const uint32_t* hgap, uint32_t fault_doc, cld_result* spec_out, uint32_t* spec_take,
-                           int ctr_total, int ctr_deq, hipStream_t s);
+                           int ctr_total, int ctr_deq, hipEvent_t mid, hipStream_t s);
 // spec_out / spec_take (nullable: no speculation): cld_long_spec_docs(n_slots)
 // results and u32 entries, k_long's speculative pass-2 results for the
 // longest documents of a small batch.

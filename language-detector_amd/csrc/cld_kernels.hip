@@ -795,18 +795,19 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                            unsigned long long* prof, uint32_t cflags, const uint8_t* special,
                            const uint32_t* priors, const uint8_t* hbuf, const uint8_t* hflag, const uint32_t* hpos,
                            const uint32_t* hgap, uint32_t fault_doc, cld_result* spec_out, uint32_t* spec_take,
-                           int ctr_total, int ctr_deq, hipStream_t s) {
+                           int ctr_total, int ctr_deq, hipEvent_t mid, hipStream_t s) {
   if (n_slots < kLongWPB) return hipErrorInvalidValue;
   dim3 grid(n_slots / kLongWPB), block(64 * kLongWPB);
   // diagnostics (trace / debug dump / stage cycles) live in their own instantiation:
   // they cost the production kernel registers even when switched off.  Then
   // the documents it handed on (seq_list, counters[kCtrRequeue2]), on the
-  // sequential span source.
+  // sequential span source; `mid` (nullable) is recorded between the two.
   if (trace || dbg || prof) {
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false>), grid, block, 0, s, d_T, buf, offs, list, out, slots,
                        seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((cld::k_long<kLongWPB, true, false, true>), grid, block, 0, s, d_T, buf, offs, seq_list, out,
                        slots, seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, nullptr, nullptr, kCtrRequeue2,
@@ -816,6 +817,7 @@ hipError_t cld_launch_long(const DevTables* d_T, const uint8_t* buf, const uint6
                        seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, spec_out, spec_take, ctr_total,
                        ctr_deq);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((cld::k_long<kLongWPB, false, false, true>), grid, block, 0, s, d_T, buf, offs, seq_list, out,
                        slots, seq_list, counters, trace, dbg, dbg_doc, prof, cflags, special, priors, hbuf, hflag,
                        fault_doc, nullptr, nullptr, nullptr, nullptr, hpos, hgap, nullptr, nullptr, kCtrRequeue2,

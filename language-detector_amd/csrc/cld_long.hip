@@ -34,8 +34,9 @@
 //
 // Anything this formulation cannot reproduce exactly (a document longer than
 // kDocCap, a non-local scanner/lowercaser state, the Squeeze restart, a
-// capacity overflow) is appended to the next re-queue list and redone by
-// k_general from scratch.
+// capacity overflow) is appended to seq_list and redone from scratch by
+// k_long's SEQ instantiation, whose spans come from the sequential span
+// source (cld_seq.hip).
 
 namespace cld {
 namespace lng {
@@ -193,9 +194,9 @@ static_assert(sizeof(Smem) <= 10240, "k_long LDS per wave: 4 blocks of 4 waves p
 //     Copy for letters, Delete + Insert(1) for a gap turned into one space
 //     (Copy(1) when the gap is one byte), Insert(4) for the pads; map2uplow_ is
 //     the identity because vec mode keeps documents whose lowering changes a
-//     character's length on the sequential kernel;
+//     character's length on the sequential span source;
 //   * Repeats overwrite instead of cutting (CheapRepWordsInplaceOverwrite), so
-//     those offsets stay valid; Squeeze documents go to the sequential kernel;
+//     those offsets stay valid; Squeeze documents go to the sequential span source;
 //   * per round, linear[] is materialised from the emission streams (rank =
 //     merge position, LinearizeAll's tie order) for SharpenBoundaries, whose
 //     BetterBoundary window scan runs across lanes; the sharpened chunk bytes
@@ -315,7 +316,15 @@ __device__ __forceinline__ void gsync() {
 // returns, so the chain walk, the gram hashes and the word scans read LDS at
 // any span length (a window reload is a few 16-byte loads per lane, once per
 // ~6 KB of text per stage).  g null: the whole span is in s.text already.
+// The pointer returned is LDS only: a biased LDS pointer (s.text - w0) must
+// never meet a global one in the same value -- the compiler then widens it to
+// a flat address before the caller adds its position back, and a window past
+// s.text's LDS offset wraps into an address outside every aperture.  So a
+// block wider than the window fails here (ok = false); the parallel kernels
+// hand that document on, and the sequential span source's instantiation
+// reads such spans in place instead (WinG below).
 struct Win {
+  static constexpr bool kSeq = false;
   const uint8_t* g;
   int w0, w1;
   int len;                                     // bytes of the span buffer that may be copied
@@ -327,11 +336,10 @@ __device__ __forceinline__ const uint8_t* win_text(Win& w, SM& s, int lo, int hi
   lo = lo > 0 ? lo : 0;
   if (lo < w.w0 || hi > w.w1) {
     const int a = (lo - 32 > 0 ? lo - 32 : 0) & ~15;
-    if (!w.g) {                                  // (outside a span held whole in LDS: never read)
+    if (!w.g || hi > a + (int)sizeof(s.text) - 15) {   // (a block wider than the buffer: handed on)
       ok = false;
       return s.text - w.w0;
     }
-    if (hi > a + (int)sizeof(s.text) - 15) return w.g;   // a block wider than the window: read in place
     const int b = min(w.len, a + (int)sizeof(s.text) - 15);
     const int n16 = (b - a + 15) >> 4;
     wsync();                                     // every lane is done with the previous window
@@ -343,6 +351,30 @@ __device__ __forceinline__ const uint8_t* win_text(Win& w, SM& s, int lo, int hi
   }
   return s.text - w.w0;
 }
+
+// The window of detect<.., SEQ> (the sequential span source's documents, the
+// ones handed on): a span held whole in LDS (g null) is read there, unbiased;
+// a longer one is read in place from the slot (g), at any block width.  The
+// two pointers may meet as one flat value: neither is biased.
+// kSeq: its span text may hold malformed characters (a lead byte claiming
+// bytes that are not continuations, ' ' included), so the hit stages take
+// their character starts from the sequential decode (char_starts) instead of
+// "not a continuation byte", and a word ends only at a space that starts a
+// character -- the positions the reference's walks visit (cldutil.cc:201-533).
+struct WinG {
+  static constexpr bool kSeq = true;
+  const uint8_t* g;
+  int w0, w1;
+  int len;
+};
+template <class SM>
+__device__ __forceinline__ const uint8_t* win_text(WinG& w, SM& s, int lo, int hi, bool& ok, int lane) {
+  (void)lo; (void)hi; (void)ok; (void)lane;
+  return w.g ? w.g : s.text;
+}
+template <bool G> struct WinSel { using type = Win; };
+template <> struct WinSel<true> { using type = WinG; };
+template <bool G> using WinOf = typename WinSel<G>::type;
 
 // First set bit at or after `from` in a bitmask over positions [0, L); L if none.
 __device__ int find_first_g(const uint64_t* m, int from, int L) {
@@ -570,7 +602,7 @@ __device__ __forceinline__ uint32_t char_props(const DevTables& T, const DocView
 // Validity of the per-character formulation over the whole document, and the
 // letter-stop bitmap (one bit per byte) the span builder searches for span
 // starts.  False if the document does not tile into characters with local
-// scanner behaviour (then k_general redoes it).
+// scanner behaviour (then the sequential span source redoes it).
 __device__ __forceinline__ bool classify(const DevTables& T, const DocView& dv, Slot& S, bool& cut, int lane,
                                          uint64_t* lsm_ext = nullptr) {
   uint64_t* const lsm = lsm_ext ? lsm_ext : S.lsm;   // (documents over kDocCap: a bitmap in the staged store)
@@ -675,7 +707,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   // (after the hard limit); -1: none; no rlo: any resume point right after
   // dropped '&'s counts as a range.
   // A document whose soft limit differs across that range, or whose range
-  // straddles a regime, is re-queued (k_general scores the page itself).
+  // straddles a regime, is handed on (the sequential span source scans the page itself).
   auto soft_of = [](int r) {
     return (kMaxScriptBytes <= r && r < 2 * kMaxScriptBytes) ? r / 2 : kMaxScriptBytes - kWithinScriptTail;
   };
@@ -817,7 +849,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     const int tl = olen + ((act && (sep || hard_here)) ? 1 : 0);
     const int opre = excl_scan(tl, lane);
     if constexpr (VEC) {
-      if (out_chr && olen != n) bad = 1;         // map2uplow_ not the identity: the sequential kernel maps it
+      if (out_chr && olen != n) bad = 1;         // map2uplow_ not the identity: the sequential span source maps it
       if (out_chr)
         for (int k = 0; k < olen; ++k) omap[lpos + opre + k] = (uint32_t)orig(x + k);   // Copy
       if (act && (sep || hard_here)) {
@@ -832,7 +864,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         // the gap's: the gap starts where they began (hgap)
         if (dv.hf && fr < L && (gld(dv.hf + fr) & 2)) {
           if (sep) from = (int)gld(hgap + fr);
-          else bad = 1;                          // (after the hard limit: the sequential kernel)
+          else bad = 1;                          // (after the hard limit: the sequential span source)
         }
         omap[lpos + opre + olen] = (uint32_t)(nl - from >= 2 ? nl : from);
       }
@@ -885,7 +917,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
         }
         // vec mode: dropped '&'s right before it may stop the reference's scan
         // at the first of them (a stale script after a foreign letter,
-        // getonescriptspan.cc:876-931), one offset earlier: the sequential kernel
+        // getonescriptspan.cc:876-931), one offset earlier: the sequential span source
         if (VEC && dv.hf && (gld(dv.hf + xs) & 2)) {
           // (only when the run's last character is a letter of another script
           // -- the single-letter continuation -- is the reference's script
@@ -1606,18 +1638,29 @@ __device__ __forceinline__ void base_adds(const DevTables& T, const DevTbl& t1, 
 // at a space), mid = 2 chars on; next = e + 1 if text[e] is the word's space,
 // else mid (+1 on a vowel).  It never jumps over a space, so it enters every
 // word at its first byte and a word's entries depend on that word alone.
-template <class SM>
-__device__ __forceinline__ bool word_lists(Win& win, SM& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
+template <class SM, class WN>
+__device__ __forceinline__ bool word_lists(WN& win, SM& s, int tb, int start, Slot& S, int& nws, int& nsp, int lane) {
   lane = wave::lane_here();
   nws = 0;
   nsp = 0;
   bool ok = true;
+  int carry = 0;
+  bool prev_sp = false;                          // (WN::kSeq) a word-ending space at w0 - 1
   for (int w0 = start; w0 <= tb; w0 += 64) {
     const uint8_t* text = win_text(win, s, w0 - 1, w0 + 65, ok, lane);
     if (!ok) return false;
     const int x = w0 + lane;
-    const bool isws = x < tb && (x == start || text[x - 1] == ' ');
-    const bool issp = x <= tb && text[x] == ' ';
+    bool isws, issp;
+    if constexpr (WN::kSeq) {
+      const uint64_t cs = char_starts(text, w0, tb + 1, nullptr, carry, true, lane);
+      issp = x <= tb && ((cs >> lane) & 1) && text[x] == ' ';
+      const uint64_t spm = __ballot(issp);
+      isws = x < tb && (x == start || (lane == 0 ? prev_sp : ((spm >> (lane - 1)) & 1) != 0));
+      prev_sp = (spm >> 63) != 0;
+    } else {
+      isws = x < tb && (x == start || text[x - 1] == ' ');
+      issp = x <= tb && text[x] == ' ';
+    }
     const uint64_t m1 = __ballot(isws), m2 = __ballot(issp);
     if (isws) {
       const int k = nws + __popcll(m1 & lanemask_lt(lane));
@@ -1663,8 +1706,8 @@ __device__ __forceinline__ int walk_word(const uint8_t* text, int s, int tb, uin
   return cnt;
 }
 
-template <class SM>
-__device__ __forceinline__ int build_chain(Win& win, SM& sm, int tb, Slot& S, int nws, int lane) {
+template <class SM, class WN>
+__device__ __forceinline__ int build_chain(WN& win, SM& sm, int tb, Slot& S, int nws, int lane) {
   lane = wave::lane_here();
   int nch = 0;
   int sn = (LNG_PF & 1) && lane < nws ? S.wst[lane] : 0;       // word starts one block ahead
@@ -1703,8 +1746,8 @@ __device__ __forceinline__ int build_chain(Win& win, SM& sm, int tb, Slot& S, in
 // them), so score_round does not read the hits back; the hit list itself is
 // kept only for the debug dump (D).  Returns the round end (the reference's
 // `next`); c0 advances.
-template <bool D, class SM>
-__device__ __forceinline__ int quad_round(const DevTables& T, Win& win, SM& sm, int tb, Slot& S, int nch, int& c0, int& nb,
+template <bool D, class SM, class WN>
+__device__ __forceinline__ int quad_round(const DevTables& T, WN& win, SM& sm, int tb, Slot& S, int nch, int& c0, int& nb,
                           int& eb, bool& ok, int lane) {
   lane = wave::lane_here();
   nb = 0;
@@ -1814,8 +1857,8 @@ __device__ __forceinline__ int quad_round(const DevTables& T, Win& win, SM& sm, 
 // hits.  As in quad_round, the hits become emissions here (ed delta / ex
 // distinct with non-zero langprobs, in hit order); the hit lists are kept
 // only for the debug dump (D).
-template <bool D, class SM>
-__device__ __forceinline__ void octa_round(const DevTables& T, Win& win, SM& sm, Slot& S, int nsp, int& j0, int off, int next,
+template <bool D, class SM, class WN>
+__device__ __forceinline__ void octa_round(const DevTables& T, WN& win, SM& sm, Slot& S, int nsp, int& j0, int off, int next,
                            int& nd, int& nx, int& edm, int& exm, bool& ok, int lane) {
   lane = wave::lane_here();
   edm = 0;
@@ -1964,8 +2007,8 @@ __device__ __forceinline__ void octa_round(const DevTables& T, Win& win, SM& sm,
 // GetUniHits + GetBiHits (cldutil.cc:201-310) for one round from off.
 // As in quad_round / octa_round, the hits become emissions here (eb base,
 // edm delta, exm distinct); the hit lists are kept only for the debug dump.
-template <bool D, class SM>
-__device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, SM& sm, int tb, Slot& S, int off, int& nb, int& nd,
+template <bool D, class SM, class WN>
+__device__ __forceinline__ int cjk_round(const DevTables& T, WN& win, SM& sm, int tb, Slot& S, int off, int& nb, int& nd,
                          int& nx, int& eb, int& edm, int& exm, bool& ok, int lane) {
   lane = wave::lane_here();
   const int start = off + (ufl(win_text(win, sm, off, off + 1, ok, lane)[off]) == ' ' ? 1 : 0);
@@ -1976,12 +2019,16 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, SM& sm, i
   exm = 0;
   int next = -1;
   uint32_t endmax = (uint32_t)start;
+  int carry = 0;
   for (int w0 = start; w0 < tb; w0 += 64) {
     const uint8_t* text = win_text(win, sm, w0, w0 + 64 + 8, ok, lane);
     if (!ok) return tb;
     const int x = w0 + lane;
     int prop = 0, len = 0;
-    if (x < tb && (text[x] & 0xC0) != 0x80) {
+    bool cst;
+    if constexpr (WN::kSeq) cst = (char_starts(text, w0, tb, nullptr, carry, true, lane) >> lane) & 1;
+    else cst = (text[x] & 0xC0) != 0x80;
+    if (x < tb && cst) {
       len = utf8_len(text[x]);
       prop = uni_prop(T, text + x, len);
       endmax = (uint32_t)(x + len) > endmax ? (uint32_t)(x + len) : endmax;
@@ -2022,12 +2069,16 @@ __device__ __forceinline__ int cjk_round(const DevTables& T, Win& win, SM& sm, i
   if (next < 0) next = (int)wave::wmax(endmax);
   nd = 0;
   nx = 0;
+  carry = 0;
   for (int w0 = off; w0 < next; w0 += 64) {
     const uint8_t* text = win_text(win, sm, w0, w0 + 64 + 12, ok, lane);
     if (!ok) return tb;
     const int x = w0 + lane;
     uint32_t dp = 0, xp = 0;
-    const bool v = x < next && (text[x] & 0xC0) != 0x80;
+    bool cst;
+    if constexpr (WN::kSeq) cst = (char_starts(text, w0, next, nullptr, carry, true, lane) >> lane) & 1;
+    else cst = (text[x] & 0xC0) != 0x80;
+    const bool v = x < next && cst;
     if (v) {
       const int len = utf8_len(text[x]);
       const int len2 = utf8_len(text[x + len]) + len;
@@ -2583,8 +2634,8 @@ __device__ void dbg_round(const Slot& S, SM& s, int off, int next, int nb, int n
 
 // ScoreOneScriptSpan (scoreonescriptspan.cc:1302-1333) with the round loops
 // of ScoreCJKScriptSpan / ScoreQuadScriptSpan (:1163-1277).
-template <bool D, bool VEC = false, class SM = Smem>
-__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, SM& s, Win& win, int tb,
+template <bool D, bool VEC = false, class SM = Smem, class WN = Win>
+__device__ __forceinline__ bool score_span(const DevTables& T, Slot& S, SM& s, WN& win, int tb,
                                            int ulscript, int lane, uint32_t* tr, uint32_t doc, uint32_t cflags,
                                            VecState* V = nullptr) {
   int rt = rtype_of(T, ulscript);
@@ -2817,7 +2868,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        Win win{nullptr, 0, 16 * n16, 16 * n16};                          // the whole span is in s.text
+        WinOf<SEQ> win{nullptr, 0, 16 * n16, 16 * n16};                   // the whole span is in s.text
         ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
       } else {
         const uint8_t* text = lb;
@@ -2834,7 +2885,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
         }
-        Win win{text, 0, 0, (tb + 48 + 15) & ~15};                       // windows of it go to s.text
+        WinOf<SEQ> win{text, 0, 0, (tb + 48 + 15) & ~15};                // windows of it go to s.text (SEQ: read in place)
         ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
       }
       if (!ok) return -kWhyCapacity;
@@ -3005,7 +3056,7 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   return (uint64_t)got << 4;
 }
 
-// Documents over kDocCap (round 5; they used to take the sequential kernel):
+// Documents over kDocCap (round 5; they used to take the sequential kernel of earlier rounds):
 // the span cache and the slot's letter-stop bitmap hold at most 512 KB of
 // spans and 1 MB of text, so the region is reserved at its worst case and
 // written directly -- the spans (at most 4 lowered bytes per raw byte plus
@@ -3109,7 +3160,7 @@ __device__ __forceinline__ int st_score(const DevTables& T, Slot& S, SM& s, cons
 
 // CheapRepWordsInplace over a document's stored spans, in order, one
 // predictor for the document (detect()'s from_cache pass 2).  False: a span
-// the in-place formulation cannot take (k_general redoes the document).
+// the in-place formulation cannot take (the fused k_long redoes the document).
 __device__ __forceinline__ bool st_rep(uint16_t* tbl, Slot& S, uint8_t* region, int lane) {
   StHdr* h = reinterpret_cast<StHdr*>(region);
   const int nsp = (int)uflu(gld(&h->nsp));

@@ -11,8 +11,7 @@
 //    totes (ChunkAll + ScoreAllHits fused), so a round touches each hit once.
 //  * Scoring tables stay in HBM and are gathered through L2/MALL (they are
 //    ~0.8 MB, far below one XCD's 4 MB L2); per-lane state lives in private
-//    (scratch) memory in the short-document kernel and in a per-lane global
-//    arena in the general kernel.
+//    (scratch) memory in the short-document kernel.
 //  * The only floating point is ReliabilityExpected; this file is compiled
 //    with -ffp-contract=off so its double ops round exactly like the oracle.
 //

@@ -380,7 +380,7 @@ struct Device {
   uint8_t* d_arena = nullptr;
   uint64_t stride = 0;
   int lanes = 0;
-  uint8_t* d_slots = nullptr; // k_long per-wave slots (0 slots: CLD_LONG=0, long documents go to k_general)
+  uint8_t* d_slots = nullptr; // k_long per-wave slots 
   cld_result* d_spec_out = nullptr;   // k_long's speculative pass-2 results (small batches; CLD_LONG_SPEC=0: off)
   uint32_t* d_spec_take = nullptr;
   int n_slots = 0;               // the fused k_long's resident waves (its grid)
@@ -403,7 +403,7 @@ struct Device {
   uint32_t* h_trace = nullptr;  // CLD_TRACE=1: pinned host progress words, 4 per k_long wave
   uint32_t* d_dbg = nullptr;    // CLD_DEBUG_DOC=i: k_long dumps document i's rounds/chunks
   uint32_t dbg_doc = 0xFFFFFFFFu;
-  uint32_t fault_doc = 0xFFFFFFFFu;   // CLD_FAULT_DOC=i (tests): batch document i fails in k_long and k_general
+  uint32_t fault_doc = 0xFFFFFFFFu;   // CLD_FAULT_DOC=i (tests): batch document i gets no result in k_long
   double trace_timeout = 0;
   unsigned long long* d_prof = nullptr;   // per-stage cycle sums (CLD_PROFILE_STAGES=1)
   uint32_t* d_counters = nullptr;
@@ -718,8 +718,8 @@ int enqueue_prepare(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
 // Enqueue the whole pipeline for n documents already on device d.  special /
 // priors (device, nullable): cld_detect_batch_ex's per-document routing bits
 // and ApplyHints langprobs (16 per document); HTML documents skip the wave and
-// long kernels and run whole in k_general, hinted plain ones take the wave /
-// long kernels with their priors.  cflags: CLD2's public flags (kCldFlags).
+// wave kernel and run in k_long (rewritten, or on its sequential span source),
+// hinted plain ones take the wave / long kernels with their priors.  cflags: CLD2's public flags (kCldFlags).
 // html_bytes > 0 (the batch holds HTML pages, special & kSpecialHtml; special
 // is then the runtime's own device copy): the pages are first rewritten into
 // plain text (cld_html.hip, k_html_rewrite) in d_hbuf, indexed like buf, whose
@@ -811,8 +811,7 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
     HIP_OK(cld_launch_long(d->d_T, buf, offs, list, out, d->d_slots, d->n_slots, d->d_requeue2, ctr, d->h_trace, d->d_dbg, d->dbg_doc,
                            d->d_prof ? d->d_prof + 8 : nullptr, cflags, special, priors, hbuf, hflag, hpos, hgap,
                            d->fault_doc,
-                           d->d_spec_out, d->d_spec_take, ctr_total, ctr_deq, s));
-    HIP_OK(hipEventRecord(ev[2], s));
+                           d->d_spec_out, d->d_spec_take, ctr_total, ctr_deq, ev[2], s));
   }
   HIP_OK(hipEventRecord(ev[3], s));
   HIP_OK(hipEventRecord(d->done, s));
@@ -865,13 +864,21 @@ int collect_stats(Device* d) {
 }
 
 // Debug (CLD_TRACE=1): a batch that overruns dumps where every k_long wave is.
+// A batch whose stream ends in an error (a faulting kernel) dumps them too.
 void watch_trace(Device* d, hipStream_t s) {
   auto t0 = std::chrono::steady_clock::now();
-  while (hipStreamQuery(s) == hipErrorNotReady) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return;
     double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (el <= d->trace_timeout) continue;
-    fprintf(stderr, "cld_mi355x: batch still running after %.0f s; k_long waves (doc stage value count):\n", el);
+    if (q == hipErrorNotReady) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      if (el <= d->trace_timeout) continue;
+      fprintf(stderr, "cld_mi355x: batch still running after %.0f s; k_long waves (doc stage value count):\n", el);
+    } else {
+      fprintf(stderr, "cld_mi355x: batch failed (%s) after %.3f s; k_long waves (doc stage value count):\n",
+              hipGetErrorString(q), el);
+    }
     int untouched = 0, exited = 0;
     for (int w = 0; w < d->n_slots; ++w) {
       volatile uint32_t* t = d->h_trace + 4 * w;
@@ -886,7 +893,8 @@ void watch_trace(Device* d, hipStream_t s) {
                 t[1] & 0xFFFF, (t[1] >> 16) & 0xFF, t[1] >> 24, t[2], t[3]);
     }
     fflush(stderr);
-    abort();
+    if (q == hipErrorNotReady) abort();
+    return;                                      // (the error reaches the caller at the next sync)
   }
 }
 
@@ -1045,7 +1053,7 @@ struct HostReg {
   ~HostReg() { release(); }
 };
 
-// run_host_shard's "some documents failed" return (k_general counted and
+// run_host_shard's "some documents failed" return (k_long counted and
 // marked them); internal, never returned to a caller.
 constexpr int kDocsFailed = 1;
 
@@ -1347,7 +1355,7 @@ int run_host_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n
 }
 
 // Documents the kernels could not score come back marked CLD_LANG_FAILED
-// (k_general, kDocsFailed above); each is redone alone, so one bad document
+// (k_long, kDocsFailed above); each is redone alone, so one bad document
 // never costs the batch.  CLD_EIO only if one still fails on its own.
 // The failed documents are retried together, as one gathered batch (scoring
 // is deterministic: outside fault injection a document that failed fails
@@ -1499,8 +1507,8 @@ int run_vec_shard(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n,
     HIP_OK(hipMemcpyAsync(res, V.out, m * sizeof(cld_result), hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(nch.data(), V.nch, m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    // statistics (cld_last_batch_stats): documents the parallel kernel finished
-    // (long_docs) and those the sequential kernel took (general_docs)
+    // statistics (cld_last_batch_stats): documents the parallel span builder
+    // finished (long_docs) and those the sequential span source took (general_docs)
     vst.docs += m;
     vst.general_docs += ctr[kCtrSeq];
     vst.long_docs += m - ctr[kCtrSeq];

@@ -26,7 +26,7 @@
 // A document the wave cannot reproduce exactly in this form (longer than CAP,
 // a byte sequence whose scanner/lowercaser state crosses a character
 // boundary, a bucket overflow, or a second pass) is appended to the re-queue
-// list and redone from scratch by the general kernel, so results stay
+// list and redone from scratch by k_long, so results stay
 // bit-identical to the sequential restatement in every case.
 
 namespace cld {

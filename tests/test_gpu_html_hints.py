@@ -6,8 +6,8 @@ tests/test_html_hints.py::test_hint_priors_match_reference); the oracle then
 scores each document with the same priors and is_plain_text flag.  HTML
 pages are rewritten into plain text on the GPU (cld_html.hip: tags -> one
 space, entities decoded, lookahead marks) and scored by the wave / long
-kernels; pages the rewrite cannot take stay on k_general, the exact
-sequential kernel.  Hinted plain documents stay on the wave / long kernels,
+kernels; pages the rewrite cannot take are scanned by k_long's sequential
+span source (cld_seq.hip).  Hinted plain documents stay on the wave / long kernels,
 which add the prior boosts and apply the whacks in their chunk totes.
 """
 import numpy as np
@@ -104,7 +104,7 @@ def test_html_rewrite_lookahead_edges(gpu, oracle):
     n = len(docs)
     got = gpu.detect_batch_ex(buf=buf, offsets=offs, html=True)
     st = gpu.last_stats()
-    assert 1 <= st.general_docs < n // 4
+    assert st.general_docs < n // 4                # (the 4-byte pages are rewritten too since round 6)
     pr = priors_for(gpu, buf, offs, True, None)
     ref = oracle.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=8)
     assert_same(got, ref, "html rewrite edges")

@@ -92,7 +92,7 @@ def test_long_documents(gpu, oracle):
 def test_squeeze_documents_stay_on_the_wavefront_path(gpu, oracle):
     """CheapSqueezeTriggerTest restarts (compact_lang_det_impl.cc:1867-1900) and
     the Squeeze / Squeeze+Repeats passes run in k_long: bit-exact, and no
-    document falls through to the sequential kernel."""
+    document falls through to the sequential span source."""
     b3, o3 = corpus.c3(2000, seed=21, boiler_frac=0.05)
     b2, o2 = corpus.c2(3000, seed=22)
     docs = [bytes(b3[o3[i]:o3[i + 1]]) for i in range(2000)]
@@ -234,7 +234,7 @@ def test_staged_long_path_and_its_hand_ons(gpu, oracle):
     spans (span-parallel, passes 1 and 2), more than 1,024 spans, the Squeeze
     restart, pass 2 with Repeats -- in one batch large enough to take the
     staged path (more than 4 documents per fused wave), all equal to the
-    oracle and none on the sequential kernel.
+    oracle and none on the sequential span source.
     Then the store exhausted (CLD_LONG_STORE_MB=1, child process): every
     document the store cannot hold goes to the fused kernel, same results."""
     import subprocess
@@ -272,7 +272,7 @@ def test_documents_over_one_megabyte(gpu, oracle):
     """Documents between 1 and 4 MB (over k_long's kDocCap): the staged path
     writes their spans straight into a worst-case region of its store with the
     letter-stop bitmap there too (cld_long.hip st_spans_big), in a small batch
-    and in a large one -- equal to the oracle, none on the sequential kernel."""
+    and in a large one -- equal to the oracle, none on the sequential span source."""
     rng = np.random.default_rng(181)
     b3, o3 = corpus.c3(260, seed=182)
     b2, o2 = corpus.c2(40000, seed=183)

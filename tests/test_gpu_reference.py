@@ -53,7 +53,7 @@ def test_gpu_html_four_byte_characters_on_parallel_kernels(gpu, ref):
     """HTML pages with emoji and other 4-byte characters (raw and as numeric
     entities, corpus.html emoji=1): rewritten on the GPU like any other page
     (k_build_cpt4: no 4-byte character lowers differently in HTML mode) and
-    scored by k_wave / k_long -- none on the sequential kernel -- equal to the
+    scored by k_wave / k_long -- none on the sequential span source -- equal to the
     reference, with and without chunk vectors."""
     for lo, hi, n, seed in ((200, 6000, 3000, 41), (14000, 18000, 300, 42), (41000, 90000, 40, 43)):
         buf, offs = corpus.html(n, seed=seed, lo=lo, hi=hi, emoji=1.0)

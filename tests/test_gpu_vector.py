@@ -140,7 +140,7 @@ print("retry ok")
 
 def test_failed_document_is_redone_alone_and_the_batch_stands():
     """One document the kernels cannot score (fault injection: CLD_FAULT_DOC=k
-    makes batch document k fail in k_long and k_general) costs neither the
+    makes batch document k fail in k_long) costs neither the
     batch nor the process: it comes back marked CLD_LANG_FAILED, is redone
     alone (as document 0 of a one-document batch, which succeeds), and every
     result equals the reference.  With CLD_FAULT_DOC=0 the retry fails too:
@@ -154,7 +154,7 @@ import sys, numpy as np, cld_amd, corpus, refcld, os
 cld_amd.init()
 ref = refcld.instance(os.environ["CLD_MI355X_TABLES"])
 fault = int(os.environ["CLD_FAULT_DOC"])
-b, off = corpus.c3(40, seed=21)                      # long documents: k_wave -> k_long -> k_general
+b, off = corpus.c3(40, seed=21)                      # long documents: k_wave -> k_long
 want = ref.detect_batch(b, off, threads=8)
 F = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
 try:

@@ -3,8 +3,7 @@ every document of BASELINE's C2 (1M tweets), C3 (100K 16 KB pages) and C4
 (1.1M CJK-heavy documents), 200K documents of C5's stream, and 100K HTML pages
 (is_plain_text = false, cld_detect_batch_ex; a quarter of them with emoji and
 other 4-byte characters, raw and as entities), through the
-product's batch entry point (cld_detect_batch: routing, k_wave, k_long,
-k_general) and through oracle/_ref/librefcld2.so (the reference's own sources
+product's batch entry point (cld_detect_batch: routing, k_wave, k_long) and through oracle/_ref/librefcld2.so (the reference's own sources
 in dynamic-data mode, 16 host threads), every result field compared.  Twice:
 with the synthetic Q1 quadgram table (the suite's default) and with the
 product's shipped Q0 tables, loaded on both sides through the cld2 data-file
@@ -49,7 +48,7 @@ def test_full_size_equals_reference(gpu, ref_tables, name):
     ub = ub_docs(buf, offs)
     bad &= ~ub
     print("%s/%s: %d documents, %d bytes, %d mismatches, %d excluded (ill-formed lead bytes); "
-          "k_wave %d, k_long %d, k_general %d; passes %s" % (name, label, n, int(offs[-1]), int(bad.sum()),
+          "k_wave %d, k_long %d, sequential spans %d; passes %s" % (name, label, n, int(offs[-1]), int(bad.sum()),
                                                               int(ub.sum()), st.short_docs, st.long_docs,
                                                               st.general_docs, list(st.passes)))
     assert not bad.any(), "%s/%s: %d of %d differ, first %s" % (name, label, bad.sum(), n, np.nonzero(bad)[0][:5])

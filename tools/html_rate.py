@@ -2,8 +2,7 @@
 mixed 200-6000 B, 16k and 64k pages, and the same with 4-byte characters on
 every page: emoji, emoji16k, emoji64k; HTML_RATE_SETS),
 inputs resident on the host (cld_detect_batch_ex): docs/s from the device
-timers (every kernel of the batch: the HTML rewrite, k_wave, k_long,
-k_general) and end to end, beside the reference CLD2 (oracle/_ref/librefcld2.so,
+timers (every kernel of the batch: the HTML rewrite, k_wave, k_long) and end to end, beside the reference CLD2 (oracle/_ref/librefcld2.so,
 ExtDetectLanguageSummary with is_plain_text = false) on the box's cores over a
 bounded sample of the same pages; every page is checked against it."""
 import json

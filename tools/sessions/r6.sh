@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-6 GPU sessions on the committed tree.  STEPS picks what runs, in order:
 #   suite  the whole GPU suite          tests  PYTESTS=<files/ids> only
+#   diag   one mixed batch (tools/diag_batch.py) against the oracle
 #   smoke  __graft_entry__.smoke()      bench  the default bench line
 #   lines  C3/C4/C5 bench lines         prof   rocprofv3 kernel statistics, C2 and C3
 #   pmc    PMC passes (k_wave @ C2, k_long @ C3)
@@ -17,11 +18,14 @@ R=$PWD
 O=$R/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 step() { local t=$1 log=$2; shift 2; echo "[$(date +%T)] $log" | tee -a $O/session.log
-  timeout -k 10 $t "$@" > $O/$log 2>&1; local rc=$?; echo "[$(date +%T)] rc=$rc" | tee -a $O/session.log
+  timeout -k 10 $t "$@" > $O/$log 2>&1; local rc=$?
+  if [ $rc -eq 0 ] && grep -q "HSA_STATUS_ERROR" $O/$log; then rc=99; fi   # a GPU fault even on exit 0
+  echo "[$(date +%T)] rc=$rc" | tee -a $O/session.log
   if [ $rc -ne 0 ]; then tail -30 $O/$log; exit $rc; fi; }
 for s in ${STEPS:-suite smoke bench}; do
   case $s in
     suite) step 1000 pytest_gpu.txt python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread; tail -1 $O/pytest_gpu.txt ;;
+    diag) step 150 diag.txt python -u tools/diag_batch.py ;;
     tests) step 600 pytest_sel.txt python -u -m pytest ${PYTESTS} -m gpu -x -v --timeout 200 --timeout-method thread; tail -1 $O/pytest_sel.txt ;;
     smoke) step 300 smoke.txt python -u -c "import __graft_entry__ as g; g.smoke()"; tail -2 $O/smoke.txt ;;
     bench) step 400 bench.json python bench.py ;;

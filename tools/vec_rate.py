@@ -3,7 +3,7 @@
 mode (oracle/_ref/librefcld2.so, ExtDetectLanguageSummary with a
 ResultChunkVector) on 16 host threads timed beside it and compared result for
 result, chunk for chunk.  Plain documents run the parallel kernels
-(k_long<VEC>); HTML pages and hand-ons the sequential kernel (k_general_vec).
+(k_long<VEC>); HTML pages and hand-ons its sequential span source (cld_seq.hip).
 One JSON line per workload."""
 import json
 import os
