@@ -93,7 +93,7 @@ __device__ __forceinline__ bool html_lower_same(const DevTables& T, uint32_t b0,
 
 // ScanToPossibleLetter (getonescriptspan.cc:150-203, 503-541) with the tag
 // parser's transition function as two LDS tables built from tag_class /
-// tag_next (cld_pipeline.hip) at block start: one lookup per byte and no
+// tag_next (cld_prims.hip) at block start: one lookup per byte and no
 // branch per state, so lanes in different states do not serialise.
 constexpr int kTagStates = 40, kTagClasses = TC_PL + 1;
 struct TagTables {

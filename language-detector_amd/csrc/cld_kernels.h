@@ -76,7 +76,7 @@ hipError_t cld_launch_wave(const DevTables* T, const uint8_t* buf, const uint64_
 // requeue_list == nullptr (counters unused), marked in their result:
 // summary_lang = kWaveRequeued.
 constexpr uint16_t kWaveRequeued = 0xFFFE;
-// kMaxScriptBytes (cld_pipeline.hip): rewritten HTML pages this long and
+// kMaxScriptBytes (cld_prims.hip): rewritten HTML pages this long and
 // longer carry page offsets (hpos / hgap) for the span soft limit
 constexpr int kHtmlSoftMin = 40928;
 // lng::kDocCap (cld_long.hip): the fused k_long takes documents up to this

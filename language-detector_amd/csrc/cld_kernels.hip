@@ -12,7 +12,7 @@
 #if defined(WAVE_STOP) || defined(LNG_EXP_NOADDS) || defined(HTML_EXP) || defined(LNG_INC)
 #error "experiment knobs (WAVE_STOP, LNG_EXP_NOADDS, HTML_EXP, LNG_INC) are not part of the product build"
 #endif
-#include "cld_pipeline.hip"
+#include "cld_prims.hip"
 #include "cld_wave.hip"
 #include "cld_long.hip"
 #include "cld_html.hip"

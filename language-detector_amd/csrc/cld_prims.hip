@@ -1,21 +1,14 @@
-// cld_pipeline.hip -- the CLD2 DetectLanguage hot path as gfx950 device code.
+// cld_prims.hip -- the device primitives every kernel shares (k_wave,
+// k_long and its staged stages, k_html_rewrite): byte helpers, the table
+// state machines (script numbers, the lowercaser), gram hashes and bucket
+// probes, the document tote, reliability, the HTML tag / entity scanner
+// pieces and the summary.  Each is a small function with the reference lines
+// whose semantics it implements; the per-document pipelines that compose them
+// are the wave-parallel kernels (cld_wave.hip, cld_long.hip, cld_seq.hip).
 //
-// One document per lane.  A wavefront carries 64 independent documents
-// through span segmentation, lowercasing, gram hashing + bucket probes, chunk
-// totes and the document tote/summary.  Design notes:
-//
-//  * No per-round hit buffers of the reference size: quad/octa/uni/bi hits are
-//    kept as packed (u16 offset, u32 indirect) streams sized to the kernel's
-//    document-length bucket; LinearizeAll's linear[] array is never built --
-//    the three sorted hit streams are merge-walked directly into the chunk
-//    totes (ChunkAll + ScoreAllHits fused), so a round touches each hit once.
-//  * Scoring tables stay in HBM and are gathered through L2/MALL (they are
-//    ~0.8 MB, far below one XCD's 4 MB L2); per-lane state lives in private
-//    (scratch) memory in the short-document kernel.
+//  * Scoring tables stay in HBM and are gathered through L2/MALL.
 //  * The only floating point is ReliabilityExpected; this file is compiled
 //    with -ffp-contract=off so its double ops round exactly like the oracle.
-//
-// Every function cites the reference lines whose semantics it implements.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
