@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "cld_coalesce.h"
+#include "cld_dlqueue.h"
 #include "cld_device.h"
 #include "cld_dynamic_data.h"
 #include "cld_hints.h"
@@ -1278,26 +1279,30 @@ bool tiny_zero_copy() {
   return v;
 }
 
-int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
-  TinySlot* t = nullptr;
-  std::unique_lock<std::mutex> lk;
-  const int ns = tiny_slots();
-  for (int k = 0; k < ns; ++k) {
-    std::unique_lock<std::mutex> l(d->tiny[k].mu, std::try_to_lock);
-    if (l.owns_lock()) { t = &d->tiny[k]; lk = std::move(l); break; }
-  }
-  if (!t) {
-    t = &d->tiny[d->tiny_rr.fetch_add(1) % ns];
-    lk = std::unique_lock<std::mutex>(t->mu);
-  }
+struct DocRef {
+  const uint8_t* p;
+  size_t len;
+};
+
+// k_wave alone over n documents of at most kWaveCap bytes in tiny slot t (the
+// caller holds t->mu): doc(i) -> DocRef, written straight into the slot's
+// pinned block.  Results in out; the documents k_wave hands on come back
+// marked kWaveRequeued (no counters).
+template <class DocFn>
+int tiny_run_slot(Device* d, TinySlot* t, size_t n, DocFn doc, cld_result* out, uint32_t flags) {
   HIP_OK(hipSetDevice(d->id));
-  const uint64_t base = offs[0], bytes = offs[n] - base;
   const size_t text_off = kTinyOffsOff + (n + 1) * sizeof(uint64_t);
   const size_t out_off = kTinyCtrOff - n * sizeof(cld_result);
   uint64_t* ho = (uint64_t*)(t->h + kTinyOffsOff);
-  for (size_t i = 0; i <= n; ++i) ho[i] = offs[i] - base;
-  memcpy(t->h + text_off, buf + base, bytes);
-  // documents k_wave cannot finish come back marked (kWaveRequeued), no counters
+  uint8_t* ht = t->h + text_off;
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const DocRef r = doc(i);
+    ho[i] = bytes;
+    memcpy(ht + bytes, r.p, r.len);
+    bytes += r.len;
+  }
+  ho[n] = bytes;
   if (tiny_zero_copy()) {
     HIP_OK(cld_launch_wave_only(&d->T, t->hd + text_off, (const uint64_t*)(t->hd + kTinyOffsOff), (int)n,
                                 (cld_result*)(t->hd + out_off), nullptr, nullptr, flags & kCldFlags, t->s));
@@ -1310,25 +1315,27 @@ int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_
   }
   HIP_OK(hipStreamSynchronize(t->s));
   memcpy(out, t->h + out_off, n * sizeof(cld_result));
-  lk.unlock();
+  return CLD_OK;
+}
+
+// The documents of a tiny call that k_wave handed on (kWaveRequeued), gathered
+// and redone on the streamed path; *st gets the call's statistics.
+template <class DocFn>
+int tiny_redo_requeued(Device* d, size_t n, DocFn doc, cld_result* out, uint32_t flags, cld_batch_stats* st) {
   std::vector<uint32_t> list;
   for (size_t i = 0; i < n; ++i)
     if (out[i].summary_lang == kWaveRequeued) list.push_back((uint32_t)i);
   const uint32_t rq = (uint32_t)list.size();
-  cld_batch_stats st{};
-  st.docs = n;
-  st.short_docs = n - rq;
-  st.passes[0] = n - rq;
-  if (rq == 0) {
-    std::unique_lock<std::mutex> dl(d->mu, std::try_to_lock);   // best effort: diagnostics only
-    if (dl.owns_lock()) { d->last = st; d->stats_pending = false; }
-    return CLD_OK;
-  }
-  // the re-queued documents, gathered, on the streamed path
+  *st = cld_batch_stats{};
+  st->docs = n;
+  st->short_docs = n - rq;
+  st->passes[0] = n - rq;
+  if (rq == 0) return CLD_OK;
   std::vector<uint8_t> gb;
   std::vector<uint64_t> go{0};
   for (uint32_t i : list) {
-    gb.insert(gb.end(), buf + offs[i], buf + offs[i + 1]);
+    const DocRef r = doc(i);
+    gb.insert(gb.end(), r.p, r.p + r.len);
     go.push_back(gb.size());
   }
   std::vector<cld_result> gout(rq);
@@ -1337,13 +1344,40 @@ int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_
   for (uint32_t k = 0; k < rq; ++k) out[list[k]] = gout[k];
   std::lock_guard<std::mutex> dl(d->mu);
   const cld_batch_stats s2 = d->last;                  // the streamed call's counts for the re-queued documents
-  st.long_docs = s2.long_docs;
-  st.general_docs = s2.general_docs;
-  st.short_docs += s2.short_docs;
-  for (int k = 0; k < 4; ++k) st.passes[k] += s2.passes[k];
-  for (int k = 0; k < 8; ++k) st.long_requeue[k] = s2.long_requeue[k];
-  st.short_ms = s2.short_ms; st.long_ms = s2.long_ms; st.general_ms = s2.general_ms;
-  d->last = st;
+  st->long_docs = s2.long_docs;
+  st->general_docs = s2.general_docs;
+  st->short_docs += s2.short_docs;
+  for (int k = 0; k < 4; ++k) st->passes[k] += s2.passes[k];
+  for (int k = 0; k < 8; ++k) st->long_requeue[k] = s2.long_requeue[k];
+  st->short_ms = s2.short_ms; st->long_ms = s2.long_ms; st->general_ms = s2.general_ms;
+  return rc;
+}
+
+int run_tiny(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_result* out, uint32_t flags) {
+  TinySlot* t = nullptr;
+  std::unique_lock<std::mutex> lk;
+  const int ns = tiny_slots();
+  for (int k = 0; k < ns; ++k) {
+    std::unique_lock<std::mutex> l(d->tiny[k].mu, std::try_to_lock);
+    if (l.owns_lock()) { t = &d->tiny[k]; lk = std::move(l); break; }
+  }
+  if (!t) {
+    t = &d->tiny[d->tiny_rr.fetch_add(1) % ns];
+    lk = std::unique_lock<std::mutex>(t->mu);
+  }
+  auto doc = [&](size_t i) { return DocRef{buf + offs[i], (size_t)(offs[i + 1] - offs[i])}; };
+  if (int rc = tiny_run_slot(d, t, n, doc, out, flags)) return rc;
+  lk.unlock();
+  cld_batch_stats st{};
+  const int rc = tiny_redo_requeued(d, n, doc, out, flags, &st);
+  if (rc != CLD_OK && rc != kDocsFailed) return rc;
+  if (st.docs == st.short_docs) {
+    std::unique_lock<std::mutex> dl(d->mu, std::try_to_lock);   // best effort: diagnostics only
+    if (dl.owns_lock()) { d->last = st; d->stats_pending = false; }
+  } else {
+    std::lock_guard<std::mutex> dl(d->mu);
+    d->last = st;
+  }
   return rc;
 }
 
@@ -1783,9 +1817,13 @@ int cld_plan_shards(const uint64_t* offsets, size_t n, int nshards, size_t* cuts
   return CLD_OK;
 }
 
+namespace {
+void dl_stop();
+}
 void cld_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   std::unique_lock<std::shared_mutex> tl(g_swap_mu);
+  dl_stop();
   for (Device* d : g_devs) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
@@ -1965,6 +2003,118 @@ int run_coalesced(const uint8_t* buf, const uint64_t* offs, size_t n, cld_result
   co.slots_tiny.store((int)g_devs.size() * tiny_slots(), std::memory_order_relaxed);
   CoReq me(buf, offs, n, out, flags, tiny_request(offs, n, flags));
   return co.submit(&me);
+}
+
+// detect_language's per-call path (cld_dlqueue.h): dispatcher threads, CLD_DL_DISPATCHERS
+// per context (default 4, at most tiny_slots()), each on tiny slot k of its
+// context, started on the first call (detached: they sleep on a futex when
+// idle) and stopped by cld_shutdown.  CLD_DL_QUEUE=0: the calls take the
+// coalescer (A/B).  C2 tweets, detect_language per call (profiles/
+// round6_dl_rate_ab.jsonl): 256 callers 158 K docs/s on the coalescer (CPU
+// quota exhausted: 117 us of CPU per call, 24 s throttled) -> 1.09 M with 2
+// dispatchers, 1.30 M with 4 (17 us of CPU per call); 64 callers 406 K ->
+// 486 K; a lone caller 25.0 K -> 22.6 K (the handoff to a dispatcher).
+cld::DlQueue g_dlq;
+int dl_dispatchers() {
+  static const int v = std::max(1, std::min(tiny_slots(), getenv("CLD_DL_DISPATCHERS") ? atoi(getenv("CLD_DL_DISPATCHERS")) : 4));
+  return v;
+}
+bool dl_queue_on() {
+  static const bool v = !(getenv("CLD_DL_QUEUE") && atoi(getenv("CLD_DL_QUEUE")) == 0);
+  return v;
+}
+// how long callers (while fewer than 16 calls are in flight) and idle dispatchers spin before sleeping
+int dl_caller_spin_us() {
+  static const int v = getenv("CLD_DL_SPIN_US") ? atoi(getenv("CLD_DL_SPIN_US")) : 30;
+  return v;
+}
+int dl_dispatcher_spin_us() {
+  static const int v = getenv("CLD_DL_IDLE_SPIN_US") ? atoi(getenv("CLD_DL_IDLE_SPIN_US")) : 100;
+  return v;
+}
+
+constexpr size_t kDlStop = ~(size_t)0;     // a request that stops the dispatcher taking it (dl_stop)
+
+void dl_dispatch(Device* d, int k) {
+  TinySlot* t = &d->tiny[k];
+  std::vector<cld::DlReq*> v, stops;
+  std::vector<cld_result> out(kTinyDocs);
+  for (;;) {
+    v.clear();
+    stops.clear();
+    for (cld::DlReq* r = g_dlq.take(dl_dispatcher_spin_us()); r; r = r->next) (r->len == kDlStop ? stops : v).push_back(r);
+    for (size_t a = 0; a < v.size(); a += kTinyDocs) {
+      const size_t n = std::min(kTinyDocs, v.size() - a);
+      cld::DlReq* const* g = v.data() + a;
+      auto doc = [&](size_t i) { return DocRef{g[i]->p, g[i]->len}; };
+      int rc;
+      {
+        std::lock_guard<std::mutex> lk(t->mu);
+        rc = tiny_run_slot(d, t, n, doc, out.data(), 0);
+      }
+      if (rc == CLD_OK) {
+        cld_batch_stats st{};
+        rc = tiny_redo_requeued(d, n, doc, out.data(), 0, &st);
+      }
+      for (size_t i = 0; i < n; ++i) {
+        *static_cast<cld_result*>(g[i]->res) = out[i];
+        // a document without a result is redone alone by its caller
+        g[i]->rc = rc == kDocsFailed ? (out[i].summary_lang == CLD_LANG_FAILED ? kDocsFailed : CLD_OK) : rc;
+        g_dlq.done_one();
+      }
+      cld::finish_batch(g, n);
+    }
+    if (!stops.empty()) {                      // (every request of the batch is finished)
+      for (size_t i = 0; i < stops.size(); ++i) g_dlq.done_one();
+      cld::finish_batch(stops.data(), stops.size());
+      return;
+    }
+  }
+}
+
+// 0: not started, 1: dispatchers running, 2: off (diagnostics on some context).
+std::atomic<int> g_dl_state{0};
+std::mutex g_dl_mu;
+int g_dl_threads = 0;
+
+// Eligible: a document k_wave takes (<= kWaveCap bytes), no diagnostics on
+// any context (they need the streamed path's launches).  The caller holds
+// g_swap_mu (shared) or g_init_mu: the contexts are fixed.
+bool dl_queue_takes(size_t len) {
+  if (len > (size_t)kWaveCap || !dl_queue_on() || !tiny_enabled()) return false;
+  int st = g_dl_state.load(std::memory_order_acquire);
+  if (st == 0) {
+    std::lock_guard<std::mutex> lk(g_dl_mu);
+    st = g_dl_state.load();
+    if (st == 0) {
+      bool ok = true;
+      for (Device* d : g_devs)
+        if (d->d_dbg || d->h_trace || d->d_prof || d->fault_doc != 0xFFFFFFFFu) ok = false;
+      if (ok) {
+        for (Device* d : g_devs)
+          for (int k = 0; k < dl_dispatchers(); ++k) std::thread(dl_dispatch, d, k).detach();
+        g_dl_threads = (int)g_devs.size() * dl_dispatchers();
+      }
+      st = ok ? 1 : 2;
+      g_dl_state.store(st, std::memory_order_release);
+    }
+  }
+  return st == 1;
+}
+
+// cld_shutdown (g_swap_mu held exclusively: no call is in flight): one stop
+// request per dispatcher, each waited for, before the contexts go.
+void dl_stop() {
+  std::lock_guard<std::mutex> lk(g_dl_mu);
+  if (g_dl_state.load() == 1)
+    for (int k = 0; k < g_dl_threads; ++k) {
+      cld_result dummy{};
+      cld::DlReq r(nullptr, kDlStop, &dummy);
+      g_dlq.push(&r);
+      r.wait(0);
+    }
+  g_dl_threads = 0;
+  g_dl_state.store(0);
 }
 
 Device* pick_context() {
@@ -2349,7 +2499,19 @@ const char* detect_language(const char* text) {
   const char* t = text ? text : "";
   const uint64_t offs[2] = {0, (uint64_t)strlen(t)};
   cld_result res{};
-  int rc = cld_detect_batch((const uint8_t*)t, offs, 1, &res, 0);
+  int rc;
+  bool queued = false;
+  {
+    std::shared_lock<std::shared_mutex> tl(g_swap_mu);   // (the tables stay while the call is in flight)
+    if (dl_queue_takes((size_t)offs[1])) {    // the per-call queue (cld_dlqueue.h)
+      cld::DlReq r((const uint8_t*)t, (size_t)offs[1], &res);
+      const int before = g_dlq.push(&r);
+      r.wait(before < 16 ? dl_caller_spin_us() : 0);
+      rc = r.rc;
+      queued = true;
+    }
+  }
+  if (!queued) rc = cld_detect_batch((const uint8_t*)t, offs, 1, &res, 0);
   if (rc != CLD_OK && !(rc == CLD_EIO && res.summary_lang == CLD_LANG_FAILED)) {
     // A coalesced call returns its whole group's code: a failure of the
     // group (e.g. CLD_ENOMEM growing the pinned arena for other callers'

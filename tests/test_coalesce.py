@@ -52,3 +52,39 @@ def test_mixed_requests_under_sanitizers(sim_sanitized, san, callers, spin, wake
     assert d["wrong"] == 0 and d["calls"] == callers * 40 and d["non_tiny_calls"] == callers // 4 * 40
     # a non-tiny request waits for at most a few groups, not for the tiny stream to dry up
     assert d["non_tiny_latency_us_p99"] < 4 * d["latency_us_p99"] + 20000
+
+
+# detect_language's per-call queue (language-detector_amd/csrc/cld_dlqueue.h)
+# with a mock dispatch (tools/dlqueue_sim.cpp): lock-free stack, futex waits,
+# binary-tree wake-ups, dispatcher stop requests.
+
+@pytest.fixture(scope="module")
+def dlsim():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools"), "build/dlqueue_sim", "build/dlqueue_sim_asan",
+                    "build/dlqueue_sim_tsan"], check=True)
+    return {k: os.path.join(ROOT, "tools", "build", "dlqueue_sim" + k) for k in ("", "_asan", "_tsan")}
+
+
+@pytest.mark.parametrize("callers,dispatchers,cspin,dspin", [(1, 2, 30, 100), (8, 2, 30, 100), (64, 2, 30, 0),
+                                                             (256, 2, 0, 100), (256, 4, 30, 0)])
+def test_dl_queue_every_caller_gets_its_own_result(dlsim, callers, dispatchers, cspin, dspin):
+    calls = max(20, 8000 // callers)
+    r = subprocess.run([dlsim[""], str(callers), str(calls), str(dispatchers), "30", str(cspin), str(dspin)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["wrong"] == 0 and d["calls"] == callers * calls
+    if callers >= 64:
+        assert d["docs_per_batch"] > 2          # calls that arrive during a launch share the next one
+
+
+@pytest.mark.parametrize("san,callers,dispatchers,cspin,dspin", [("_tsan", 64, 2, 30, 100), ("_tsan", 16, 1, 0, 0),
+                                                                 ("_asan", 128, 3, 0, 0), ("_asan", 32, 2, 30, 50)])
+def test_dl_queue_under_sanitizers(dlsim, san, callers, dispatchers, cspin, dspin):
+    """Each request is a heap object freed the moment wait() returns: a
+    dispatcher or a wake-up parent still touching it is a report."""
+    r = subprocess.run([dlsim[san], str(callers), "40", str(dispatchers), "20", str(cspin), str(dspin)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "Sanitizer" not in r.stderr, r.stdout + r.stderr[-4000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["wrong"] == 0 and d["calls"] == callers * 40

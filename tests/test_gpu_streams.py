@@ -5,6 +5,7 @@ slots, staging) is shared, so every enqueue waits on the previous batch's
 the oracle's.  Device buffers and streams come straight from the HIP runtime
 (ctypes), the way a caller that owns its own streams would make them."""
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -269,3 +270,40 @@ def test_detect_language_many_callers(gpu, oracle):
     [t.join() for t in th]
     bad = [i for i in range(len(texts)) if got[i] != want[i]]
     assert not bad, (len(bad), bad[:5], [got[i] for i in bad[:5]], [want[i] for i in bad[:5]])
+
+
+DL_SHUTDOWN_SCRIPT = r"""
+import sys, threading
+sys.path[:0] = [sys.argv[1] + "/language-detector_amd", sys.argv[1] + "/oracle", sys.argv[1] + "/tests"]
+import ctypes, corpus, cld_amd
+from oracle import Oracle
+b2, o2 = corpus.c2(2000, seed=171)
+texts = [bytes(b2[o2[i]:o2[i + 1]]) for i in range(2000)]
+want = [Oracle().detect_language(t) for t in texts]
+for rnd in range(2):                       # the queue's dispatchers stop at cld_shutdown and restart after
+    got = [None] * len(texts)
+    def worker(lo):
+        for i in range(lo, len(texts), 128):
+            got[i] = cld_amd.detect_language(texts[i])
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(128)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    bad = [i for i in range(len(texts)) if got[i] != want[i]]
+    assert not bad, (rnd, len(bad), bad[:5])
+    cld_amd.lib().cld_shutdown()
+print("ok")
+"""
+
+
+def test_detect_language_queue_across_shutdown(tmp_path):
+    """detect_language's per-call queue (cld_dlqueue.h) from 128 threads: every
+    answer equals the oracle's, cld_shutdown stops the dispatcher threads
+    before the contexts go, and the next call starts them again.  In its own
+    process (it shuts the runtime down)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "dl_shutdown.py"
+    script.write_text(DL_SHUTDOWN_SCRIPT)
+    r = subprocess.run([sys.executable, str(script), root], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-3000:]

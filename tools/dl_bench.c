@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <time.h>
 
 #include "wrapper.h"
@@ -30,6 +31,25 @@ static double now_s(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
   return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static double cpu_s(void) {           /* user + system CPU of the process so far */
+  struct rusage r;
+  getrusage(RUSAGE_SELF, &r);
+  return (double)r.ru_utime.tv_sec + 1e-6 * (double)r.ru_utime.tv_usec + (double)r.ru_stime.tv_sec +
+         1e-6 * (double)r.ru_stime.tv_usec;
+}
+
+/* cgroup v2 CPU throttling so far (microseconds), or -1 where not readable */
+static long long throttled_us(void) {
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return -1;
+  char k[64];
+  long long v, t = -1;
+  while (fscanf(f, "%63s %lld", k, &v) == 2)
+    if (!strcmp(k, "throttled_usec")) t = v;
+  fclose(f);
+  return t;
 }
 
 static void* slurp(const char* path, size_t* n) {
@@ -127,9 +147,11 @@ int main(int argc, char** argv) {
     pthread_create(&th[c], NULL, run, &jobs[c]);
   }
   pthread_barrier_wait(&bar);          /* everyone warmed up */
-  const double t0 = now_s();
+  const double t0 = now_s(), c0 = cpu_s();
+  const long long th0 = throttled_us();
   pthread_barrier_wait(&bar);          /* everyone done */
-  const double wall = now_s() - t0;
+  const double wall = now_s() - t0, cpu = cpu_s() - c0;
+  const long long th1 = throttled_us();
   for (int c = 0; c < callers; ++c) pthread_join(th[c], NULL);
   const size_t nl = (size_t)callers * (size_t)calls;
   double* all = (double*)malloc(sizeof(double) * nl);
@@ -141,8 +163,10 @@ int main(int argc, char** argv) {
   }
   qsort(all, nl, sizeof(double), cmp_d);
   printf("{\"mode\": \"%s\", \"callers\": %d, \"calls\": %zu, \"latency_us_p50\": %.1f, \"latency_us_p99\": %.1f, "
-         "\"latency_us_max\": %.1f, \"docs_per_s\": %.0f, \"seconds\": %.3f, \"sink\": %llu}\n",
+         "\"latency_us_max\": %.1f, \"docs_per_s\": %.0f, \"seconds\": %.3f, \"cpu_us_per_call\": %.2f, "
+         "\"throttled_ms\": %.1f, \"sink\": %llu}\n",
          ref ? "reference" : "gpu", callers, nl, 1e6 * all[nl / 2], 1e6 * all[(size_t)(0.99 * (double)(nl - 1))],
-         1e6 * all[nl - 1], (double)nl / wall, wall, sink);
+         1e6 * all[nl - 1], (double)nl / wall, wall, 1e6 * cpu / (double)nl,
+         (th0 >= 0 && th1 >= 0) ? 1e-3 * (double)(th1 - th0) : -1.0, sink);
   return 0;
 }
