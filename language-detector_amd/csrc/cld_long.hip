@@ -682,6 +682,45 @@ __device__ __forceinline__ int next_stop(const uint64_t* lsm, int y, int L) {
   return r < L ? r : L;
 }
 
+// The span builder's software pipeline, carried from one span of a document
+// to the next (the staged span kernel's loop, st_spans): the window the span
+// ended in (raw bytes and property gathers), the next window's (gathers
+// issued) and the raw words of the one after.  Short spans (C3's pages hold
+// 200-760 in 16 KB) start in the window the previous one stopped in, so the
+// next call decodes it at once instead of paying a raw load and a dependent
+// property gather -- two L2 round trips -- per span.  w < 0: nothing carried.
+struct SpanCursor {
+  int w = -1;
+  uint32_t lo, hi;                               // window w
+  uint64_t e;
+  int i2;
+  uint32_t nlo, nhi;                             // window w + 1
+  uint64_t ne;
+  int ni2;
+  uint32_t r0, r1, r2;                           // raw words of window w + 2
+  int mw = -1;                                   // letter-stop bitmap word mw (positions >= the last stop)
+  uint64_t mv;
+};
+
+// find_first_g with the cursor's bitmap word: the next span's start is
+// usually in the word the previous span stopped in (no slot read then).
+__device__ __forceinline__ int find_first_c(const uint64_t* m, int from, int L, const SpanCursor* cur) {
+  if (!cur) return find_first_g(m, from, L);
+  from = ufl(from);
+  if (from >= L) return L;
+  int w = from >> 6;
+  uint64_t x = (cur->mw == w ? cur->mv : ufl64(m[w])) & (~0ull << (from & 63));
+  for (;;) {
+    if (x) {
+      const int r = (w << 6) + __builtin_ctzll(x);
+      return r < L ? r : L;
+    }
+    ++w;
+    if ((w << 6) >= L) return L;
+    x = ufl64(m[w]);
+  }
+}
+
 // vec mode: omap receives map2original_'s MapBack per span text byte; hpos
 // (a rewritten HTML page, cld_html.hip) maps each byte of dv to its offset in
 // the page as given -- offsets in omap are always page offsets.
@@ -692,7 +731,8 @@ constexpr int kResumeRange = 1 << 30;           // next_span's *rlo: a range's l
 template <bool VEC = false, bool HB = false>
 LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t* lb, int& next, int& ulscript,
                          int& status, int lane, uint32_t* omap = nullptr, const uint32_t* hpos = nullptr,
-                         const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr, int* rlo = nullptr) {
+                         const uint32_t* hgap = nullptr, const uint64_t* lsm_ext = nullptr, int* rlo = nullptr,
+                         SpanCursor* cur = nullptr) {
   const uint64_t* const lsm = lsm_ext ? lsm_ext : S.lsm;
   lane = wave::lane_here();
   const int L = dv.len;
@@ -729,7 +769,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
   }
   const int soft = soft_of(remaining);
-  const int q = find_first_g(lsm, next, L);
+  const int q = find_first_c(lsm, next, L, cur);
   status = 1;
   if (q >= L) {
     next = L;
@@ -767,8 +807,23 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
   uint32_t r0 = 0, r1 = 0, r2 = 0, lo = 0, hi = 0, e2 = 0;
   uint64_t e = 0;
   int i2 = -1;
-  {
-    const int x0 = ((q >> 6) << 6) + lane;
+  // the carried pipeline (cur): window q >> 6 decoded from it at once, or its
+  // next window as the usual pipeline state; else a fresh start
+  const int w0 = q >> 6;
+  bool next_ready = false;
+  uint32_t nlo = 0, nhi = 0;
+  uint64_t ne = 0;
+  int ni2 = -1;
+  if (cur && cur->w == w0) {
+    lo = cur->lo; hi = cur->hi; e = cur->e; i2 = cur->i2;
+    nlo = cur->nlo; nhi = cur->nhi; ne = cur->ne; ni2 = cur->ni2;
+    r0 = cur->r0; r1 = cur->r1; r2 = cur->r2;
+    next_ready = true;
+  } else if (cur && cur->w >= 0 && cur->w + 1 == w0) {
+    lo = cur->nlo; hi = cur->nhi; e = cur->ne; i2 = cur->ni2;
+    r0 = cur->r0; r1 = cur->r1; r2 = cur->r2;
+  } else {
+    const int x0 = (w0 << 6) + lane;
     raw_load(dv, x0, r0, r1, r2);
     raw_bytes(dv, x0, r0, r1, r2, lo, hi);
     int i1;
@@ -776,21 +831,31 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     cp_gather<false>(T, i1, i2, e, e2);
     raw_load(dv, x0 + 64, r0, r1, r2);          // (guarded: nothing past the document is read)
   }
-  for (int w = q >> 6;; ++w) {
+  uint32_t slo = 0, shi = 0;                     // (cur) the decoded window's own state
+  uint64_t se = 0;
+  int si2 = -1;
+  for (int w = w0;; ++w) {
     const int x = (w << 6) + lane;
     uint32_t lw = 0, cw = 0;
     int cur_i2 = -1;                             // property index of the next character (cp_index)
     {
-      uint32_t lo1, hi1, e2n;
+      uint32_t lo1, hi1, e2n = 0;
       uint64_t en;
-      int j1, j2;
-      raw_bytes(dv, x + 64, r0, r1, r2, lo1, hi1);
-      cp_index(dv, x + 64, lo1, hi1, j1, j2);
-      cp_gather<false>(T, j1, j2, en, e2n);
-      raw_load(dv, x + 128, r0, r1, r2);
+      int j2;
+      if (next_ready) {                          // (carried: window w + 1 gathered, w + 2 loaded)
+        lo1 = nlo; hi1 = nhi; en = ne; j2 = ni2;
+        next_ready = false;
+      } else {
+        int j1;
+        raw_bytes(dv, x + 64, r0, r1, r2, lo1, hi1);
+        cp_index(dv, x + 64, lo1, hi1, j1, j2);
+        cp_gather<false>(T, j1, j2, en, e2n);
+        raw_load(dv, x + 128, r0, r1, r2);
+      }
       int ignore2 = 0;
       cw = cp_decode<false>(T, dv, x, lo, hi, e, e2, i2, lw, ignore2, ignore2, ignore2);
       cur_i2 = i2;
+      if (cur) { slo = lo; shi = hi; se = e; si2 = i2; }
       lo = lo1;
       hi = hi1;
       e = en;
@@ -881,13 +946,22 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     // kMaxScriptBytes + 1: the hard limit stops the span)
     if (lpos + 64 > kLB) {
       bad = 1;
+      if (cur) cur->w = -1;
       break;
     }
     if (stop < 64) {
+      if (cur) {                                 // the next span starts at or after this window
+        cur->mw = w;                             // (its letter stops at and after the stop: bit 20 of cw)
+        cur->mv = __ballot((cw >> 20) & 1);
+        cur->w = w;
+        cur->lo = slo; cur->hi = shi; cur->e = se; cur->i2 = si2;
+        cur->nlo = lo; cur->nhi = hi; cur->ne = e; cur->ni2 = i2;
+        cur->r0 = r0; cur->r1 = r1; cur->r2 = r2;
+      }
       const int xs = (w << 6) + stop;
       if ((Hm >> stop) & 1) {
         const int xe = xs + rdl(n, stop);
-        nxt = find_first_g(lsm, xe, L);
+        nxt = find_first_c(lsm, xe, L, cur);
         // after the hard limit the reference's gap scan keeps the last
         // letter's script: the first dropped '&' in the gap stops it
         if (HB && rlo && dv.hp) {
@@ -901,7 +975,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
           }
         }
       } else if ((Sm >> stop) & 1) {
-        nxt = find_first_g(lsm, xs, L);                               // the gap scan starts at the break char
+        nxt = find_first_c(lsm, xs, L, cur);                          // the gap scan starts at the break char
       } else {
         nxt = xs;                                                     // another script's letter stop
         // dropped '&'s right before it: after a letter of a third script (the
@@ -932,6 +1006,7 @@ LNG_NS_INL int next_span(const DevTables& T, const DocView& dv, Slot& S, uint8_t
     }
     if (evm) run = (Om >> topbit(evm)) & 1;
     if ((w << 6) + 64 >= L) {                                         // end of document
+      if (cur) cur->w = -1;
       if (run && wmax((uint32_t)(cutx + 1)) == 0) {                 // (a cut character brings its own)
         if (lane == 0) lb[lpos] = ' ';
         if (VEC && lane == 0) omap[lpos] = (uint32_t)dend;           // Insert(1) at the document end
@@ -2989,12 +3064,14 @@ __device__ __forceinline__ uint64_t st_spans(const DevTables& T, const DocView& 
   return kStNone;                                // (lab builds only: stage timing)
 #endif
   int next = 0, nsp = 0, cur = 0, rlo = -1;
+  SpanCursor sc;                                 // the span builder's pipeline, span to span
   for (;;) {
     if (cur + kLB > kLbdCap || nsp >= kMaxSpans) return kStNone;
     int ul = 0, st = 0;
     const int tb = dv.hp ? next_span<false, true>(T, dv, S, S.lbd + cur, next, ul, st, lane, nullptr, nullptr, nullptr,
                                                   nullptr, &rlo)
-                         : next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane);
+                         : next_span<false>(T, dv, S, S.lbd + cur, next, ul, st, lane, nullptr, nullptr, nullptr,
+                                            nullptr, nullptr, &sc);
     if (st == 0) break;
     if (st < 0) return kStNone;
     if (tb > 2048 && squeeze_trigger(S, S.lbd + cur, careful, lane)) return kStNone;   // the Squeeze restart
