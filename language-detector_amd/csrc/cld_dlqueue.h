@@ -8,10 +8,11 @@
 // whole queue and condition-variable handoffs, and the box's 16-CPU cgroup
 // quota then throttled it for tens of milliseconds at a time.  Here:
 //
-//  * callers push a request onto a lock-free stack (one CAS) and wait on a
-//    word of their own request: they spin briefly while few calls are in
-//    flight (a lone caller's round trip stays short), otherwise sleep on a
-//    futex at once;
+//  * a caller with no other call in flight runs its call itself (no handoff:
+//    a lone caller's round trip stays what it was); otherwise it pushes a
+//    request onto a lock-free stack (one CAS) and waits on a word of its own
+//    request, spinning briefly while few calls are in flight, else sleeping
+//    on a futex at once;
 //  * dispatcher threads (a few per GPU, one tiny slot each) take the whole
 //    stack with one exchange -- everything that arrived while they were busy
 //    becomes the next launch -- run it, write each request's result and wake
@@ -101,16 +102,19 @@ inline void finish_batch(DlReq* const* v, size_t n) {
 
 class DlQueue {
  public:
-  // Caller: enqueue; returns the number of calls in flight before this one.
-  int push(DlReq* r) {
-    const int before = inflight_.fetch_add(1);
+  // Caller: counts itself in (returns the calls in flight before it); then
+  // either runs its call itself (nothing else in flight) and leave()s, or
+  // push()es it.
+  int enter() { return inflight_.fetch_add(1); }
+  void leave() { inflight_.fetch_sub(1); }
+  // Caller (entered): enqueue.
+  void push(DlReq* r) {
     DlReq* h = head_.load();
     do r->next = h; while (!head_.compare_exchange_weak(h, r));
     if (sleepers_.load() > 0) {
       seq_.fetch_add(1);
       futex_wake(&seq_);
     }
-    return before;
   }
   // Dispatcher: blocks until a request is queued, then takes every queued
   // one, oldest first (linked through next).  Spins up to spin_us before

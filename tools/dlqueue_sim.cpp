@@ -88,7 +88,8 @@ int main(int argc, char** argv) {
         Res* res = new Res{0, 0};
         cld::DlReq* r = new cld::DlReq(p, len, res);
         const double a = now_s();
-        const int before = g_q.push(r);
+        const int before = g_q.enter();
+        g_q.push(r);
         r->wait(before < 16 ? cspin : 0);
         lat[c].push_back(now_s() - a);
         if (r->rc != 0 || res->p != reinterpret_cast<uintptr_t>(p) || res->len != len) wrong.fetch_add(1);
@@ -101,6 +102,7 @@ int main(int argc, char** argv) {
   for (int k = 0; k < nd; ++k) {                 // one stop request per dispatcher, each waited for
     Res res{0, 0};
     cld::DlReq r(nullptr, kStop, &res);
+    g_q.enter();
     g_q.push(&r);
     r.wait(0);
   }
