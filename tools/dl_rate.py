@@ -6,8 +6,9 @@ own per-document call (oracle/_ref/librefcld2.so, test infrastructure) on 1
 and 16 threads over the same documents.  One JSON line per run.
 
 Env: DL_RATE_CFG (c2 | c5, default both), DL_RATE_CALLERS (default 1,8,64,256),
-DL_RATE_VARIANTS (";"-separated runtime environments for A/B, e.g.
-"-;CLD_TINY_ZC=1;CLD_TINY=0", "-" = as is; default "-").
+DL_RATE_VARIANTS (";"-separated runtime environments for A/B, each one or more
+","-separated K=V, e.g. "-;CLD_TINY_ZC=1;CLD_LONG_SMALL=0,CLD_MI355X_CONTEXTS=4",
+"-" = as is; default "-").
 """
 import json
 import os
@@ -55,8 +56,9 @@ for cfg in os.environ.get("DL_RATE_CFG", "c2,c5").split(","):
     for var in os.environ.get("DL_RATE_VARIANTS", "-").split(";"):
         env = dict(os.environ)
         if var != "-":
-            k, v = var.split("=")
-            env[k] = v
+            for kv in var.split(","):
+                k, v = kv.split("=")
+                env[k] = v
         for callers in callers_list:
             calls = max(200, 20000 // callers)
             line = run([exe, "gpu", cb, co, str(callers), str(calls)], env=env)

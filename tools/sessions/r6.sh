@@ -6,6 +6,7 @@
 #   lines  C3/C4/C5 bench lines         prof   rocprofv3 kernel statistics, C2 and C3
 #   pmc    PMC passes (k_wave @ C2, k_long @ C3)
 #   dl     detect_language per-call rates (tools/dl_rate.py)
+#   dlc5   the same on C5 documents only, DLVARS runtime variants (A/B)
 #   req    request-sized batch rates (tools/req_rate.py)
 #   rates  HTML and vector-mode rates
 #   gpus2  bench.py --gpus 2 on this 1-GPU box: must refuse (exit 3), print no line
@@ -37,6 +38,7 @@ for s in ${STEPS:-suite smoke bench}; do
       step 400 pmc_c2.log bash tools/pmc_session.sh ${TAG}_pmc_c2 c2 k_wave
       step 400 pmc_c3.log bash tools/pmc_session.sh ${TAG}_pmc_c3 c3 "k_l(span|score|group|finish|rep|ong)" ;;
     dl) step 400 dl_rate.jsonl python3 tools/dl_rate.py ;;
+    dlc5) step 600 dl_c5_ab.jsonl env DL_RATE_CFG=c5 DL_RATE_CALLERS=${DLCALLERS:-1,8,64} DL_RATE_VARIANTS="${DLVARS:--}" python3 tools/dl_rate.py ;;
     ab)  # staged vs fused long-document path (A/B), C3 and C5 lines
       for c in ${ABCFG:-c3 c5}; do
         step 400 ab_${c}_staged.json python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-host --no-sub
