@@ -1099,8 +1099,16 @@ __device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, i
   const bool nc = valid && (b & 0xC0) != 0x80;
   const int n = utf8_len(b);
   bool mal = false;
-  if (nc)
+  if (nc) {
     for (int k = 1; k < n; ++k) mal |= (text[x + k] & 0xC0) != 0x80;
+  } else if (valid && x >= base + carry) {
+    // a continuation byte that no lead byte before it claims is a character
+    // of its own in the sequential decode (0x80-0xBF advance one byte): the
+    // walk takes the window (the carried bytes are checked below)
+    const uint32_t p1 = x >= 1 ? text[x - 1] : 0u, p2 = x >= 2 ? text[x - 2] : 0u, p3 = x >= 3 ? text[x - 3] : 0u;
+    const bool k1 = (p1 & 0xC0) == 0x80, k2 = (p2 & 0xC0) == 0x80;
+    mal = !(p1 >= 0xC0 || (k1 && p2 >= 0xE0) || (k1 && k2 && p3 >= 0xF0));
+  }
   const uint64_t ncm = __ballot(nc);
   const int end = min(base + 64, len);
   // well-formed window whose carried bytes (the tail of a character begun in
@@ -2270,8 +2278,12 @@ __device__ __forceinline__ int add_score(uint64_t a, uint32_t ps) {
   if ((uint32_t)((a >> 32) & 0xFF) == ps) r += (int)((a >> 40) & 0xFF);
   return r;
 }
-// ScriptScanner::MapBack (getonescriptspan.cc:1076-1078) for y in [0, text_bytes]
-__device__ __forceinline__ int vec_map_back(const VecState& V, int y) { return y < 0 ? 0 : (int)gld(V.vs->omap + y); }
+// ScriptScanner::MapBack (getonescriptspan.cc:1076-1078) for y <= text_bytes:
+// map2original_.MapBack(map2uplow_.MapBack(y)).  The inner MapBack of a
+// negative y is 0 (offsetmap.cc:430; a span whose lowercaser stopped early on
+// a malformed character has text_bytes < 1), and the outer one maps that to
+// the span's page offset, omap[0] -- not to 0.
+__device__ __forceinline__ int vec_map_back(const VecState& V, int y) { return (int)gld(V.vs->omap + (y < 0 ? 0 : y)); }
 __device__ __forceinline__ void vec_store(VecState& V, int lane) {
   if (lane == 0 && !V.over && V.n > 0) {
     cld_chunk c;
