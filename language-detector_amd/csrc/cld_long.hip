@@ -1446,7 +1446,9 @@ __device__ __forceinline__ int rep_words(Slot& S, const uint8_t* src, uint8_t* d
     if (dst != src)
       for (int k = lane; k < 48; k += 64) dst[len + k] = src[len + k];   // pads as they are (:758-767)
     gsync();
-    return len + carry;
+    // (a span whose lowercaser stopped early can have len < 1: the
+    // reference's loop then copies nothing and the span has 0 bytes)
+    return len > 0 ? len + carry : 0;
   }
   int dpos = 0;
   for (int w = 0; w < nw; ++w) {

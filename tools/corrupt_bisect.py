@@ -1,7 +1,7 @@
 """Shrinks a document on which cuda:0 and the oracle disagree: the shortest
 failing prefix, then the shortest failing suffix of that, then single-byte
 deletions until none still fails (each round one GPU batch of all candidates).
-Usage: corrupt_bisect.py DOC.bin [OUT.bin]"""
+Usage: [BISECT_MODE=vec] corrupt_bisect.py DOC.bin [OUT.bin]"""
 import os
 import sys
 
@@ -18,8 +18,25 @@ cld_amd.init_device(0, tables=cld_amd.SYNTH_TABLES)
 o = Oracle()
 
 
+VEC = os.environ.get("BISECT_MODE", "plain") == "vec"    # cld_detect_batch_vec: result fields and the vector
+
+
 def failing(docs):
     buf, offs = cld_amd.pack(docs)
+    if VEC:
+        got, chunks, coffs = cld_amd.detect_batch_vec(buf=buf, offsets=offs)
+        bad = np.zeros(len(docs), bool)
+        ref = []
+        for i, d in enumerate(docs):
+            r, ch = o.detect_vec(d)
+            ref.append((r.summary_lang, list(r.lang3), list(r.percent3), r.text_bytes, list(r.normalized3),
+                        [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in ch]))
+            g = got[i]
+            mine = (int(g["summary_lang"]), [int(x) for x in g["lang3"]], [int(x) for x in g["percent3"]],
+                    int(g["text_bytes"]), [float(x) for x in g["normalized3"]],
+                    [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in chunks[coffs[i]:coffs[i + 1]]])
+            bad[i] = mine != ref[-1]
+        return bad, got, ref
     got = cld_amd.detect_batch(buf=buf, offsets=offs)
     ref = o.detect_batch(buf, offs, threads=8)
     bad = np.zeros(len(docs), bool)
