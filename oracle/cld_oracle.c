@@ -1169,11 +1169,14 @@ static void tote_top3(const tote_t* t, int* key3) {
     m >>= 1; base += 4;
   }
 }
-/* GetScore(-1) would read the word before score_[] (tote.h:53-58); it is
- * unreachable because every chunk holds >= 1 langprob with top1 != 0.
- * Report it loudly instead of guessing. */
+/* GetScore(-1) reads the uint16 before score_[] (tote.h:52-58): the high
+ * half of the int score_count_ (in_use_mask_ at 0, byte_count_ at 8,
+ * score_count_ at 12, the union at 16; little-endian), 0 for any count below
+ * 65536.  A chunk whose tote stays empty gets there: ScoreAsQuads on text
+ * whose spans score no langprob (malformed bytes, tests/test_gpu_corrupt.py);
+ * the GPU takes 0 as well. */
 static int tote_score(const tote_t* t, int key) {
-  if (key < 0) { fprintf(stderr, "cld_oracle: tote_score(-1) reached\n"); abort(); }
+  if (key < 0) return t->score_count >= 65536 ? (t->score_count >> 16) & 0xFFFF : 0;
   return t->score[key];
 }
 

@@ -59,6 +59,14 @@ def test_corrupted_documents_plain(gpu, oracle, seed):
     assert_same(got, oracle.detect_batch(buf, offs, threads=16), "corrupted, plain (seed %d)" % seed)
 
 
+@pytest.mark.parametrize("flags", [0x100, 0x4100])      # kCLDFlagScoreAsQuads, with kCLDFlagBestEffort
+def test_corrupted_documents_flags(gpu, oracle, flags):
+    docs = docs_for(20, 3000)                             # (seed 20 reached GetScore(-1): an empty chunk tote)
+    buf, offs = gpu.pack(docs)
+    got = gpu.detect_batch(buf=buf, offsets=offs, flags=flags)
+    assert_same(got, oracle.detect_batch_ex(buf, offs, flags=flags, threads=16), "corrupted, flags %#x" % flags)
+
+
 def test_corrupted_documents_html(gpu, oracle):
     docs = docs_for(13, 1200)
     pages = [b"<p>" + d.replace(b" ", b" <b>x</b> ", 2) + b" &eacute;t&eacute; &#x1F600;</p>" for d in docs]
