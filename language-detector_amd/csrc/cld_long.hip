@@ -250,7 +250,8 @@ __device__ __forceinline__ void mark_sub(SM& s, int lane, int stage, long long& 
   }
 }
 
-// Debug dump records (u32 words): 'S' span {ul, tb, pass}; 'R' round {off, next,
+// Debug dump records (u32 words): 'S' span {ul, tb, pass} and 'T' its text
+// {tb, bytes packed}; 'R' round {off, next,
 // nb, nd, nx, then nb+nd+nx (offset, indirect) pairs}; 'C' chunk {lo, hi, lang1,
 // lang2, score1, score2, grams, rel_delta, rel_score}.
 template <class SM>
@@ -259,6 +260,28 @@ __device__ void dbg_words(SM& s, int lane, const uint32_t* v, int n) {
   if (lane == 0) {
     for (int i = 0; i < n; ++i) s.dbg[1 + s.dbg_pos + i] = v[i];
     s.dbg_pos += n;
+    s.dbg[0] = s.dbg_pos;
+  }
+  wave::wsync();
+}
+
+// 'T' record: a span's text as scored (after Squeeze / Repeats), tb bytes
+// packed four to a word.
+template <class SM>
+__device__ void dbg_text(SM& s, int lane, const uint8_t* text, int tb) {
+  if (!s.dbg) return;
+  const int n = tb > 0 ? (tb + 3) >> 2 : 0;
+  uint32_t* o = s.dbg + 1 + s.dbg_pos;
+  if (lane == 0) { o[0] = 'T'; o[1] = (uint32_t)tb; }
+  for (int i = lane; i < n; i += 64) {
+    uint32_t w = 0;
+    for (int k = 0; k < 4; ++k)
+      if (4 * i + k < tb) w |= (uint32_t)text[4 * i + k] << (8 * k);
+    o[2 + i] = w;
+  }
+  wave::wsync();
+  if (lane == 0) {
+    s.dbg_pos += 2 + n;
     s.dbg[0] = s.dbg_pos;
   }
   wave::wsync();
@@ -1119,6 +1142,8 @@ __device__ __forceinline__ uint64_t char_starts(const uint8_t* text, int base, i
       const int last = base + topbit(ncm);
       const int q = last + utf8_len(ufl(text[last]));
       carry = q > end ? q - end : 0;
+    } else {                                      // no start here: the carried character ends in this window
+      carry = base + carry > end ? base + carry - end : 0;   // (or runs past the text's end)
     }
     return ncm;
   }
@@ -2956,6 +2981,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         if constexpr (D) {
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
+          dbg_text(s, lane, s.text, tb);
         }
         WinOf<SEQ> win{nullptr, 0, 16 * n16, 16 * n16};                   // the whole span is in s.text
         ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);
@@ -2973,6 +2999,7 @@ __device__ __forceinline__ int detect(const DevTables& T, const uint8_t* g, int 
         if constexpr (D) {
           const uint32_t v[4] = {'S', (uint32_t)ul, (uint32_t)tb, (uint32_t)pass};
           dbg_words(s, lane, v, 4);
+          dbg_text(s, lane, text, tb);
         }
         WinOf<SEQ> win{text, 0, 0, (tb + 48 + 15) & ~15};                // windows of it go to s.text (SEQ: read in place)
         ok = score_span<D, VEC>(T, S, s, win, tb, ul, lane, tr, doc, cflags, V);

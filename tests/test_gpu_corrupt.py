@@ -9,6 +9,8 @@ Every routing path sees them: k_wave, the staged span kernels, the fused
 k_long and its sequential span source.  The reference itself is no judge here:
 it reads past its tables on such bytes and segfaults on random ones.
 Needs an MI355X."""
+import os
+
 import numpy as np
 import pytest
 
@@ -82,3 +84,21 @@ def test_corrupted_documents_vector(gpu, oracle):
     docs = docs_for(14, 1200)
     buf, offs = gpu.pack(docs)
     vec_check(gpu, oracle, buf, offs, "corrupted, vector")
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "corrupt")
+
+
+def test_shrunk_regressions(gpu, oracle):
+    """The documents the sweeps shrank (tools/corrupt_bisect.py), one per fixed
+    difference: an orphan continuation byte in a Repeats span; a span with
+    text_bytes < 1 in vector mode; a character that ends in the first byte of
+    a window with no character start (the carry was kept); an empty chunk tote
+    under ScoreAsQuads.  Plain with both flags, and vector mode."""
+    docs = [open(os.path.join(GOLDEN, f), "rb").read() for f in sorted(os.listdir(GOLDEN))]
+    assert len(docs) == 4
+    buf, offs = gpu.pack(docs)
+    for flags in (0, 0x100):
+        got = gpu.detect_batch(buf=buf, offsets=offs, flags=flags)
+        assert_same(got, oracle.detect_batch_ex(buf, offs, flags=flags), "shrunk regressions, flags %#x" % flags)
+    vec_check(gpu, oracle, buf, offs, "shrunk regressions, vector")

@@ -47,6 +47,34 @@ def failing(docs):
 
 d = open(sys.argv[1], "rb").read()
 assert failing([d])[0][0], "the document does not fail"
+# long documents: binary search for a failing prefix, then suffix, first (one document per step)
+while len(d) > 4096:
+    n0 = len(d)
+    lo, hi = 0, len(d)                         # d[:hi] fails
+    while hi - lo > 64:
+        mid = (lo + hi) // 2
+        if failing([d[:mid]])[0][0]:
+            hi = mid
+        else:
+            lo = mid
+    d = d[:hi]
+    lo, hi = 0, len(d)                         # d[lo:] fails
+    while hi - lo > 64:
+        mid = (lo + hi) // 2
+        if failing([d[mid:]])[0][0]:
+            lo = mid
+        else:
+            hi = mid
+    d = d[lo:]
+    # then blocks of 1/16 of it at a time
+    bs = max(64, len(d) // 16)
+    cands = [d[:k] + d[k + bs:] for k in range(0, len(d), bs)]
+    ks = np.nonzero(failing(cands)[0])[0]
+    if len(ks):
+        d = cands[ks[0]]
+    print("long: %d bytes" % len(d), flush=True)
+    if len(d) >= n0:
+        break
 # shortest failing prefix, then suffix
 for side in ("prefix", "suffix"):
     cands = [d[:k] for k in range(1, len(d) + 1)] if side == "prefix" else [d[k:] for k in range(len(d))]

@@ -33,6 +33,8 @@ def gpu_dump(doc):
         elif t == ord('C'):
             v = [int(x) for x in w[i + 1:i + 18]]; i += 18
             recs.append(("C", v))
+        elif t == ord('T'):
+            tb = int(np.int32(np.uint32(w[i + 1]))); i += 2 + (max(tb, 0) + 3) // 4
         else:
             raise ValueError("bad record %d at %d" % (t, i))
     return recs

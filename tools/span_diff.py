@@ -20,11 +20,14 @@ st = cld_amd.last_stats(0)
 print("gpu", got[0], "long", st.long_docs, "seq", st.general_docs, "passes", list(st.passes), flush=True)
 w = np.fromfile(os.environ["CLD_DEBUG_OUT"], dtype=np.uint32)
 n, w, i = int(w[0]), w[1:], 0
-spans = []
+spans, texts = [], []
 while i < n:
     t = int(w[i])
     if t == ord('S'):
         spans.append(tuple(int(x) for x in w[i + 1:i + 4])); i += 4
+    elif t == ord('T'):
+        tb = int(np.int32(np.uint32(w[i + 1]))); nw = (max(tb, 0) + 3) // 4
+        texts.append(w[i + 2:i + 2 + nw].astype("<u4").tobytes()[:max(tb, 0)]); i += 2 + nw
     elif t == ord('R'):
         nb, nd, nx = (int(x) for x in w[i + 3:i + 6]); i += 6 + 2 * (nb + nd + nx)
     elif t == ord('C'):
@@ -38,3 +41,8 @@ for k in range(max(len(spans), len(ospans))):
     a = spans[k] if k < len(spans) else None
     b = ospans[k] if k < len(ospans) else None
     print(k, a, b)
+out = os.environ.get("SPAN_TEXT_OUT")
+if out:                                           # the GPU's scored span texts, for replay on the CPU
+    with open(out, "wb") as f:
+        for x in texts:
+            f.write(len(x).to_bytes(4, "little") + x)
