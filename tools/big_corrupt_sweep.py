@@ -23,7 +23,7 @@ o = Oracle(tables=tables)
 out_dir = os.path.join(ROOT, "gpurun_out", "corrupt_diag")
 os.makedirs(out_dir, exist_ok=True)
 total = 0
-for seed in (60, 61):
+for seed in (int(x) for x in os.environ.get("BIG_SEEDS", "60,61").split(",")):
     rng = np.random.default_rng(seed)
     b3, o3 = corpus.c3(200, seed=seed)
     b5, o5 = corpus.c5(4000, seed=seed)

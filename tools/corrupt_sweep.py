@@ -1,6 +1,7 @@
 """Wider corruption sweep than tests/test_gpu_corrupt.py, for the GPU box:
 many seeds of the corrupted corpora (tests/test_gpu_corrupt.docs_for) in
-plain mode with each CLD2 flag set, HTML mode, and vector mode, against the
+plain mode with each CLD2 flag set, with random CLDHints, HTML mode, and
+vector mode, against the
 oracle; prints the mismatch count per leg and saves the first mismatching
 documents under gpurun_out/corrupt_diag/ (tools/corrupt_bisect.py shrinks
 them).  SWEEP_SEEDS (default 20-27)."""
@@ -15,7 +16,7 @@ for p in ("language-detector_amd", "oracle", "tests"):
 import cld_amd  # noqa: E402
 from oracle import Oracle  # noqa: E402
 import test_gpu_corrupt as tc  # noqa: E402
-from test_gpu_html_hints import priors_for  # noqa: E402
+from test_gpu_html_hints import priors_for, random_hints  # noqa: E402
 from test_gpu_vector import vecs, oracle_vecs  # noqa: E402
 
 FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
@@ -51,6 +52,15 @@ for seed in seeds:
         total += len(idx)
         save("sw_s%d_f%x" % (seed, flags), docs, idx)
         print("seed %d flags %#x: %d docs, %d mismatches %s" % (seed, flags, n, len(idx), idx[:5]), flush=True)
+    hints = random_hints(cld_amd, n, seed=seed)         # CLDHints (tld, content-language, encoding, language)
+    got = cld_amd.detect_batch_ex(buf=buf, offsets=offs, hints=hints)
+    pr = priors_for(cld_amd, buf, offs, False, hints)
+    ref = o.detect_batch_ex(buf, offs, priors=pr, threads=16)
+    idx = diff(got, ref, n)
+    total += len(idx)
+    save("sw_s%d_hints" % seed, docs, idx)
+    print("seed %d hints: %d docs (%d hinted), %d mismatches %s" % (seed, n, int((pr != 0).any(axis=1).sum()),
+                                                                   len(idx), idx[:5]), flush=True)
     pages = [b"<p>" + d.replace(b" ", b" <b>x</b> ", 2) + b" &amp;&#233;</p>" for d in docs[:2500]]
     pb, po = cld_amd.pack(pages)
     got = cld_amd.detect_batch_ex(buf=pb, offsets=po, html=True)
