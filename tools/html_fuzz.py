@@ -3,7 +3,8 @@ benchmark corpora and HTML fragments -- tags, unterminated tags, comments,
 script/style blocks, entities (named, numeric, broken), lang attributes and
 content-language metas, stray '<' '>' '&', malformed UTF-8 -- through
 cld_detect_batch_ex (HTML mode) and cld_detect_batch_vec (html=True) against
-the oracle with the product's hint priors.  FUZZ_SEEDS (default 40-45)."""
+the oracle with the product's hint priors, or (HTML_REF=1, valid UTF-8 only)
+against the reference CLD2 itself.  FUZZ_SEEDS (default 40-45)."""
 import os
 import sys
 
@@ -26,6 +27,13 @@ FRAG = [b"<p>", b"</p>", b"<b>", b"</b>", b"<br/>", b"<!-- c -->", b"<!--", b"--
         b"<meta http-equiv=\"content-language\" content=\"es\">", b"<title>t</title>", b"<img alt=\"x\">",
         b"<div lang=ja>", b"</div>", b"<unclosed", b"\"", b"'", b"\xc3", b"\x80", b"\xf0\x9f\x98\x80", b"\xe2\x80\x8b",
         b"\xff", b"\n", b"\t", b" "]
+# HTML_REF=1: valid UTF-8 only, and the reference CLD2 itself (its own HTML
+# scanner and hint code) is the judge instead of the oracle
+REF = os.environ.get("HTML_REF") == "1"
+if REF:
+    import refcld  # noqa: E402
+    FRAG = [f for f in FRAG if f not in (b"\xc3", b"\x80", b"\xff")]
+    ref_cld = refcld.instance(cld_amd.SYNTH_TABLES)
 out_dir = os.path.join(ROOT, "gpurun_out", "corrupt_diag")
 os.makedirs(out_dir, exist_ok=True)
 cld_amd.init_device(0, tables=cld_amd.SYNTH_TABLES)
@@ -50,11 +58,14 @@ for seed in (int(s) for s in os.environ.get("FUZZ_SEEDS", "40,41,42,43,44,45").s
     n = len(pages)
     got = cld_amd.detect_batch_ex(buf=buf, offsets=offs, html=True)
     st = cld_amd.last_stats(0)
-    pr = priors_for(cld_amd, buf, offs, True, None)
-    ref = o.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=16)
+    if REF:
+        ref = ref_cld.detect_batch(buf, offs, plain=np.zeros(n, np.uint8), threads=16)
+    else:
+        pr = priors_for(cld_amd, buf, offs, True, None)
+        ref = o.detect_batch_ex(buf, offs, plain=np.zeros(n, np.uint8), priors=pr, threads=16)
     bad = np.zeros(n, bool)
     for f in FIELDS:
-        bad |= (got[f] != ref[f]).reshape(n, -1).any(axis=1)
+        bad |= (got[f].astype(np.float64) != ref[f].astype(np.float64)).reshape(n, -1).any(axis=1)
     idx = np.nonzero(bad)[0]
     total += len(idx)
     for i in idx[:3]:
@@ -66,9 +77,17 @@ for seed in (int(s) for s in os.environ.get("FUZZ_SEEDS", "40,41,42,43,44,45").s
     vb, vo = cld_amd.pack(vp)
     g, chunks, coffs = cld_amd.detect_batch_vec(buf=vb, offsets=vo, html=True)
     gv = vecs(chunks, coffs)
-    rr, ov = oracle_vecs(o, cld_amd, vb, vo, html=True)
-    vidx = [i for i in range(len(vp)) if gv[i] != ov[i] or (int(g[i]["summary_lang"]), list(g[i]["percent3"]),
-            int(g[i]["text_bytes"])) != (rr[i].summary_lang, list(rr[i].percent3), rr[i].text_bytes)]
+    if REF:
+        vidx = []
+        for i in range(len(vp)):
+            rb, cb = ref_cld.detect_vec(vp[i], plain=False)
+            if gv[i] != [(int(c["offset"]), int(c["bytes"]), int(c["lang1"])) for c in cb] or \
+                    int(g[i]["summary_lang"]) != int(rb["summary_lang"]) or int(g[i]["text_bytes"]) != int(rb["text_bytes"]):
+                vidx.append(i)
+    else:
+        rr, ov = oracle_vecs(o, cld_amd, vb, vo, html=True)
+        vidx = [i for i in range(len(vp)) if gv[i] != ov[i] or (int(g[i]["summary_lang"]), list(g[i]["percent3"]),
+                int(g[i]["text_bytes"])) != (rr[i].summary_lang, list(rr[i].percent3), rr[i].text_bytes)]
     total += len(vidx)
     for i in vidx[:3]:
         with open(os.path.join(out_dir, "htmlvec_s%d_d%d.bin" % (seed, i)), "wb") as f:
