@@ -692,6 +692,19 @@ uint32_t small_long_list(const Device* d) {
   static const long v = getenv("CLD_LONG_SMALL") ? atol(getenv("CLD_LONG_SMALL")) : -1;
   return v >= 0 ? (uint32_t)v : 64u;
 }
+// ...unless it holds a document of CLD_LONG_SMALL_KB KB or more (default 0:
+// no such rule).  A page that long may hold thousands of spans, which one
+// fused wave scores in tens of milliseconds (a 64 KB page of 3,082 spans:
+// 44-48 ms) where the staged path splits them into span-parallel groups.
+// detect_language on C5 documents (profiles/round6_dl_rate_c5_heavy_ab.jsonl),
+// 32 KB against off: the slowest call 45-48 -> 24-29 ms, p99 at 64 callers
+// 20 -> 17 ms, but 8 callers 11.3K -> 10.8K docs/s (the few-span 32-64 KB
+// pages lose the fused kernel's two-wave speculation) -- a tail-latency
+// option, not the default.
+uint64_t small_list_heavy_bytes() {
+  static const long v = getenv("CLD_LONG_SMALL_KB") ? atol(getenv("CLD_LONG_SMALL_KB")) : 0;
+  return v > 0 ? (uint64_t)v << 10 : ~0ull;
+}
 
 // Batches holding a document of this many KB go to the fused k_long whole
 // (CLD_LONG_HEAVY_KB; default 0: never).  Before span-parallel scoring a C5
@@ -801,9 +814,12 @@ int enqueue(Device* d, const uint8_t* buf, const uint64_t* offs, size_t n, cld_r
       if (grow(&d->d_parlists, &d->parlists_cap, 2 * np + 4 * gcap)) return CLD_ENOMEM;
       // a list of at most small_long_list() documents (64) goes whole to the
       // fused kernel: small batches keep its two-wave speculation (section 6)
+      // (the host's count says the list is longer than that, or holds a
+      // document of small_list_heavy_bytes() or more: no list goes whole)
+      const uint32_t small_total = long_hint > (int64_t)small_long_list(d) ? 0u : small_long_list(d);
       HIP_OK(cld_launch_staged(d->d_T, buf, offs, list, out, d->d_slots, d->st_waves, d->d_store, d->store_bytes,
                                d->d_meta, d->d_stlists, d->d_stlists + c, fall, ctr, cflags, special,
-                               priors, hbuf, hflag, hpos, hgap, d->fault_doc, small_long_list(d),
+                               priors, hbuf, hflag, hpos, hgap, d->fault_doc, small_total,
                                d->long_order ? d->d_lhist : nullptr, heavy_kb(), d->d_parlists, np, gcap, s));
       list = fall;
       ctr_total = kCtrStFall;
@@ -1178,10 +1194,11 @@ int run_host_stream(Device* d, const uint8_t* buf, const uint64_t* offs, size_t 
     {
       const int64_t lim = (int64_t)small_long_list(d);
       const uint64_t* o = offs + a;
+      const uint64_t heavy = small_list_heavy_bytes();
       for (size_t i = 0; i < m && long_hint <= lim; ++i) {
         const uint64_t len = o[i + 1] - o[i];
         long_hint += len > (uint64_t)kWaveCap;
-        if (len > kLongDocCap - 64) long_hint = lim + 1;
+        if (len > kLongDocCap - 64 || len >= heavy) long_hint = lim + 1;
       }
     }
     if (flags & kPrepFlags) {
