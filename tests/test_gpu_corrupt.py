@@ -27,9 +27,9 @@ BAD = [b"\x80", b"\xbf", b"\x80\x80\x80", b"\xc3", b"\xe4\xb8", b"\xf0\x9f\x98",
        b"\xc2\xa0", b"\xe3\x80\x80"]
 
 
-def corrupt(rng, d):
+def corrupt(rng, d, max_bad=7):
     d = bytearray(d)
-    for _ in range(int(rng.integers(0, 7))):
+    for _ in range(int(rng.integers(0, max_bad))):
         p = int(rng.integers(0, len(d) + 1))
         k = int(rng.integers(3))
         if k == 0:                                        # splice a bad sequence in
@@ -41,12 +41,12 @@ def corrupt(rng, d):
     return bytes(d)
 
 
-def docs_for(seed, n_each, random_docs=True):
+def docs_for(seed, n_each, random_docs=True, max_bad=7):
     rng = np.random.default_rng(seed)
     docs = []
     for cfg, n in (("c2", n_each), ("c3", max(8, n_each // 40)), ("c4", n_each // 2), ("c5", n_each)):
         b, o = corpus.GENERATORS[cfg](n, seed=seed)
-        docs += [corrupt(rng, bytes(b[o[i]:o[i + 1]])) for i in range(n)]
+        docs += [corrupt(rng, bytes(b[o[i]:o[i + 1]]), max_bad) for i in range(n)]
     for _ in range(n_each // 10 if random_docs else 0):   # random bytes, 0-3000 of them
         docs.append(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes())
     order = rng.permutation(len(docs))

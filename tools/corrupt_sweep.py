@@ -22,8 +22,11 @@ from test_gpu_vector import vecs, oracle_vecs  # noqa: E402
 FIELDS = ("lang3", "summary_lang", "percent3", "is_reliable", "text_bytes", "normalized3")
 out_dir = os.path.join(ROOT, "gpurun_out", "corrupt_diag")
 os.makedirs(out_dir, exist_ok=True)
-cld_amd.init_device(0, tables=cld_amd.SYNTH_TABLES)
-o = Oracle()
+# SWEEP_TABLES=q0: the shipped Q0 tables on both sides; SWEEP_MAX_BAD: splices per document (7)
+tables = cld_amd.Q0_TABLES if os.environ.get("SWEEP_TABLES") == "q0" else cld_amd.SYNTH_TABLES
+max_bad = int(os.environ.get("SWEEP_MAX_BAD", "7"))
+cld_amd.init_device(0, tables=tables)
+o = Oracle(tables=tables)
 
 
 def diff(got, ref, n):
@@ -42,7 +45,7 @@ def save(tag, docs, idx):
 total = 0
 seeds = [int(s) for s in os.environ.get("SWEEP_SEEDS", "20,21,22,23,24,25,26,27").split(",")]
 for seed in seeds:
-    docs = tc.docs_for(seed, 3000)
+    docs = tc.docs_for(seed, 3000, max_bad=max_bad)
     buf, offs = cld_amd.pack(docs)
     n = len(docs)
     for flags in (0, 0x100, 0x4000, 0x4100):
